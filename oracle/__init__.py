@@ -1,0 +1,5 @@
+"""ORACLE — test infrastructure only (CPU restatement of the reference hot path).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+Never imported by the product package (ducosy-gan_amd/).
+"""
