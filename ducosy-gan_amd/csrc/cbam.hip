@@ -1,0 +1,457 @@
+// CBAM tail of ResidualBlockWithCBAM (modules/model.py:6-52, 68-87) on NHWC fp32:
+//   z = IN(y);  ca = sigmoid(fc(avgpool z) + fc(maxpool z));  zc = z*ca
+//   s = [mean_c zc, max_c zc];  sa = sigmoid(conv7x7(s));  out = x + zc*sa
+// avgpool(IN(y)) is identically 0 (IN output has zero mean per (n,c)), so the avg branch is
+// evaluated on exact zeros: it contributes fc(0) = 0 forward and exactly 0 gradient.
+// maxpool(IN(y)) = IN(max y) because the IN scale is positive, so the max comes from the
+// statistics pass over y.  Channel reductions use one wave64 per pixel (channels on lanes,
+// float4 per lane, xor-shuffle reductions).
+#include "common.hpp"
+
+namespace dcs {
+
+// ---- channel attention MLP (one block per image) ----------------------------------------
+__global__ __launch_bounds__(256) void ca_forward_kernel(const float* __restrict__ ymax, const float* __restrict__ sc,
+                                                         const float* __restrict__ sh, const float* __restrict__ w1,
+                                                         const float* __restrict__ w2, int C, int Cr,
+                                                         float* __restrict__ ca) {
+    extern __shared__ float sm[];
+    float* vmax = sm;          // [C]
+    float* h = sm + C;         // [Cr] relu(W1 vmax)
+    float* h0 = h + Cr;        // [Cr] relu(W1 * 0)
+    const int n = blockIdx.x, tid = threadIdx.x;
+    for (int c = tid; c < C; c += blockDim.x) vmax[c] = fmaf(ymax[n * C + c], sc[n * C + c], sh[n * C + c]);
+    __syncthreads();
+    for (int j = tid; j < Cr; j += blockDim.x) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a = fmaf(w1[j * C + c], vmax[c], a);
+        h[j] = a > 0.f ? a : 0.f;
+        h0[j] = 0.f;  // relu(W1 * avgpool(IN(y))) with avgpool == 0
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += blockDim.x) {
+        float oa = 0.f, om = 0.f;
+        for (int j = 0; j < Cr; ++j) {
+            oa = fmaf(w2[c * Cr + j], h0[j], oa);
+            om = fmaf(w2[c * Cr + j], h[j], om);
+        }
+        ca[n * C + c] = sigmoidf_(oa + om);
+    }
+}
+
+// ---- spatial attention input: per pixel mean/max over channels of zc ---------------------
+__global__ __launch_bounds__(256) void sa_reduce_kernel(const float* __restrict__ y, const float* __restrict__ sc,
+                                                        const float* __restrict__ sh, const float* __restrict__ ca,
+                                                        int HW, int C, long long P, float* __restrict__ sin_,
+                                                        int* __restrict__ sarg) {
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= P) return;
+    const int n = (int)(p / HW);
+    const float* yp = y + p * C;
+    const float* s = sc + (long long)n * C;
+    const float* b = sh + (long long)n * C;
+    const float* a = ca + (long long)n * C;
+    float sum = 0.f, mx = -INFINITY;
+    int am = 0;
+    for (int c4 = lane; c4 < C / 4; c4 += 64) {
+        float4 v = reinterpret_cast<const float4*>(yp)[c4];
+        float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int c = c4 * 4 + q;
+            float zc = fmaf(e[q], s[c], b[c]) * a[c];
+            sum += zc;
+            if (zc > mx) { mx = zc; am = c; }
+        }
+    }
+    sum = wave_sum(sum);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float om = __shfl_xor(mx, o, 64);
+        int oa = __shfl_xor(am, o, 64);
+        if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    if (lane == 0) {
+        sin_[p * 2 + 0] = sum / (float)C;
+        sin_[p * 2 + 1] = mx;
+        sarg[p] = am;
+    }
+}
+
+// ---- spatial attention conv + sigmoid + scale + residual add (wave per pixel) ------------
+__global__ __launch_bounds__(256) void sa_apply_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                       const float* __restrict__ sc, const float* __restrict__ sh,
+                                                       const float* __restrict__ ca, const float* __restrict__ sin_,
+                                                       const float* __restrict__ wsa, int H, int W, int C, int ksa,
+                                                       long long P, float* __restrict__ sa,
+                                                       float* __restrict__ out) {
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= P) return;
+    const int HW = H * W;
+    const int n = (int)(p / HW);
+    const int rem = (int)(p - (long long)n * HW);
+    const int py = rem / W, px = rem - py * W;
+    const int r = ksa / 2, taps = ksa * ksa;
+    float pre = 0.f;
+    for (int t = lane; t < 2 * taps; t += 64) {
+        int ch = t / taps, tt = t - ch * taps;
+        int ty = tt / ksa, tx = tt - ty * ksa;
+        int yy = py + ty - r, xx = px + tx - r;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+            pre = fmaf(wsa[t], sin_[((long long)n * HW + yy * W + xx) * 2 + ch], pre);
+    }
+    pre = wave_sum(pre);
+    const float g = sigmoidf_(pre);
+    if (lane == 0) sa[p] = g;
+    const float* s = sc + (long long)n * C;
+    const float* b = sh + (long long)n * C;
+    const float* a = ca + (long long)n * C;
+    for (int c4 = lane; c4 < C / 4; c4 += 64) {
+        float4 v = reinterpret_cast<const float4*>(y + p * C)[c4];
+        float4 xv = reinterpret_cast<const float4*>(x + p * C)[c4];
+        int c = c4 * 4;
+        float4 o;
+        o.x = xv.x + fmaf(v.x, s[c + 0], b[c + 0]) * a[c + 0] * g;
+        o.y = xv.y + fmaf(v.y, s[c + 1], b[c + 1]) * a[c + 1] * g;
+        o.z = xv.z + fmaf(v.z, s[c + 2], b[c + 2]) * a[c + 2] * g;
+        o.w = xv.w + fmaf(v.w, s[c + 3], b[c + 3]) * a[c + 3] * g;
+        reinterpret_cast<float4*>(out + p * C)[c4] = o;
+    }
+}
+
+// ---- backward ---------------------------------------------------------------------------
+// b1: dpre[p] = (sum_c dout*zc) * sa*(1-sa)
+__global__ __launch_bounds__(256) void cb_bwd_dsa_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                         const float* __restrict__ sc, const float* __restrict__ sh,
+                                                         const float* __restrict__ ca, const float* __restrict__ sa,
+                                                         int HW, int C, long long P, float* __restrict__ dpre) {
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= P) return;
+    const int n = (int)(p / HW);
+    const float* s = sc + (long long)n * C;
+    const float* b = sh + (long long)n * C;
+    const float* a = ca + (long long)n * C;
+    float acc = 0.f;
+    for (int c4 = lane; c4 < C / 4; c4 += 64) {
+        float4 v = reinterpret_cast<const float4*>(y + p * C)[c4];
+        float4 d = reinterpret_cast<const float4*>(dout + p * C)[c4];
+        int c = c4 * 4;
+        acc = fmaf(d.x, fmaf(v.x, s[c + 0], b[c + 0]) * a[c + 0], acc);
+        acc = fmaf(d.y, fmaf(v.y, s[c + 1], b[c + 1]) * a[c + 1], acc);
+        acc = fmaf(d.z, fmaf(v.z, s[c + 2], b[c + 2]) * a[c + 2], acc);
+        acc = fmaf(d.w, fmaf(v.w, s[c + 3], b[c + 3]) * a[c + 3], acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+        float g = sa[p];
+        dpre[p] = acc * g * (1.f - g);
+    }
+}
+
+// b2: dsin[q][ch] = sum_t wsa[ch][t] * dpre[q - (t - r)]  (adjoint of the zero-padded conv)
+__global__ void cb_bwd_dsin_kernel(const float* __restrict__ dpre, const float* __restrict__ wsa, int H, int W, int ksa,
+                                   long long P, float* __restrict__ dsin) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    const int HW = H * W;
+    const int n = (int)(q / HW);
+    const int rem = (int)(q - (long long)n * HW);
+    const int qy = rem / W, qx = rem - qy * W;
+    const int r = ksa / 2, taps = ksa * ksa;
+    float a0 = 0.f, a1 = 0.f;
+    for (int ty = 0; ty < ksa; ++ty) {
+        int yy = qy - ty + r;
+        if (yy < 0 || yy >= H) continue;
+        for (int tx = 0; tx < ksa; ++tx) {
+            int xx = qx - tx + r;
+            if (xx < 0 || xx >= W) continue;
+            float d = dpre[(long long)n * HW + yy * W + xx];
+            a0 = fmaf(wsa[ty * ksa + tx], d, a0);
+            a1 = fmaf(wsa[taps + ty * ksa + tx], d, a1);
+        }
+    }
+    dsin[q * 2 + 0] = a0;
+    dsin[q * 2 + 1] = a1;
+}
+
+// dwsa partials: grid (2*taps, nchunk); part[chunk][t] = sum_{p in chunk} dpre[p]*sin[p+t-r][ch]
+__global__ __launch_bounds__(256) void cb_bwd_dwsa_partial_kernel(const float* __restrict__ dpre,
+                                                                  const float* __restrict__ sin_, int H, int W,
+                                                                  int ksa, long long P, int nchunk,
+                                                                  float* __restrict__ part) {
+    __shared__ float red[4];
+    const int t = blockIdx.x, chunk = blockIdx.y;
+    const int taps = ksa * ksa, r = ksa / 2;
+    const int ch = t / taps, tt = t - ch * taps;
+    const int ty = tt / ksa, tx = tt - ty * ksa;
+    const long long per = (P + nchunk - 1) / nchunk;
+    const long long p0 = chunk * per, p1 = min(P, p0 + per);
+    const int HW = H * W;
+    float acc = 0.f;
+    for (long long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        int n = (int)(p / HW);
+        int rem = (int)(p - (long long)n * HW);
+        int py = rem / W, px = rem - py * W;
+        int yy = py + ty - r, xx = px + tx - r;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+            acc = fmaf(dpre[p], sin_[((long long)n * HW + yy * W + xx) * 2 + ch], acc);
+    }
+    acc = block_sum_256(acc, red);
+    if (threadIdx.x == 0) part[(long long)chunk * gridDim.x + t] = acc;
+}
+
+__global__ void cb_bwd_dwsa_final_kernel(const float* __restrict__ part, int nt, int nchunk, float* __restrict__ dwsa) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    double s = 0.0;
+    for (int k = 0; k < nchunk; ++k) s += part[(long long)k * nt + t];
+    dwsa[t] = (float)s;
+}
+
+struct Sum3 {
+    float a, b, c;
+};
+
+// b3: per (n,c) sums over pixels of dzc*z, dz0, dz0*z
+__global__ __launch_bounds__(256) void cb_bwd_sums_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                          const float* __restrict__ sc, const float* __restrict__ sh,
+                                                          const float* __restrict__ ca, const float* __restrict__ sa,
+                                                          const float* __restrict__ dsin,
+                                                          const int* __restrict__ sarg, int HW, int C, int nchunk,
+                                                          Sum3* __restrict__ parts) {
+    const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const bool packed = (C <= 256) && (256 % C == 0);
+    const int lanes = packed ? 256 / C : 1;
+    const int plane = packed ? tid / C : 0;
+    __shared__ float s_a[256], s_b[256], s_c[256];
+    const float invC = 1.f / (float)C;
+    for (int cbase = 0; cbase < C; cbase += (packed ? C : 256)) {
+        const int c = packed ? (tid % C) : (cbase + tid);
+        float A = 0.f, B = 0.f, Cc = 0.f;
+        if (c < C) {
+            const long long nc = (long long)n * C + c;
+            const float s = sc[nc], b = sh[nc], a = ca[nc];
+            for (int p = p0 + plane; p < p1; p += lanes) {
+                const long long pp = (long long)n * HW + p;
+                const long long o = pp * C + c;
+                float z = fmaf(y[o], s, b);
+                float dzc = fmaf(dout[o], sa[pp], dsin[pp * 2] * invC);
+                if (sarg[pp] == c) dzc += dsin[pp * 2 + 1];
+                float dz0 = dzc * a;
+                A = fmaf(dzc, z, A);
+                B += dz0;
+                Cc = fmaf(dz0, z, Cc);
+            }
+        }
+        if (packed) {
+            s_a[tid] = A; s_b[tid] = B; s_c[tid] = Cc;
+            __syncthreads();
+            if (plane == 0) {
+                for (int l = 1; l < lanes; ++l) { A += s_a[l * C + c]; B += s_b[l * C + c]; Cc += s_c[l * C + c]; }
+                parts[((long long)n * nchunk + chunk) * C + c] = Sum3{A, B, Cc};
+            }
+            __syncthreads();
+        } else if (c < C) {
+            parts[((long long)n * nchunk + chunk) * C + c] = Sum3{A, B, Cc};
+        }
+    }
+}
+
+// b4: one block; channel-attention MLP backward + IN-backward coefficients per (n,c).
+// coef[n][c] = {mean(dz), mean(dz*z), dvmax}; dw1/dw2 summed over n in fixed order.
+__global__ __launch_bounds__(256) void cb_bwd_ca_kernel(const Sum3* __restrict__ parts, int nchunk,
+                                                        const float* __restrict__ ymax, const float* __restrict__ sc,
+                                                        const float* __restrict__ sh, const float* __restrict__ ca,
+                                                        const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        int N, int HW, int C, int Cr, Sum3* __restrict__ coef,
+                                                        float* __restrict__ dw1, float* __restrict__ dw2) {
+    extern __shared__ float sm[];
+    float* vmax = sm;            // [C]
+    float* dpc = vmax + C;       // [C] d(pre-sigmoid)
+    float* hp = dpc + C;         // [Cr] W1 vmax (pre-relu)
+    float* dhm = hp + Cr;        // [Cr]
+    float* S1 = dhm + Cr;        // [C] sum dz0
+    float* S2 = S1 + C;          // [C] sum dz0*z
+    const int tid = threadIdx.x;
+    for (int i = tid; i < C * Cr; i += blockDim.x) { dw1[i] = 0.f; dw2[i] = 0.f; }
+    __syncthreads();
+    for (int n = 0; n < N; ++n) {
+        for (int c = tid; c < C; c += blockDim.x) {
+            const long long nc = (long long)n * C + c;
+            double A = 0.0, B = 0.0, Cc = 0.0;
+            for (int k = 0; k < nchunk; ++k) {
+                Sum3 p = parts[((long long)n * nchunk + k) * C + c];
+                A += p.a; B += p.b; Cc += p.c;
+            }
+            vmax[c] = fmaf(ymax[nc], sc[nc], sh[nc]);
+            float g = ca[nc];
+            dpc[c] = (float)A * g * (1.f - g);
+            S1[c] = (float)B;
+            S2[c] = (float)Cc;
+        }
+        __syncthreads();
+        for (int j = tid; j < Cr; j += blockDim.x) {
+            float hpre = 0.f, dh = 0.f;
+            for (int c = 0; c < C; ++c) {
+                hpre = fmaf(w1[j * C + c], vmax[c], hpre);
+                dh = fmaf(w2[c * Cr + j], dpc[c], dh);
+            }
+            hp[j] = hpre;
+            dhm[j] = hpre > 0.f ? dh : 0.f;   // avg branch: relu'(0) = 0 -> no gradient
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += blockDim.x) {
+            float dvm = 0.f;
+            for (int j = 0; j < Cr; ++j) {
+                dvm = fmaf(w1[j * C + c], dhm[j], dvm);
+                dw2[c * Cr + j] += dpc[c] * (hp[j] > 0.f ? hp[j] : 0.f);
+                dw1[j * C + c] += dhm[j] * vmax[c];
+            }
+            // dz = dz0 + dvmax * [p == argmax]; sum_p z = 0 (IN output), z[argmax] = vmax
+            const float inv = 1.f / (float)HW;
+            coef[(long long)n * C + c] = Sum3{(S1[c] + dvm) * inv, (S2[c] + dvm * vmax[c]) * inv, dvm};
+        }
+        __syncthreads();
+    }
+}
+
+// b5: dy = scale*(dz - mean(dz) - z*mean(dz*z))
+__global__ void cb_bwd_apply_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                    const float* __restrict__ sc, const float* __restrict__ sh,
+                                    const float* __restrict__ ca, const float* __restrict__ sa,
+                                    const float* __restrict__ dsin, const int* __restrict__ sarg,
+                                    const int* __restrict__ yarg, const Sum3* __restrict__ coef, int HW, int C,
+                                    long long total, float* __restrict__ dy) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int c = (int)(i % C);
+    const long long pp = i / C;
+    const int n = (int)(pp / HW);
+    const int p = (int)(pp - (long long)n * HW);
+    const long long nc = (long long)n * C + c;
+    const float s = sc[nc], b = sh[nc];
+    const float z = fmaf(y[i], s, b);
+    float dzc = fmaf(dout[i], sa[pp], dsin[pp * 2] * (1.f / (float)C));
+    if (sarg[pp] == c) dzc += dsin[pp * 2 + 1];
+    const Sum3 k = coef[nc];
+    float dz = dzc * ca[nc];
+    if (yarg[nc] == p) dz += k.c;
+    dy[i] = s * (dz - k.a - z * k.b);
+}
+
+static inline int cb_chunks(int N, int HW) {
+    int want = (int)cdiv(1024, N);
+    int maxc = (int)cdiv(HW, 64);
+    int c = want < maxc ? want : maxc;
+    return c < 1 ? 1 : c;
+}
+static inline int sa_wchunks(long long P) {
+    long long c = cdiv(P, 4096);
+    if (c < 1) c = 1;
+    if (c > 64) c = 64;
+    return (int)c;
+}
+
+struct CbWs {
+    float* dpre;
+    float* dsin;
+    float* wpart;
+    Sum3* parts;
+    Sum3* coef;
+    size_t total;
+};
+static CbWs cb_layout(void* base, int N, int H, int W, int C, int ksa) {
+    CbWs w;
+    long long P = (long long)N * H * W;
+    size_t off = 0;
+    char* b = reinterpret_cast<char*>(base);
+    w.dpre = reinterpret_cast<float*>(b + off); off = align_up(off + P * sizeof(float), 256);
+    w.dsin = reinterpret_cast<float*>(b + off); off = align_up(off + 2 * P * sizeof(float), 256);
+    w.wpart = reinterpret_cast<float*>(b + off); off = align_up(off + (size_t)sa_wchunks(P) * 2 * ksa * ksa * sizeof(float), 256);
+    int nch = cb_chunks(N, H * W);
+    w.parts = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * nch * C * sizeof(Sum3), 256);
+    w.coef = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * C * sizeof(Sum3), 256);
+    w.total = off;
+    return w;
+}
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" int dcs_cbam_forward(const float* x, const float* y, const float* scale, const float* shift,
+                                const float* ymax, const float* w1, const float* w2, const float* wsa, int N, int H,
+                                int W, int C, int Cr, int ksa, float* ca, float* sin_, int32_t* sarg, float* sa,
+                                float* out, void* stream) {
+    if (!x || !y || !scale || !shift || !ymax || !w1 || !w2 || !wsa || !ca || !sin_ || !sarg || !sa || !out)
+        return fail(DCS_E_INVALID, "cbam_forward: null pointer");
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || Cr <= 0 || ksa <= 0 || (ksa & 1) == 0)
+        return fail(DCS_E_INVALID, "cbam_forward: bad dims");
+    hipStream_t s = as_stream(stream);
+    long long P = (long long)N * H * W;
+    hipLaunchKernelGGL(ca_forward_kernel, dim3(N), dim3(256), (size_t)(C + 2 * Cr) * sizeof(float), s, ymax, scale,
+                       shift, w1, w2, C, Cr, ca);
+    int e = check_launch("ca_forward");
+    if (e) return e;
+    hipLaunchKernelGGL(sa_reduce_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, y, scale, shift, ca, H * W, C, P,
+                       sin_, sarg);
+    e = check_launch("sa_reduce");
+    if (e) return e;
+    hipLaunchKernelGGL(sa_apply_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, x, y, scale, shift, ca, sin_, wsa,
+                       H, W, C, ksa, P, sa, out);
+    return check_launch("sa_apply");
+}
+
+extern "C" size_t dcs_cbam_backward_workspace_size(int N, int H, int W, int C, int Cr, int ksa) {
+    (void)Cr;
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || ksa <= 0) return 0;
+    return cb_layout(nullptr, N, H, W, C, ksa).total;
+}
+
+extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float* scale, const float* shift,
+                                 const float* ymax, const int32_t* yargmax, const float* w1, const float* w2,
+                                 const float* wsa, const float* ca, const float* sin_, const int32_t* sarg,
+                                 const float* sa, int N, int H, int W, int C, int Cr, int ksa, float* dy, float* dw1,
+                                 float* dw2, float* dwsa, void* ws, size_t ws_bytes, void* stream) {
+    if (!dout || !y || !scale || !shift || !ymax || !yargmax || !w1 || !w2 || !wsa || !ca || !sin_ || !sarg || !sa ||
+        !dy || !dw1 || !dw2 || !dwsa || !ws)
+        return fail(DCS_E_INVALID, "cbam_backward: null pointer");
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || Cr <= 0 || ksa <= 0)
+        return fail(DCS_E_INVALID, "cbam_backward: bad dims");
+    if (ws_bytes < dcs_cbam_backward_workspace_size(N, H, W, C, Cr, ksa))
+        return fail(DCS_E_WORKSPACE, "cbam_backward: workspace too small");
+    CbWs w = cb_layout(ws, N, H, W, C, ksa);
+    hipStream_t s = as_stream(stream);
+    const long long P = (long long)N * H * W;
+    const int HW = H * W;
+    hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca, sa,
+                       HW, C, P, w.dpre);
+    int e = check_launch("cb_bwd_dsa");
+    if (e) return e;
+    hipLaunchKernelGGL(cb_bwd_dsin_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, w.dpre, wsa, H, W, ksa, P,
+                       w.dsin);
+    if ((e = check_launch("cb_bwd_dsin"))) return e;
+    const int nt = 2 * ksa * ksa, nwc = sa_wchunks(P);
+    hipLaunchKernelGGL(cb_bwd_dwsa_partial_kernel, dim3(nt, nwc), dim3(256), 0, s, w.dpre, sin_, H, W, ksa, P, nwc,
+                       w.wpart);
+    if ((e = check_launch("cb_bwd_dwsa_partial"))) return e;
+    hipLaunchKernelGGL(cb_bwd_dwsa_final_kernel, dim3((unsigned)cdiv(nt, 128)), dim3(128), 0, s, w.wpart, nt, nwc, dwsa);
+    if ((e = check_launch("cb_bwd_dwsa_final"))) return e;
+    const int nch = cb_chunks(N, HW);
+    hipLaunchKernelGGL(cb_bwd_sums_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin, sarg,
+                       HW, C, nch, w.parts);
+    if ((e = check_launch("cb_bwd_sums"))) return e;
+    hipLaunchKernelGGL(cb_bwd_ca_kernel, dim3(1), dim3(256), (size_t)(4 * C + 2 * Cr) * sizeof(float), s, w.parts, nch,
+                       ymax, scale, shift, ca, w1, w2, N, HW, C, Cr, w.coef, dw1, dw2);
+    if ((e = check_launch("cb_bwd_ca"))) return e;
+    const long long total = P * C;
+    hipLaunchKernelGGL(cb_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dout, y, scale, shift, ca,
+                       sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy);
+    return check_launch("cb_bwd_apply");
+}

@@ -1,0 +1,916 @@
+// Convolution family for the DuCoSy-GAN hot path on gfx950 (MI355X).
+//
+// Every nn.Conv2d of modules/model.py (Generator :94-112, ResidualBlockWithCBAM :72-80,
+// Discriminator :122-129) in forward, data-gradient and weight-gradient form is one
+// implicit GEMM on the f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
+//
+//   rows pass   out[m][n] = sum_k  A[m][k] * B[k][n]
+//       m = output pixel, k = (tap, source channel), n = output channel
+//       A is gathered on the fly from the NHWC source (reflection/zero padding, nearest
+//       x2 upsampling, channel-concat of two sources, stride 1/2, and stride-2 transposed
+//       "parity classes" are all folded into the gather — never materialised), with the
+//       previous layer's InstanceNorm + ReLU/LeakyReLU applied as a per-(n,c) prologue.
+//       B is the packed weight matrix.
+//   wgrad pass  dW[co][k] = sum_pixels dy[p][co] * A[p][k], split over pixels, partial
+//       slabs reduced deterministically by a second kernel.
+//
+// Tiling: 256-thread workgroups (4 waves as 2x2), BM x BN output tile, BK = 32, register-
+// staged double-buffered LDS ([k][m] layouts, m contiguous, padded by 4 floats), each wave
+// owns (BM/2)x(BN/2) = 2x2 or 2x1 32x32 MFMA accumulators.
+#include "common.hpp"
+
+namespace dcs {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr int NT = 256;
+
+// ---------------------------------------------------------------------------------------
+// geometry helpers
+// ---------------------------------------------------------------------------------------
+struct ClassGeom {
+    int My, Mx, ntaps, ry, rx;
+};
+
+__device__ __host__ inline ClassGeom class_geom(const dcs_conv_desc& d, int z) {
+    ClassGeom g;
+    if (!d.parity) {
+        g.My = d.Ho; g.Mx = d.Wo; g.ntaps = d.KH * d.KW; g.ry = 0; g.rx = 0;
+    } else {
+        g.ry = z >> 1; g.rx = z & 1;
+        g.My = (d.Ho - g.ry + 1) >> 1;
+        g.Mx = (d.Wo - g.rx + 1) >> 1;
+        int ty0 = (g.ry + d.pt) & 1, tx0 = (g.rx + d.pl) & 1;
+        int nty = (d.KH - ty0 + 1) >> 1, ntx = (d.KW - tx0 + 1) >> 1;
+        g.ntaps = nty * ntx;
+    }
+    return g;
+}
+
+// tap j of class z -> offset added to the row's base source coordinate, and the packed tap
+__device__ __forceinline__ void tap_decode(const dcs_conv_desc& d, const ClassGeom& g, int j,
+                                           int& ady, int& adx, int& btap) {
+    if (!d.parity) {
+        int ty = j / d.KW, tx = j - ty * d.KW;
+        ady = ty; adx = tx; btap = j;
+    } else {
+        int ty0 = (g.ry + d.pt) & 1, tx0 = (g.rx + d.pl) & 1;
+        int ntx = (d.KW - tx0 + 1) >> 1;
+        int jy = j / ntx, jx = j - jy * ntx;
+        int ty = ty0 + 2 * jy, tx = tx0 + 2 * jx;
+        ady = (g.ry + d.pt - ty) >> 1;  // exact (even numerator)
+        adx = (g.rx + d.pl - tx) >> 1;
+        btap = ty * d.KW + tx;
+    }
+}
+
+// virtual coordinate -> source coordinate (padding + nearest upsampling); false = zero pad
+__device__ __forceinline__ bool map_coord(int v, int Hv, int up, int mode, int& s) {
+    if (v < 0 || v >= Hv) {
+        if (mode == DCS_PAD_ZERO) return false;
+        v = v < 0 ? -v : 2 * (Hv - 1) - v;
+    }
+    s = up == 2 ? (v >> 1) : v;
+    return true;
+}
+
+struct RowInfo {
+    int n, by, bx;        // image, base virtual source coords
+    long long out_off;    // element offset of the output pixel (channel 0), -1 if invalid
+};
+
+__device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassGeom& g, int m) {
+    // 32-bit index math: the host guarantees N*My*Mx < 2^31
+    RowInfo r;
+    const int per = g.My * g.Mx;
+    if (m >= per * d.N) { r.n = 0; r.by = -100000; r.bx = -100000; r.out_off = -1; return r; }
+    const int n = m / per;
+    const int rem = m - n * per;
+    const int qy = rem / g.Mx, qx = rem - qy * g.Mx;
+    int oy, ox;
+    if (!d.parity) {
+        oy = qy; ox = qx;
+        r.by = oy * d.stride - d.pt;
+        r.bx = ox * d.stride - d.pl;
+    } else {
+        oy = 2 * qy + g.ry; ox = 2 * qx + g.rx;
+        r.by = qy; r.bx = qx;
+    }
+    r.n = n;
+    r.out_off = ((long long)(n * d.Ho + oy) * d.Wo + ox) * d.Co;
+    return r;
+}
+
+__device__ __forceinline__ float4 affine_act4(float4 v, const float* sc, const float* sh, int act) {
+    float4 s = *reinterpret_cast<const float4*>(sc);
+    float4 b = *reinterpret_cast<const float4*>(sh);
+    v.x = act_apply(fmaf(v.x, s.x, b.x), act);
+    v.y = act_apply(fmaf(v.y, s.y, b.y), act);
+    v.z = act_apply(fmaf(v.z, s.z, b.z), act);
+    v.w = act_apply(fmaf(v.w, s.w, b.w), act);
+    return v;
+}
+
+// gather 4 consecutive source channels (c..c+3, same tap) for a row; Cs % 4 == 0, s_c == 1
+__device__ __forceinline__ float4 gather4(const dcs_conv_desc& d, const float* __restrict__ src,
+                                          const float* __restrict__ psc, const float* __restrict__ psh,
+                                          int n, int vy, int vx, int c) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    int sy, sx;
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    if (map_coord(vy, Hv, d.up, d.pad_mode, sy) && map_coord(vx, Wv, d.up, d.pad_mode, sx)) {
+        v = *reinterpret_cast<const float4*>(src + n * d.s_n + sy * d.s_h + sx * d.s_w + c);
+        if (d.pro_act != DCS_ACT_NONE) {
+            long long o = (long long)n * d.Cs + c;
+            v = affine_act4(v, psc + o, psh + o, d.pro_act);
+        }
+    }
+    return v;
+}
+
+// gather one source element (general strides, concat of two sources)
+__device__ __forceinline__ float gather1(const dcs_conv_desc& d, const float* __restrict__ src,
+                                         const float* __restrict__ src2,
+                                         const float* __restrict__ psc, const float* __restrict__ psh,
+                                         int n, int vy, int vx, int c) {
+    int sy, sx;
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    if (!(map_coord(vy, Hv, d.up, d.pad_mode, sy) && map_coord(vx, Wv, d.up, d.pad_mode, sx)))
+        return 0.f;
+    float v;
+    if (c < d.csplit)
+        v = src[n * d.s_n + (long long)c * d.s_c + sy * d.s_h + sx * d.s_w];
+    else
+        v = src2[n * d.s2_n + (long long)(c - d.csplit) * d.s2_c + sy * d.s2_h + sx * d.s2_w];
+    if (d.pro_act != DCS_ACT_NONE) {
+        long long o = (long long)n * d.Cs + c;
+        v = act_apply(fmaf(v, psc[o], psh[o]), d.pro_act);
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// weight packing
+// ---------------------------------------------------------------------------------------
+__global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
+                                    int kind, int ci_count, int Kpad, int ldb, float* __restrict__ out) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)Kpad * ldb;
+    if (idx >= total) return;
+    int k = (int)(idx / ldb), col = (int)(idx - (long long)k * ldb);
+    int taps = KH * KW;
+    float v = 0.f;
+    if (kind == 0) {  // B[(tap)*Cin + ci][co]
+        int cin_eff = ci_count;
+        int tap = k / cin_eff, ci = k - tap * cin_eff;
+        if (tap < taps && col < Cout) {
+            int ty = tap / KW, tx = tap - ty * KW;
+            v = w[(((long long)col * Cin + ci) * KH + ty) * KW + tx];
+        }
+    } else {  // B[(tap)*Cout + co][ci]
+        int tap = k / Cout, co = k - tap * Cout;
+        if (tap < taps && col < ci_count) {
+            int ty = tap / KW, tx = tap - ty * KW;
+            if (kind == 1) { ty = KH - 1 - ty; tx = KW - 1 - tx; }
+            v = w[(((long long)co * Cin + col) * KH + ty) * KW + tx];
+        }
+    }
+    out[idx] = v;
+}
+
+// ---------------------------------------------------------------------------------------
+// rows pass: implicit GEMM on v_mfma_f32_32x32x2_f32
+// ---------------------------------------------------------------------------------------
+template <int BM, int BN, bool VEC>
+__global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
+    const dcs_conv_desc d, const float* __restrict__ src, const float* __restrict__ src2,
+    const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
+    const float* __restrict__ psh, float* __restrict__ out) {
+    static_assert(BM == 128, "A loader assumes 128 rows (2 threads per row)");
+    constexpr int WM = BM / 2, WN = BN / 2;        // per-wave tile
+    constexpr int IM = WM / 32, JN = WN / 32;      // 32x32 blocks per wave
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int BCH = (BK * BN / 4) / NT;        // float4 chunks of B per thread
+
+    __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+    __shared__ long long rowoff[BM];
+
+    const int z = blockIdx.z;
+    const ClassGeom g = class_geom(d, z);
+    const long long M = (long long)g.My * g.Mx * d.N;
+    const long long m0 = (long long)blockIdx.x * BM;
+    if (m0 >= M) return;
+    const int n0 = blockIdx.y * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    // A loader: one row, 16 consecutive k
+    const int arow = tid >> 1, akq = (tid & 1) * 16;
+    const RowInfo ri = row_info(d, g, (int)(m0 + arow));
+    if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
+    const bool rvalid = ri.out_off >= 0;
+
+    const int K = g.ntaps * d.Cs;
+    const int nkt = (K + BK - 1) / BK;
+
+    float4 ra[4];
+    float4 rb[BCH];
+
+    auto load_a = [&](int kt) {
+        if (VEC) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int k = kt * BK + akq + 4 * i;
+                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                int j = k / d.Cs, c = k - j * d.Cs;
+                if (rvalid && j < g.ntaps) {
+                    int ady, adx, bt;
+                    tap_decode(d, g, j, ady, adx, bt);
+                    ra[i] = gather4(d, src, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    int k = kt * BK + akq + 4 * i + q;
+                    int j = k / d.Cs, c = k - j * d.Cs;
+                    e[q] = 0.f;
+                    if (rvalid && j < g.ntaps) {
+                        int ady, adx, bt;
+                        tap_decode(d, g, j, ady, adx, bt);
+                        e[q] = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                    }
+                }
+                ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+    };
+    // B loader: 8 threads per k-row, BN/8 consecutive columns each
+    const int bkr = tid >> 3, bc0 = (tid & 7) * (BN / 8);
+    auto load_b = [&](int kt) {
+        const int k = kt * BK + bkr;
+        long long row;
+        bool ok = true;
+        if (!d.parity) {
+            row = k;
+        } else {
+            int j = k / d.Cs, c = k - j * d.Cs;
+            ok = j < g.ntaps;
+            int ady, adx, bt = 0;
+            if (ok) tap_decode(d, g, j, ady, adx, bt);
+            row = (long long)bt * d.Cs + c;
+        }
+        const float* bp = wp + row * d.ldb + n0 + bc0;
+#pragma unroll
+        for (int i = 0; i < BCH; ++i)
+            rb[i] = ok ? *reinterpret_cast<const float4*>(bp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto store_tiles = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            As[buf][akq + 4 * i + 0][arow] = ra[i].x;
+            As[buf][akq + 4 * i + 1][arow] = ra[i].y;
+            As[buf][akq + 4 * i + 2][arow] = ra[i].z;
+            As[buf][akq + 4 * i + 3][arow] = ra[i].w;
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][bkr][bc0 + 4 * i]) = rb[i];
+    };
+
+    floatx16 acc[IM][JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    load_a(0);
+    load_b(0);
+    store_tiles(0);
+    __syncthreads();
+
+    const int l32 = lane & 31, lk = lane >> 5;
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
+#pragma unroll
+        for (int ks = 0; ks < BK / 2; ++ks) {
+            const int k = 2 * ks + lk;
+            float a[IM], b[JN];
+#pragma unroll
+            for (int i = 0; i < IM; ++i) a[i] = As[cur][k][wm * WM + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < JN; ++j) b[j] = Bs[cur][k][wn * WN + j * 32 + l32];
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nkt) store_tiles(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: + bias, activation, NHWC store
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + l32;
+        if (col >= d.Co) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < IM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                const long long off = rowoff[row];
+                if (off < 0) continue;
+                float v = acc[i][j][r] + bv;
+                if (d.epi_act != DCS_ACT_NONE) v = act_apply(v, d.epi_act);
+                out[off + col] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// wgrad pass: dW[co][k] = sum_p dy[p][co] * A[p][k]  (split over pixels -> partial slabs)
+// ---------------------------------------------------------------------------------------
+template <int BM, int BN, bool VEC>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
+    const dcs_conv_desc d, const float* __restrict__ dy, const float* __restrict__ src,
+    const float* __restrict__ src2, const float* __restrict__ psc, const float* __restrict__ psh,
+    float* __restrict__ ws, int kt_per_split) {
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int IM = WM / 32, JN = WN / 32;
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int ACH = (BK * BM / 4) / NT;
+    constexpr int BCH = (BK * BN / 4) / NT;
+
+    __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+
+    const ClassGeom g = class_geom(d, 0);
+    const long long P = (long long)g.My * g.Mx * d.N;   // pixels (reduction)
+    const int Ktot = g.ntaps * d.Cs;                    // GEMM N
+    const int m0 = blockIdx.y * BM;                     // output channel tile
+    const int n0 = blockIdx.x * BN;                     // (tap, ci) tile
+    const int split = blockIdx.z;
+    const long long nkt_all = (P + BK - 1) / BK;
+    const long long kt_beg = (long long)split * kt_per_split;
+    long long kt_end = kt_beg + kt_per_split;
+    if (kt_end > nkt_all) kt_end = nkt_all;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    float4 ra[ACH];
+    float4 rb[BCH];
+
+    // both loaders: 8 threads per k-row (pixel), each a run of consecutive columns
+    const int kr = tid >> 3;
+    const int ac0 = (tid & 7) * (BM / 8), bc0 = (tid & 7) * (BN / 8);
+    auto load_a = [&](long long kt) {  // dy rows: [p][co]
+        const long long p = kt * BK + kr;
+        const int co = m0 + ac0;
+        const bool ok = p < P;
+#pragma unroll
+        for (int i = 0; i < ACH; ++i)
+            ra[i] = (ok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto load_b = [&](long long kt) {  // gathered source rows: [p][(tap, ci)]
+        const long long p = kt * BK + kr;
+        const RowInfo ri = row_info(d, g, (int)(p < P ? p : P));
+        const bool ok = ri.out_off >= 0;
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int nn = n0 + bc0 + 4 * i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ok) {
+                if (VEC) {
+                    if (nn < Ktot) {
+                        int j = nn / d.Cs, c = nn - j * d.Cs;
+                        int ady, adx, bt;
+                        tap_decode(d, g, j, ady, adx, bt);
+                        v = gather4(d, src, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                    }
+                } else {
+                    float e[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        e[q] = 0.f;
+                        int n1 = nn + q;
+                        if (n1 < Ktot) {
+                            int j = n1 / d.Cs, c = n1 - j * d.Cs;
+                            int ady, adx, bt;
+                            tap_decode(d, g, j, ady, adx, bt);
+                            e[q] = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                        }
+                    }
+                    v = make_float4(e[0], e[1], e[2], e[3]);
+                }
+            }
+            rb[i] = v;
+        }
+    };
+    auto store_tiles = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * i]) = ra[i];
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * i]) = rb[i];
+    };
+
+    floatx16 acc[IM][JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (kt_beg < kt_end) {
+        load_a(kt_beg);
+        load_b(kt_beg);
+        store_tiles(0);
+    }
+    __syncthreads();
+    const int l32 = lane & 31, lk = lane >> 5;
+    for (long long kt = kt_beg; kt < kt_end; ++kt) {
+        const int cur = (int)((kt - kt_beg) & 1);
+        if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
+#pragma unroll
+        for (int ks = 0; ks < BK / 2; ++ks) {
+            const int k = 2 * ks + lk;
+            float a[IM], b[JN];
+#pragma unroll
+            for (int i = 0; i < IM; ++i) a[i] = As[cur][k][wm * WM + i * 32 + l32];
+#pragma unroll
+            for (int j = 0; j < JN; ++j) b[j] = Bs[cur][k][wn * WN + j * 32 + l32];
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < kt_end) store_tiles(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* slab = ws + (long long)split * d.Co * Ktot;
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + l32;
+        if (col >= Ktot) continue;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                if (row < d.Co) slab[(long long)row * Ktot + col] = acc[i][j][r];
+            }
+    }
+}
+
+// dw[co][ci][ty][tx] = sum_s ws[s][co][(ty*KW+tx)*Cs + ci]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int Co, int Cs, int KH,
+                                    int KW, float* __restrict__ dw) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int taps = KH * KW;
+    const long long Ktot = (long long)taps * Cs;
+    const long long total = (long long)Co * Ktot;
+    if (idx >= total) return;
+    // idx enumerates the OIHW output
+    int tap = (int)(idx % taps);
+    long long t2 = idx / taps;
+    int ci = (int)(t2 % Cs);
+    int co = (int)(t2 / Cs);
+    long long src = (long long)co * Ktot + (long long)tap * Cs + ci;
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += ws[(long long)k * total + src];
+    dw[idx] = s;
+}
+
+// ---------------------------------------------------------------------------------------
+// narrow rows (Co <= 4): one thread per output pixel, weights in LDS
+// ---------------------------------------------------------------------------------------
+template <int NO, bool VEC>
+__global__ __launch_bounds__(256) void conv_rows_narrow_kernel(
+    const dcs_conv_desc d, const float* __restrict__ src, const float* __restrict__ src2,
+    const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
+    const float* __restrict__ psh, float* __restrict__ out, int Krows) {
+    extern __shared__ __attribute__((aligned(16))) float wl[];  // [Krows][NO]
+    for (int i = threadIdx.x; i < Krows * NO; i += blockDim.x) {
+        int k = i / NO, o = i - k * NO;
+        wl[i] = wp[(long long)k * d.ldb + o];
+    }
+    __syncthreads();
+    const int z = blockIdx.y;
+    const ClassGeom g = class_geom(d, z);
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    const RowInfo ri = row_info(d, g, m);
+    if (ri.out_off < 0) return;
+    float acc[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[o] = 0.f;
+    for (int j = 0; j < g.ntaps; ++j) {
+        int ady, adx, bt;
+        tap_decode(d, g, j, ady, adx, bt);
+        const float* wt = wl + (long long)bt * d.Cs * NO;
+        if (VEC) {
+            int sy, sx;
+            const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+            if (!(map_coord(ri.by + ady, Hv, d.up, d.pad_mode, sy) &&
+                  map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx)))
+                continue;
+            const float* sp = src + ri.n * d.s_n + sy * d.s_h + sx * d.s_w;
+            const long long so = (long long)ri.n * d.Cs;
+            for (int c = 0; c < d.Cs; c += 4) {
+                float4 v = *reinterpret_cast<const float4*>(sp + c);
+                if (d.pro_act != DCS_ACT_NONE) v = affine_act4(v, psc + so + c, psh + so + c, d.pro_act);
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    acc[o] = fmaf(v.x, wt[(c + 0) * NO + o], acc[o]);
+                    acc[o] = fmaf(v.y, wt[(c + 1) * NO + o], acc[o]);
+                    acc[o] = fmaf(v.z, wt[(c + 2) * NO + o], acc[o]);
+                    acc[o] = fmaf(v.w, wt[(c + 3) * NO + o], acc[o]);
+                }
+            }
+        } else {
+            for (int c = 0; c < d.Cs; ++c) {
+                float v = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+#pragma unroll
+                for (int o = 0; o < NO; ++o) acc[o] = fmaf(v, wt[c * NO + o], acc[o]);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+        if (o >= d.Co) break;
+        float v = acc[o] + (bias ? bias[o] : 0.f);
+        if (d.epi_act != DCS_ACT_NONE) v = act_apply(v, d.epi_act);
+        out[ri.out_off + o] = v;
+    }
+}
+
+// narrow wgrad: partial[s][o][k] = sum_{p in split s} dy[p][o] * A[p][k]
+template <int NO, bool VEC>
+__global__ __launch_bounds__(256) void conv_wgrad_narrow_kernel(
+    const dcs_conv_desc d, const float* __restrict__ dy, const float* __restrict__ src,
+    const float* __restrict__ src2, const float* __restrict__ psc, const float* __restrict__ psh,
+    float* __restrict__ ws, long long pix_per_split) {
+    const ClassGeom g = class_geom(d, 0);
+    const long long P = (long long)g.My * g.Mx * d.N;
+    const int Ktot = g.ntaps * d.Cs;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int split = blockIdx.y;
+    const long long p0 = (long long)split * pix_per_split;
+    long long p1 = p0 + pix_per_split;
+    if (p1 > P) p1 = P;
+    if (k >= Ktot) return;
+    const int j = k / d.Cs, c = k - j * d.Cs;
+    int ady, adx, bt;
+    tap_decode(d, g, j, ady, adx, bt);
+    float acc[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[o] = 0.f;
+    for (long long p = p0; p < p1; ++p) {
+        RowInfo ri = row_info(d, g, (int)p);
+        float v = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+        const float* dp = dy + p * d.Co;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[o] = fmaf(dp[o], v, acc[o]);
+    }
+    float* slab = ws + (long long)split * d.Co * Ktot;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+        if (o < d.Co) slab[(long long)o * Ktot + k] = acc[o];
+}
+
+// ---------------------------------------------------------------------------------------
+// padding / upsampling adjoints
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int reflect_pre(int i, int H, int pad, int* a) {
+    // padded positions a with reflect(a - pad) == i
+    int n = 0;
+    a[n++] = i + pad;
+    if (i >= 1 && i <= pad) a[n++] = pad - i;
+    if (i >= H - 1 - pad && i <= H - 2) a[n++] = 2 * (H - 1) - i + pad;
+    return n;
+}
+
+__global__ void reflect_fold_kernel(const float* __restrict__ dxp, const float* __restrict__ add,
+                                    float* __restrict__ dx, int N, int H, int W, int C4, int pad) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)N * H * W * C4;
+    if (idx >= total) return;
+    int c4 = (int)(idx % C4);
+    long long t = idx / C4;
+    int j = (int)(t % W); t /= W;
+    int i = (int)(t % H);
+    int n = (int)(t / H);
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+    int ay[3], ax[3];
+    int ny = reflect_pre(i, H, pad, ay), nx = reflect_pre(j, W, pad, ax);
+    float4 s = add ? reinterpret_cast<const float4*>(add)[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < ny; ++p)
+        for (int q = 0; q < nx; ++q) {
+            float4 v = reinterpret_cast<const float4*>(dxp)[(((long long)n * Hp + ay[p]) * Wp + ax[q]) * C4 + c4];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    reinterpret_cast<float4*>(dx)[idx] = s;
+}
+
+__global__ void reflect_fold_scalar_kernel(const float* __restrict__ dxp, const float* __restrict__ add,
+                                           float* __restrict__ dx, int N, int H, int W, int C, int pad) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)N * H * W * C;
+    if (idx >= total) return;
+    int c = (int)(idx % C);
+    long long t = idx / C;
+    int j = (int)(t % W); t /= W;
+    int i = (int)(t % H);
+    int n = (int)(t / H);
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+    int ay[3], ax[3];
+    int ny = reflect_pre(i, H, pad, ay), nx = reflect_pre(j, W, pad, ax);
+    float s = add ? add[idx] : 0.f;
+    for (int p = 0; p < ny; ++p)
+        for (int q = 0; q < nx; ++q) s += dxp[(((long long)n * Hp + ay[p]) * Wp + ax[q]) * C + c];
+    dx[idx] = s;
+}
+
+__global__ void upsample2_grad_kernel(const float* __restrict__ du, float* __restrict__ dx, int N, int H,
+                                      int W, int C4) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long total = (long long)N * H * W * C4;
+    if (idx >= total) return;
+    int c4 = (int)(idx % C4);
+    long long t = idx / C4;
+    int j = (int)(t % W); t /= W;
+    int i = (int)(t % H);
+    int n = (int)(t / H);
+    const float4* u = reinterpret_cast<const float4*>(du);
+    const long long W2 = 2LL * W;
+    long long b = (((long long)n * 2 * H + 2 * i) * W2 + 2 * j) * C4 + c4;
+    float4 a0 = u[b], a1 = u[b + C4], a2 = u[b + W2 * C4], a3 = u[b + W2 * C4 + C4];
+    reinterpret_cast<float4*>(dx)[idx] =
+        make_float4(a0.x + a1.x + a2.x + a3.x, a0.y + a1.y + a2.y + a3.y, a0.z + a1.z + a2.z + a3.z,
+                    a0.w + a1.w + a2.w + a3.w);
+}
+
+// ---------------------------------------------------------------------------------------
+// host-side validation and dispatch
+// ---------------------------------------------------------------------------------------
+static int validate(const dcs_conv_desc* d, bool rows) {
+    if (!d) return fail(DCS_E_INVALID, "null descriptor");
+    if (d->N <= 0 || d->Hs <= 0 || d->Ws <= 0 || d->Cs <= 0 || d->Ho <= 0 || d->Wo <= 0 || d->Co <= 0)
+        return fail(DCS_E_INVALID, "conv: non-positive dimension");
+    if (d->KH <= 0 || d->KW <= 0 || d->KH * d->KW > 64) return fail(DCS_E_INVALID, "conv: bad kernel");
+    if (d->up != 1 && d->up != 2) return fail(DCS_E_INVALID, "conv: up must be 1 or 2");
+    if (d->stride != 1 && d->stride != 2) return fail(DCS_E_INVALID, "conv: stride must be 1 or 2");
+    if (d->parity && (d->stride != 2 || d->up != 1 || d->pad_mode != DCS_PAD_ZERO))
+        return fail(DCS_E_INVALID, "conv: parity rows need stride 2, no upsample, zero pad");
+    if (d->pad_mode == DCS_PAD_REFLECT && (d->pt >= d->Hs * d->up || d->pl >= d->Ws * d->up))
+        return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
+    if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
+    if (!d->parity) {
+        // output dims must be those of the forward conv over the virtual input
+        int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
+        (void)Hv; (void)Wv;
+    }
+    (void)rows;
+    return DCS_OK;
+}
+
+static bool vec_ok(const dcs_conv_desc* d, const float* src) {
+    return (d->Cs % 4 == 0) && d->s_c == 1 && d->csplit == d->Cs &&
+           (d->s_w % 4 == 0) && (d->s_h % 4 == 0) && (d->s_n % 4 == 0) &&
+           ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+}
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                                int Kpad, int ldb, float* out, void* stream) {
+    if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ldb <= 0 || ci_count <= 0 ||
+        ci_count > Cin || kind < 0 || kind > 2)
+        return fail(DCS_E_INVALID, "pack_weights: bad arguments");
+    long long total = (long long)Kpad * ldb;
+    hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
+                       Cout, Cin, KH, KW, kind, ci_count, Kpad, ldb, out);
+    return check_launch("pack_weights");
+}
+
+extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack,
+                             const float* bias, const float* psc, const float* psh, float* out, void* stream) {
+    int e = validate(dp, true);
+    if (e) return e;
+    const dcs_conv_desc& d = *dp;
+    if (!src || !wpack || !out) return fail(DCS_E_INVALID, "conv_rows: null pointer");
+    if (d.pro_act != DCS_ACT_NONE && (!psc || !psh)) return fail(DCS_E_INVALID, "conv_rows: missing prologue");
+    if (d.csplit < d.Cs && !src2) return fail(DCS_E_INVALID, "conv_rows: missing src2");
+    const int BN = d.Co > 64 ? 128 : 64;
+    if (d.ldb % BN != 0 || d.ldb < d.Co) return fail(DCS_E_INVALID, "conv_rows: ldb must be a multiple of the N tile");
+    if (d.Co % 4 != 0) return fail(DCS_E_INVALID, "conv_rows: Co must be a multiple of 4 (use the narrow path)");
+    long long Mmax = 0;
+    const int ncls = d.parity ? 4 : 1;
+    for (int z = 0; z < ncls; ++z) {
+        ClassGeom g = class_geom(d, z);
+        long long M = (long long)g.My * g.Mx * d.N;
+        if (M > Mmax) Mmax = M;
+    }
+    dim3 grid((unsigned)cdiv(Mmax, 128), (unsigned)cdiv(d.Co, BN), ncls);
+    const bool vec = vec_ok(dp, src);
+    hipStream_t s = as_stream(stream);
+    if (BN == 128) {
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+    } else {
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+    }
+    return check_launch("conv_rows");
+}
+
+namespace {
+struct WgradPlan {
+    int BM, BN, nsplit, kt_per_split;
+    long long Ktot;
+};
+WgradPlan wgrad_plan(const dcs_conv_desc& d) {
+    WgradPlan p;
+    ClassGeom g = class_geom(d, 0);
+    long long P = (long long)g.My * g.Mx * d.N;
+    p.Ktot = (long long)g.ntaps * d.Cs;
+    p.BM = d.Co > 64 ? 128 : 64;
+    p.BN = 128;
+    long long tiles = cdiv(d.Co, p.BM) * cdiv(p.Ktot, p.BN);
+    long long nkt = cdiv(P, BK);
+    long long want = cdiv(1024, tiles);           // aim for >= 1024 workgroups
+    long long maxs = cdiv(nkt, 8);               // >= 8 k-tiles per split
+    long long ns = want < maxs ? want : maxs;
+    if (ns < 1) ns = 1;
+    if (ns > 256) ns = 256;
+    p.kt_per_split = (int)cdiv(nkt, ns);
+    p.nsplit = (int)cdiv(nkt, p.kt_per_split);
+    return p;
+}
+}  // namespace
+
+extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
+    if (!dp) return 0;
+    WgradPlan p = wgrad_plan(*dp);
+    return (size_t)p.nsplit * dp->Co * p.Ktot * sizeof(float);
+}
+
+extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const float* x, const float* x2,
+                              const float* psc, const float* psh, float* dw, void* ws, size_t ws_bytes,
+                              void* stream) {
+    int e = validate(dp, false);
+    if (e) return e;
+    const dcs_conv_desc& d = *dp;
+    if (d.parity) return fail(DCS_E_INVALID, "conv_wgrad: describe the forward conv (parity=0)");
+    if (!dy || !x || !dw || !ws) return fail(DCS_E_INVALID, "conv_wgrad: null pointer");
+    if (d.Co % 4 != 0) return fail(DCS_E_INVALID, "conv_wgrad: Co must be a multiple of 4");
+    if (ws_bytes < dcs_conv_wgrad_workspace_size(dp)) return fail(DCS_E_WORKSPACE, "conv_wgrad: workspace too small");
+    WgradPlan p = wgrad_plan(d);
+    dim3 grid((unsigned)cdiv(p.Ktot, p.BN), (unsigned)cdiv(d.Co, p.BM), p.nsplit);
+    const bool vec = vec_ok(dp, x);
+    hipStream_t s = as_stream(stream);
+    float* w = reinterpret_cast<float*>(ws);
+    if (p.BM == 128) {
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+    } else {
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+    }
+    e = check_launch("conv_wgrad");
+    if (e) return e;
+    long long total = (long long)d.Co * p.Ktot;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, p.nsplit, d.Co,
+                       d.Cs, d.KH, d.KW, dw);
+    return check_launch("conv_wgrad_reduce");
+}
+
+extern "C" int dcs_conv_rows_narrow(const dcs_conv_desc* dp, const float* src, const float* src2,
+                                    const float* wpack, const float* bias, const float* psc, const float* psh,
+                                    float* out, void* stream) {
+    int e = validate(dp, true);
+    if (e) return e;
+    const dcs_conv_desc& d = *dp;
+    if (!src || !wpack || !out) return fail(DCS_E_INVALID, "conv_rows_narrow: null pointer");
+    if (d.Co > 4) return fail(DCS_E_INVALID, "conv_rows_narrow: Co must be <= 4");
+    if (d.ldb < d.Co) return fail(DCS_E_INVALID, "conv_rows_narrow: ldb < Co");
+    const int NO = d.Co <= 1 ? 1 : 4;
+    const int Krows = d.KH * d.KW * d.Cs;
+    size_t lds = (size_t)Krows * NO * sizeof(float);
+    if (lds > 64 * 1024) return fail(DCS_E_INVALID, "conv_rows_narrow: weights exceed 64 KiB of LDS");
+    long long Mmax = 0;
+    const int ncls = d.parity ? 4 : 1;
+    for (int z = 0; z < ncls; ++z) {
+        ClassGeom g = class_geom(d, z);
+        long long M = (long long)g.My * g.Mx * d.N;
+        if (M > Mmax) Mmax = M;
+    }
+    dim3 grid((unsigned)cdiv(Mmax, 256), ncls);
+    const bool vec = vec_ok(dp, src);
+    hipStream_t s = as_stream(stream);
+    // the kernel reads wp[k*ldb + o] for o < NO: ldb must cover NO columns
+    if (d.ldb < NO) return fail(DCS_E_INVALID, "conv_rows_narrow: ldb must be >= 4 when Co > 1");
+    if (NO == 1) {
+        if (vec) hipLaunchKernelGGL((conv_rows_narrow_kernel<1, true>), grid, dim3(256), lds, s, d, src, src2, wpack, bias, psc, psh, out, Krows);
+        else hipLaunchKernelGGL((conv_rows_narrow_kernel<1, false>), grid, dim3(256), lds, s, d, src, src2, wpack, bias, psc, psh, out, Krows);
+    } else {
+        if (vec) hipLaunchKernelGGL((conv_rows_narrow_kernel<4, true>), grid, dim3(256), lds, s, d, src, src2, wpack, bias, psc, psh, out, Krows);
+        else hipLaunchKernelGGL((conv_rows_narrow_kernel<4, false>), grid, dim3(256), lds, s, d, src, src2, wpack, bias, psc, psh, out, Krows);
+    }
+    return check_launch("conv_rows_narrow");
+}
+
+namespace {
+long long narrow_pix_per_split(const dcs_conv_desc& d, int* nsplit) {
+    ClassGeom g = class_geom(d, 0);
+    long long P = (long long)g.My * g.Mx * d.N;
+    long long Ktot = (long long)g.ntaps * d.Cs;
+    long long kb = cdiv(Ktot, 256);
+    long long want = cdiv(2048, kb);
+    long long ns = want < P ? want : P;
+    if (ns < 1) ns = 1;
+    if (ns > 4096) ns = 4096;
+    long long pps = cdiv(P, ns);
+    *nsplit = (int)cdiv(P, pps);
+    return pps;
+}
+}  // namespace
+
+extern "C" size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* dp) {
+    if (!dp) return 0;
+    int ns;
+    narrow_pix_per_split(*dp, &ns);
+    ClassGeom g = class_geom(*dp, 0);
+    return (size_t)ns * dp->Co * g.ntaps * dp->Cs * sizeof(float);
+}
+
+extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, const float* x, const float* x2,
+                                     const float* psc, const float* psh, float* dw, void* ws, size_t ws_bytes,
+                                     void* stream) {
+    int e = validate(dp, false);
+    if (e) return e;
+    const dcs_conv_desc& d = *dp;
+    if (d.parity || d.Co > 4) return fail(DCS_E_INVALID, "conv_wgrad_narrow: forward conv with Co <= 4 expected");
+    if (!dy || !x || !dw || !ws) return fail(DCS_E_INVALID, "conv_wgrad_narrow: null pointer");
+    if (ws_bytes < dcs_conv_wgrad_narrow_workspace_size(dp)) return fail(DCS_E_WORKSPACE, "conv_wgrad_narrow: workspace too small");
+    int ns;
+    long long pps = narrow_pix_per_split(d, &ns);
+    ClassGeom g = class_geom(d, 0);
+    long long Ktot = (long long)g.ntaps * d.Cs;
+    dim3 grid((unsigned)cdiv(Ktot, 256), ns);
+    hipStream_t s = as_stream(stream);
+    float* w = reinterpret_cast<float*>(ws);
+    if (d.Co == 1) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<1, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
+    else if (d.Co == 2) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<2, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
+    else if (d.Co == 3) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<3, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
+    else hipLaunchKernelGGL((conv_wgrad_narrow_kernel<4, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
+    e = check_launch("conv_wgrad_narrow");
+    if (e) return e;
+    long long total = (long long)d.Co * Ktot;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
+                       d.KH, d.KW, dw);
+    return check_launch("conv_wgrad_narrow_reduce");
+}
+
+extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* dx, int N, int H, int W, int C,
+                                int pad, void* stream) {
+    if (!dxpad || !dx || N <= 0 || H <= 0 || W <= 0 || C <= 0 || pad < 0 || pad > 3 || pad >= H || pad >= W)
+        return fail(DCS_E_INVALID, "reflect_fold: bad arguments");
+    hipStream_t s = as_stream(stream);
+    if (C % 4 == 0) {
+        long long total = (long long)N * H * W * (C / 4);
+        hipLaunchKernelGGL(reflect_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dxpad, addend, dx,
+                           N, H, W, C / 4, pad);
+    } else {
+        long long total = (long long)N * H * W * C;
+        hipLaunchKernelGGL(reflect_fold_scalar_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dxpad,
+                           addend, dx, N, H, W, C, pad);
+    }
+    return check_launch("reflect_fold");
+}
+
+extern "C" int dcs_upsample2_grad(const float* dup, float* dx, int N, int H, int W, int C, void* stream) {
+    if (!dup || !dx || N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0)
+        return fail(DCS_E_INVALID, "upsample2_grad: bad arguments (C % 4 == 0 required)");
+    long long total = (long long)N * H * W * (C / 4);
+    hipLaunchKernelGGL(upsample2_grad_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream),
+                       dup, dx, N, H, W, C / 4);
+    return check_launch("upsample2_grad");
+}

@@ -1,0 +1,722 @@
+// Loss kernels of the G step (modules/trainer.py:22-184, 347-351, 469-512) and SSIM
+// (pytorch_msssim.SSIM restated).  Every loss computes its value AND its gradient with
+// respect to `pred` in the same call (the backward only rescales by the incoming scalar),
+// all on single-channel planes [N,1,H,W].  Global reductions are two-level (per-block
+// double partials, then one fixed-order finalize block) — deterministic.
+#include "common.hpp"
+
+namespace dcs {
+
+constexpr int RB = 256;        // threads per block
+constexpr int MAXBLK = 1024;   // reduction grid cap
+
+static inline int red_blocks(long long n) {
+    long long b = cdiv(n, RB);
+    if (b > MAXBLK) b = MAXBLK;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+// workspace layout (floats): [0,256) scalars, [256, 256+8*MAXBLK*2) double partials, then maps
+struct LossWs {
+    float* sc;      // scalars
+    double* part;   // partials [MAXBLK][8]
+    unsigned* hist; // 256 bins
+    unsigned* st;   // radix state
+    float* maps;    // map region
+};
+static LossWs loss_ws(void* ws) {
+    LossWs w;
+    char* b = reinterpret_cast<char*>(ws);
+    w.sc = reinterpret_cast<float*>(b);
+    w.part = reinterpret_cast<double*>(b + 1024);
+    w.hist = reinterpret_cast<unsigned*>(b + 1024 + (size_t)MAXBLK * 8 * sizeof(double));
+    w.st = w.hist + 256;
+    w.maps = reinterpret_cast<float*>(b + 1024 + (size_t)MAXBLK * 8 * sizeof(double) + 4096);
+    return w;
+}
+static size_t loss_ws_fixed() { return 1024 + (size_t)MAXBLK * 8 * sizeof(double) + 4096; }
+
+template <int K>
+__device__ __forceinline__ void block_partials(double (&v)[K], double* part) {
+    __shared__ double red[K][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        double x = wave_sum_d(v[q]);
+        if (lane == 0) red[q][w] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        int q = threadIdx.x;
+        part[(long long)blockIdx.x * 8 + q] = red[q][0] + red[q][1] + red[q][2] + red[q][3];
+    }
+}
+
+// sum of partials of quantity q over nb blocks, in block order (called by one thread)
+__device__ __forceinline__ double sum_parts(const double* part, int nb, int q) {
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[(long long)b * 8 + q];
+    return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// L1 / MSE (nn.L1Loss, nn.MSELoss; trainer.py:347-349)
+// ---------------------------------------------------------------------------------------
+template <int KIND>  // 0 L1, 1 MSE, 2 MSE vs constant
+__global__ __launch_bounds__(RB) void pointwise_kernel(const float* __restrict__ p, const float* __restrict__ t,
+                                                       float tc, long long n, float* __restrict__ grad,
+                                                       double* part) {
+    double acc[1] = {0.0};
+    const float inv = 1.f / (float)n;
+    for (long long i = (long long)blockIdx.x * RB + threadIdx.x; i < n; i += (long long)gridDim.x * RB) {
+        float d = p[i] - (KIND == 2 ? tc : t[i]);
+        if (KIND == 0) {
+            acc[0] += fabsf(d);
+            if (grad) grad[i] = sgnf(d) * inv;
+        } else {
+            acc[0] += (double)d * d;
+            if (grad) grad[i] = 2.f * d * inv;
+        }
+    }
+    block_partials<1>(acc, part);
+}
+
+__global__ void finalize_mean_kernel(const double* part, int nb, long long n, float* out) {
+    if (threadIdx.x == 0) out[0] = (float)(sum_parts(part, nb, 0) / (double)n);
+}
+
+// ---------------------------------------------------------------------------------------
+// GradientLoss (trainer.py:22-40)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(RB) void gradient_loss_kernel(const float* __restrict__ p, const float* __restrict__ t,
+                                                           int N, int H, int W, float* __restrict__ grad,
+                                                           double* part) {
+    double acc[2] = {0.0, 0.0};
+    const long long n = (long long)N * H * W;
+    const float ix = 1.f / (float)((long long)N * H * (W - 1));
+    const float iy = 1.f / (float)((long long)N * (H - 1) * W);
+    for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < n; e += (long long)gridDim.x * RB) {
+        int j = (int)(e % W);
+        int i = (int)((e / W) % H);
+        float pv = p[e], tv = t[e];
+        float g = 0.f;
+        if (j + 1 < W) {  // x-difference owned by (i, j)
+            float dp = p[e + 1] - pv, dt = t[e + 1] - tv;
+            float ex = fabsf(dp) - fabsf(dt);
+            acc[0] += fabsf(ex);
+            g -= sgnf(ex) * sgnf(dp) * ix;
+        }
+        if (j > 0) {
+            float dp = pv - p[e - 1], dt = tv - t[e - 1];
+            float ex = fabsf(dp) - fabsf(dt);
+            g += sgnf(ex) * sgnf(dp) * ix;
+        }
+        if (i + 1 < H) {
+            float dp = p[e + W] - pv, dt = t[e + W] - tv;
+            float ey = fabsf(dp) - fabsf(dt);
+            acc[1] += fabsf(ey);
+            g -= sgnf(ey) * sgnf(dp) * iy;
+        }
+        if (i > 0) {
+            float dp = pv - p[e - W], dt = tv - t[e - W];
+            float ey = fabsf(dp) - fabsf(dt);
+            g += sgnf(ey) * sgnf(dp) * iy;
+        }
+        if (grad) grad[e] = g;
+    }
+    block_partials<2>(acc, part);
+}
+
+__global__ void gradient_loss_final(const double* part, int nb, int N, int H, int W, float* out) {
+    if (threadIdx.x == 0) {
+        double sx = sum_parts(part, nb, 0), sy = sum_parts(part, nb, 1);
+        out[0] = (float)(sx / ((double)N * H * (W - 1)) + sy / ((double)N * (H - 1) * W));
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// ContrastAttentionLoss (trainer.py:43-86): AvgPool(k, s1, p k/2, count_include_pad)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float box_mean(const float* __restrict__ x, int n, int i, int j, int H, int W, int k) {
+    const int r = k / 2;
+    float s = 0.f;
+    for (int a = -r; a <= r; ++a) {
+        int ii = i + a;
+        if (ii < 0 || ii >= H) continue;
+        const float* row = x + ((long long)n * H + ii) * W;
+        for (int b = -r; b <= r; ++b) {
+            int jj = j + b;
+            if (jj >= 0 && jj < W) s += row[jj];
+        }
+    }
+    return s / (float)(k * k);
+}
+
+__global__ __launch_bounds__(RB) void ca_loss_kernel(const float* __restrict__ p, const float* __restrict__ t,
+                                                     const float* __restrict__ s, int N, int H, int W, float sigma,
+                                                     float minw, float maxw, int k, float* __restrict__ gmap,
+                                                     double* part) {
+    double acc[1] = {0.0};
+    const long long n = (long long)N * H * W;
+    const float inv = 1.f / (float)n;
+    for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < n; e += (long long)gridDim.x * RB) {
+        int j = (int)(e % W);
+        long long r = e / W;
+        int i = (int)(r % H);
+        int nn = (int)(r / H);
+        float tb = box_mean(t, nn, i, j, H, W, k);
+        float sb = box_mean(s, nn, i, j, H, W, k);
+        float pb = box_mean(p, nn, i, j, H, W, k);
+        float w = minw + (maxw - minw) * (1.f - expf(-fabsf(tb - sb) / sigma));
+        acc[0] += (double)(w * fabsf(pb - tb));
+        gmap[e] = w * sgnf(pb - tb) * inv;
+    }
+    block_partials<1>(acc, part);
+}
+
+__global__ void box_adjoint_kernel(const float* __restrict__ g, int N, int H, int W, int k, float* __restrict__ grad) {
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long n = (long long)N * H * W;
+    if (e >= n) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int i = (int)(r % H);
+    int nn = (int)(r / H);
+    grad[e] = box_mean(g, nn, i, j, H, W, k);  // symmetric window: adjoint == same box
+}
+
+// ---------------------------------------------------------------------------------------
+// ContrastRegionLoss (trainer.py:89-130)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(RB) void cr_loss_kernel(const float* __restrict__ p, const float* __restrict__ t,
+                                                     const float* __restrict__ s, int N, int H, int W, float thr,
+                                                     float* __restrict__ gq, double* part) {
+    // quantities: 0 region sum, 1 sum p, 2 sum p^2, 3 sum t, 4 sum t^2
+    double acc[5] = {0, 0, 0, 0, 0};
+    const int Hp = H / 8, Wp = W / 8;
+    const long long nq = (long long)N * Hp * Wp;
+    const long long n = (long long)N * H * W;
+    const float invq = nq > 0 ? 1.f / (float)nq : 0.f;
+    for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < n; e += (long long)gridDim.x * RB) {
+        float pv = p[e], tv = t[e];
+        acc[1] += pv; acc[2] += (double)pv * pv;
+        acc[3] += tv; acc[4] += (double)tv * tv;
+    }
+    for (long long q = (long long)blockIdx.x * RB + threadIdx.x; q < nq; q += (long long)gridDim.x * RB) {
+        int qx = (int)(q % Wp);
+        long long r = q / Wp;
+        int qy = (int)(r % Hp);
+        int nn = (int)(r / Hp);
+        float sp = 0.f, st = 0.f, ss = 0.f;
+        for (int a = 0; a < 8; ++a) {
+            long long row = ((long long)nn * H + qy * 8 + a) * W + qx * 8;
+            for (int b = 0; b < 8; ++b) { sp += p[row + b]; st += t[row + b]; ss += s[row + b]; }
+        }
+        sp /= 64.f; st /= 64.f; ss /= 64.f;
+        float m = sigmoidf_(5.f * ((st - ss) - thr));
+        acc[0] += (double)(m * fabsf(sp - st));
+        gq[q] = m * sgnf(sp - st) * invq;
+    }
+    block_partials<5>(acc, part);
+}
+
+__global__ void cr_loss_final(const double* part, int nb, long long n, long long nq, float weight, float* sc,
+                              float* out) {
+    if (threadIdx.x != 0) return;
+    double reg = sum_parts(part, nb, 0);
+    double s1 = sum_parts(part, nb, 1), s2 = sum_parts(part, nb, 2);
+    double t1 = sum_parts(part, nb, 3), t2 = sum_parts(part, nb, 4);
+    double mp = s1 / n, mt = t1 / n;
+    double sp = sqrt(fmax((s2 - n * mp * mp) / (n - 1), 0.0));
+    double st = sqrt(fmax((t2 - n * mt * mt) / (n - 1), 0.0));
+    double region = nq > 0 ? reg / nq : 0.0;
+    double v = weight * (region + 0.5 * (fabs(mp - mt) + fabs(sp - st)));
+    out[0] = (float)v;
+    sc[0] = (float)mp;
+    sc[1] = (float)sp;
+    // d/dp of 0.5*weight*(|mp-mt| + |sp-st|): a + b*(p - mp)
+    double sg1 = (mp > mt) ? 1.0 : ((mp < mt) ? -1.0 : 0.0);
+    double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
+    sc[2] = (float)(0.5 * weight * sg1 / n);
+    sc[3] = (float)(sp > 0 ? 0.5 * weight * sg2 / ((n - 1) * sp) : 0.0);
+}
+
+__global__ void cr_grad_kernel(const float* __restrict__ p, const float* __restrict__ gq, const float* __restrict__ sc,
+                               int N, int H, int W, float weight, float* __restrict__ grad) {
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long n = (long long)N * H * W;
+    if (e >= n) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int i = (int)(r % H);
+    int nn = (int)(r / H);
+    const int Hp = H / 8, Wp = W / 8;
+    float g = sc[2] + sc[3] * (p[e] - sc[0]);
+    if (i < Hp * 8 && j < Wp * 8) g += weight * gq[((long long)nn * Hp + i / 8) * Wp + j / 8] / 64.f;
+    grad[e] = g;
+}
+
+// ---------------------------------------------------------------------------------------
+// ContrastEdgeLoss (trainer.py:133-184): Sobel magnitude stats + exact top-10 % mean
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void sobel(const float* __restrict__ x, int nn, int i, int j, int H, int W, float& ex,
+                                      float& ey) {
+    float v[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            int ii = i + a - 1, jj = j + b - 1;
+            v[a][b] = (ii >= 0 && ii < H && jj >= 0 && jj < W) ? x[((long long)nn * H + ii) * W + jj] : 0.f;
+        }
+    // cross-correlation with Sx = [[-1,0,1],[-2,0,2],[-1,0,1]], Sy = Sx^T
+    ex = (-v[0][0] + v[0][2]) + (-2.f * v[1][0] + 2.f * v[1][2]) + (-v[2][0] + v[2][2]);
+    ey = (-v[0][0] - 2.f * v[0][1] - v[0][2]) + (v[2][0] + 2.f * v[2][1] + v[2][2]);
+}
+
+__global__ __launch_bounds__(RB) void edge_maps_kernel(const float* __restrict__ p, const float* __restrict__ t, int N,
+                                                       int H, int W, float* __restrict__ ep, float* __restrict__ et,
+                                                       double* part) {
+    double acc[4] = {0, 0, 0, 0};
+    const long long n = (long long)N * H * W;
+    for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < n; e += (long long)gridDim.x * RB) {
+        int j = (int)(e % W);
+        long long r = e / W;
+        int i = (int)(r % H);
+        int nn = (int)(r / H);
+        float ex, ey;
+        sobel(p, nn, i, j, H, W, ex, ey);
+        float a = sqrtf(ex * ex + ey * ey + 1e-6f);
+        sobel(t, nn, i, j, H, W, ex, ey);
+        float b = sqrtf(ex * ex + ey * ey + 1e-6f);
+        ep[e] = a;
+        et[e] = b;
+        acc[0] += a; acc[1] += (double)a * a;
+        acc[2] += b; acc[3] += (double)b * b;
+    }
+    block_partials<4>(acc, part);
+}
+
+// radix select of the k-th largest positive float: state st = {prefix, kleft, shift_done}
+__global__ void radix_init_kernel(unsigned* st, unsigned k, unsigned* hist) {
+    if (threadIdx.x == 0) { st[0] = 0u; st[1] = k; }
+    hist[threadIdx.x] = 0u;
+}
+
+__global__ __launch_bounds__(RB) void radix_hist_kernel(const float* __restrict__ x, long long n, int shift,
+                                                        const unsigned* __restrict__ st, unsigned* hist) {
+    __shared__ unsigned h[256];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    const unsigned prefix = st[0];
+    const unsigned himask = shift >= 24 ? 0u : (0xFFFFFFFFu << (shift + 8));
+    for (long long i = (long long)blockIdx.x * RB + threadIdx.x; i < n; i += (long long)gridDim.x * RB) {
+        unsigned u = __float_as_uint(x[i]);
+        if ((u & himask) == (prefix & himask)) atomicAdd(&h[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ void radix_select_kernel(unsigned* st, int shift, unsigned* hist) {
+    if (threadIdx.x == 0) {
+        unsigned k = st[1], cum = 0u;
+        int b = 255;
+        for (; b > 0; --b) {
+            if (cum + hist[b] >= k) break;
+            cum += hist[b];
+        }
+        st[0] |= ((unsigned)b << shift);
+        st[1] = k - cum;  // still to take from elements whose bits so far equal prefix
+    }
+    __syncthreads();
+    hist[threadIdx.x] = 0u;
+}
+
+// sum of elements > tau, count of elements == tau
+__global__ __launch_bounds__(RB) void topk_sum_kernel(const float* __restrict__ x, long long n,
+                                                      const unsigned* __restrict__ st, double* part) {
+    double acc[2] = {0.0, 0.0};
+    const float tau = __uint_as_float(st[0]);
+    for (long long i = (long long)blockIdx.x * RB + threadIdx.x; i < n; i += (long long)gridDim.x * RB) {
+        float v = x[i];
+        if (v > tau) acc[0] += v;
+        else if (v == tau) acc[1] += 1.0;
+    }
+    block_partials<2>(acc, part);
+}
+
+// stores in sc: [0]=tau_p [1]=kleft_p/cnt_eq_p [2..] coefficients
+__global__ void edge_final_kernel(const double* part_stats, int nb_stats, const double* part_tp, int nb_tp,
+                                  const double* part_tt, int nb_tt, const unsigned* st_p, const unsigned* st_t,
+                                  long long n, long long k, float* sc, float* out) {
+    if (threadIdx.x != 0) return;
+    double s1 = sum_parts(part_stats, nb_stats, 0), s2 = sum_parts(part_stats, nb_stats, 1);
+    double t1 = sum_parts(part_stats, nb_stats, 2), t2 = sum_parts(part_stats, nb_stats, 3);
+    double mp = s1 / n, mt = t1 / n;
+    double sp = sqrt(fmax((s2 - n * mp * mp) / (n - 1), 0.0));
+    double st = sqrt(fmax((t2 - n * mt * mt) / (n - 1), 0.0));
+    double taup = (double)__uint_as_float(st_p[0]), taut = (double)__uint_as_float(st_t[0]);
+    double tkp = (sum_parts(part_tp, nb_tp, 0) + (double)st_p[1] * taup) / (double)k;
+    double tkt = (sum_parts(part_tt, nb_tt, 0) + (double)st_t[1] * taut) / (double)k;
+    double eqp = sum_parts(part_tp, nb_tp, 1);
+    out[0] = (float)(fabs(mp - mt) + fabs(sp - st) + fabs(tkp - tkt));
+    double sg1 = (mp > mt) ? 1.0 : ((mp < mt) ? -1.0 : 0.0);
+    double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
+    double sg3 = (tkp > tkt) ? 1.0 : ((tkp < tkt) ? -1.0 : 0.0);
+    sc[0] = __uint_as_float(st_p[0]);
+    sc[1] = (float)(eqp > 0 ? (double)st_p[1] / eqp : 0.0);  // share of each tied element
+    sc[2] = (float)(sg1 / n);
+    sc[3] = (float)(sp > 0 ? sg2 / ((n - 1) * sp) : 0.0);
+    sc[4] = (float)mp;
+    sc[5] = (float)(sg3 / (double)k);
+}
+
+// gx = de * ex/e, gy = de * ey/e  (de = d loss / d edge_p)
+__global__ void edge_grad_maps_kernel(const float* __restrict__ p, const float* __restrict__ ep,
+                                      const float* __restrict__ sc, int N, int H, int W, float* __restrict__ gx,
+                                      float* __restrict__ gy) {
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long n = (long long)N * H * W;
+    if (e >= n) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int i = (int)(r % H);
+    int nn = (int)(r / H);
+    float v = ep[e];
+    float sel = v > sc[0] ? 1.f : (v == sc[0] ? sc[1] : 0.f);
+    float de = sc[2] + sc[3] * (v - sc[4]) + sc[5] * sel;
+    float ex, ey;
+    sobel(p, nn, i, j, H, W, ex, ey);
+    gx[e] = de * ex / v;
+    gy[e] = de * ey / v;
+}
+
+// adjoint of the zero-padded Sobel cross-correlations
+__global__ void edge_grad_kernel(const float* __restrict__ gx, const float* __restrict__ gy, int N, int H, int W,
+                                 float* __restrict__ grad) {
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long n = (long long)N * H * W;
+    if (e >= n) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int i = (int)(r % H);
+    int nn = (int)(r / H);
+    const float SX[3][3] = {{-1.f, 0.f, 1.f}, {-2.f, 0.f, 2.f}, {-1.f, 0.f, 1.f}};
+    const float SY[3][3] = {{-1.f, -2.f, -1.f}, {0.f, 0.f, 0.f}, {1.f, 2.f, 1.f}};
+    float g = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            int ii = i - a + 1, jj = j - b + 1;  // output position whose window holds (i,j) at (a,b)
+            if (ii >= 0 && ii < H && jj >= 0 && jj < W) {
+                long long o = ((long long)nn * H + ii) * W + jj;
+                g = fmaf(SX[a][b], gx[o], g);
+                g = fmaf(SY[a][b], gy[o], g);
+            }
+        }
+    grad[e] = g;
+}
+
+// ---------------------------------------------------------------------------------------
+// SSIM (pytorch_msssim.ssim, size_average=True, valid separable gaussian)
+// ---------------------------------------------------------------------------------------
+struct Gauss {
+    float g[16];
+};
+static Gauss make_gauss(int win, float sigma) {
+    Gauss G;
+    float s = 0.f;
+    for (int i = 0; i < win; ++i) {
+        float c = (float)i - (float)(win / 2);
+        G.g[i] = expf(-(c * c) / (2.f * sigma * sigma));
+        s += G.g[i];
+    }
+    for (int i = 0; i < win; ++i) G.g[i] /= s;
+    for (int i = win; i < 16; ++i) G.g[i] = 0.f;
+    return G;
+}
+
+// vertical valid pass of X, Y, XX, YY, XY -> V[5][N][Hv][W]
+__global__ void ssim_v_kernel(const float* __restrict__ X, const float* __restrict__ Y, int N, int H, int W, int win,
+                              Gauss G, float* __restrict__ V) {
+    const int Hv = H - win + 1;
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long tot = (long long)N * Hv * W;
+    if (e >= tot) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int i = (int)(r % Hv);
+    int nn = (int)(r / Hv);
+    float a[5] = {0, 0, 0, 0, 0};
+    for (int q = 0; q < win; ++q) {
+        long long o = ((long long)nn * H + i + q) * W + j;
+        float x = X[o], y = Y[o], g = G.g[q];
+        a[0] = fmaf(g, x, a[0]);
+        a[1] = fmaf(g, y, a[1]);
+        a[2] = fmaf(g, x * x, a[2]);
+        a[3] = fmaf(g, y * y, a[3]);
+        a[4] = fmaf(g, x * y, a[4]);
+    }
+#pragma unroll
+    for (int m = 0; m < 5; ++m) V[m * tot + e] = a[m];
+}
+
+// horizontal valid pass + ssim map + derivative maps D[3][N][Hv][Wv]
+__global__ __launch_bounds__(RB) void ssim_h_kernel(const float* __restrict__ V, int N, int H, int W, int win, Gauss G,
+                                                    float C1, float C2, float* __restrict__ D, double* part) {
+    const int Hv = H - win + 1, Wv = W - win + 1;
+    const long long totv = (long long)N * Hv * W;
+    const long long tot = (long long)N * Hv * Wv;
+    const float inv = 1.f / (float)tot;
+    double acc[1] = {0.0};
+    for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < tot; e += (long long)gridDim.x * RB) {
+        int j = (int)(e % Wv);
+        long long r = e / Wv;  // = nn*Hv + i
+        float m[5] = {0, 0, 0, 0, 0};
+        for (int q = 0; q < win; ++q) {
+            long long o = r * W + j + q;
+            float g = G.g[q];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) m[k] = fmaf(g, V[k * totv + o], m[k]);
+        }
+        float mu1 = m[0], mu2 = m[1];
+        float s11 = m[2] - mu1 * mu1, s22 = m[3] - mu2 * mu2, s12 = m[4] - mu1 * mu2;
+        float A = 2.f * mu1 * mu2 + C1, B = mu1 * mu1 + mu2 * mu2 + C1;
+        float Cc = 2.f * s12 + C2, Dd = s11 + s22 + C2;
+        float cs = Cc / Dd;
+        float s = (A / B) * cs;
+        acc[0] += s;
+        float BD = B * Dd;
+        D[e] = (2.f * mu2 * (Cc - A) / BD - s * 2.f * mu1 * (1.f / B - 1.f / Dd)) * inv;  // d/d mu1
+        D[tot + e] = (-s / Dd) * inv;                                                     // d/d E[XX]
+        D[2 * tot + e] = (2.f * A / BD) * inv;                                            // d/d E[XY]
+    }
+    block_partials<1>(acc, part);
+}
+
+__global__ void ssim_final(const double* part, int nb, long long tot, float* out) {
+    if (threadIdx.x == 0) out[0] = (float)(sum_parts(part, nb, 0) / (double)tot);
+}
+
+// adjoint horizontal: T[3][N][Hv][W] = sum_b g[b] D[.][i][v-b]
+__global__ void ssim_ht_kernel(const float* __restrict__ D, int N, int H, int W, int win, Gauss G,
+                               float* __restrict__ T) {
+    const int Hv = H - win + 1, Wv = W - win + 1;
+    const long long tot = (long long)N * Hv * Wv, totv = (long long)N * Hv * W;
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= totv) return;
+    int v = (int)(e % W);
+    long long r = e / W;
+    float a[3] = {0, 0, 0};
+    for (int b = 0; b < win; ++b) {
+        int jj = v - b;
+        if (jj < 0 || jj >= Wv) continue;
+        long long o = r * Wv + jj;
+        a[0] = fmaf(G.g[b], D[o], a[0]);
+        a[1] = fmaf(G.g[b], D[tot + o], a[1]);
+        a[2] = fmaf(G.g[b], D[2 * tot + o], a[2]);
+    }
+    T[e] = a[0];
+    T[totv + e] = a[1];
+    T[2 * totv + e] = a[2];
+}
+
+// adjoint vertical + chain rule: dX = R0 + 2 X R1 + Y R2
+__global__ void ssim_vt_kernel(const float* __restrict__ T, const float* __restrict__ X, const float* __restrict__ Y,
+                               int N, int H, int W, int win, Gauss G, float* __restrict__ grad) {
+    const int Hv = H - win + 1;
+    const long long totv = (long long)N * Hv * W;
+    long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long tot = (long long)N * H * W;
+    if (e >= tot) return;
+    int j = (int)(e % W);
+    long long r = e / W;
+    int u = (int)(r % H);
+    int nn = (int)(r / H);
+    float a[3] = {0, 0, 0};
+    for (int q = 0; q < win; ++q) {
+        int ii = u - q;
+        if (ii < 0 || ii >= Hv) continue;
+        long long o = ((long long)nn * Hv + ii) * W + j;
+        a[0] = fmaf(G.g[q], T[o], a[0]);
+        a[1] = fmaf(G.g[q], T[totv + o], a[1]);
+        a[2] = fmaf(G.g[q], T[2 * totv + o], a[2]);
+    }
+    grad[e] = a[0] + 2.f * X[e] * a[1] + Y[e] * a[2];
+}
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" size_t dcs_loss_workspace_size(int N, int H, int W) {
+    if (N <= 0 || H <= 0 || W <= 0) return 0;
+    size_t n = (size_t)N * H * W;
+    return loss_ws_fixed() + 10 * n * sizeof(float) + 4096;
+}
+
+#define LOSS_CHECK_WS(N, H, W)                                                        \
+    if (!ws || ws_bytes < dcs_loss_workspace_size(N, H, W))                           \
+        return fail(DCS_E_WORKSPACE, "loss: workspace too small");
+
+extern "C" int dcs_loss_l1(const float* pred, const float* target, int64_t n, float* out, float* grad, void* ws,
+                           size_t ws_bytes, void* stream) {
+    if (!pred || !target || !out || n <= 0) return fail(DCS_E_INVALID, "loss_l1: bad arguments");
+    if (!ws || ws_bytes < loss_ws_fixed()) return fail(DCS_E_WORKSPACE, "loss_l1: workspace too small");
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    int nb = red_blocks(n);
+    hipLaunchKernelGGL(pointwise_kernel<0>, dim3(nb), dim3(RB), 0, s, pred, target, 0.f, (long long)n, grad, w.part);
+    hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, w.part, nb, (long long)n, out);
+    return check_launch("loss_l1");
+}
+
+extern "C" int dcs_loss_mse(const float* pred, const float* target, int64_t n, float* out, float* grad, void* ws,
+                            size_t ws_bytes, void* stream) {
+    if (!pred || !target || !out || n <= 0) return fail(DCS_E_INVALID, "loss_mse: bad arguments");
+    if (!ws || ws_bytes < loss_ws_fixed()) return fail(DCS_E_WORKSPACE, "loss_mse: workspace too small");
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    int nb = red_blocks(n);
+    hipLaunchKernelGGL(pointwise_kernel<1>, dim3(nb), dim3(RB), 0, s, pred, target, 0.f, (long long)n, grad, w.part);
+    hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, w.part, nb, (long long)n, out);
+    return check_launch("loss_mse");
+}
+
+extern "C" int dcs_loss_mse_const(const float* pred, float target, int64_t n, float* out, float* grad, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    if (!pred || !out || n <= 0) return fail(DCS_E_INVALID, "loss_mse_const: bad arguments");
+    if (!ws || ws_bytes < loss_ws_fixed()) return fail(DCS_E_WORKSPACE, "loss_mse_const: workspace too small");
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    int nb = red_blocks(n);
+    hipLaunchKernelGGL(pointwise_kernel<2>, dim3(nb), dim3(RB), 0, s, pred, nullptr, target, (long long)n, grad, w.part);
+    hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, w.part, nb, (long long)n, out);
+    return check_launch("loss_mse_const");
+}
+
+extern "C" int dcs_loss_gradient(const float* pred, const float* target, int N, int H, int W, float* out, float* grad,
+                                 void* ws, size_t ws_bytes, void* stream) {
+    if (!pred || !target || !out || N <= 0 || H < 2 || W < 2) return fail(DCS_E_INVALID, "loss_gradient: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    long long n = (long long)N * H * W;
+    int nb = red_blocks(n);
+    hipLaunchKernelGGL(gradient_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, N, H, W, grad, w.part);
+    hipLaunchKernelGGL(gradient_loss_final, dim3(1), dim3(64), 0, s, w.part, nb, N, H, W, out);
+    return check_launch("loss_gradient");
+}
+
+extern "C" int dcs_loss_contrast_attention(const float* pred, const float* target, const float* source, int N, int H,
+                                           int W, float sigma, float min_w, float max_w, int k, float* out,
+                                           float* grad, void* ws, size_t ws_bytes, void* stream) {
+    if (!pred || !target || !source || !out || N <= 0 || H <= 0 || W <= 0 || k <= 0 || (k & 1) == 0)
+        return fail(DCS_E_INVALID, "loss_contrast_attention: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    long long n = (long long)N * H * W;
+    int nb = red_blocks(n);
+    float* gmap = w.maps;
+    hipLaunchKernelGGL(ca_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, source, N, H, W, sigma, min_w, max_w, k,
+                       gmap, w.part);
+    hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, w.part, nb, n, out);
+    if (grad)
+        hipLaunchKernelGGL(box_adjoint_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, gmap, N, H, W, k, grad);
+    return check_launch("loss_contrast_attention");
+}
+
+extern "C" int dcs_loss_contrast_region(const float* pred, const float* target, const float* source, int N, int H,
+                                        int W, float threshold, float weight, float* out, float* grad, void* ws,
+                                        size_t ws_bytes, void* stream) {
+    if (!pred || !target || !source || !out || N <= 0 || H <= 0 || W <= 0 || (long long)N * H * W < 2)
+        return fail(DCS_E_INVALID, "loss_contrast_region: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    long long n = (long long)N * H * W;
+    long long nq = (long long)N * (H / 8) * (W / 8);
+    int nb = red_blocks(n);
+    float* gq = w.maps;
+    hipLaunchKernelGGL(cr_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, source, N, H, W, threshold, gq, w.part);
+    hipLaunchKernelGGL(cr_loss_final, dim3(1), dim3(64), 0, s, w.part, nb, n, nq, weight, w.sc, out);
+    if (grad)
+        hipLaunchKernelGGL(cr_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, pred, gq, w.sc, N, H, W, weight,
+                           grad);
+    return check_launch("loss_contrast_region");
+}
+
+extern "C" int dcs_loss_contrast_edge(const float* pred, const float* target, int N, int H, int W, float* out,
+                                      float* grad, void* ws, size_t ws_bytes, void* stream) {
+    if (!pred || !target || !out || N <= 0 || H <= 0 || W <= 0) return fail(DCS_E_INVALID, "loss_contrast_edge: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    const long long n = (long long)N * H * W;
+    const long long k = (long long)((double)n * 0.1);  // int(numel * 0.1)
+    if (k < 1 || n < 2) return fail(DCS_E_INVALID, "loss_contrast_edge: too few elements for top-10%");
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    float* ep = w.maps;
+    float* et = ep + n;
+    float* gx = et + n;
+    float* gy = gx + n;
+    int nb = red_blocks(n);
+    double* part_stats = w.part;  // slots 0-3 of each block row
+    hipLaunchKernelGGL(edge_maps_kernel, dim3(nb), dim3(RB), 0, s, pred, target, N, H, W, ep, et, part_stats);
+    int e = check_launch("edge_maps");
+    if (e) return e;
+    unsigned* stp = w.st;
+    unsigned* stt = w.st + 4;
+    double* part_tp = w.part + 4;  // slots 4-5 of each block row (stats use 0-3)
+    double* part_tt = w.part + 6;  // slots 6-7
+    const float* srcs[2] = {ep, et};
+    unsigned* sts[2] = {stp, stt};
+    double* parts[2] = {part_tp, part_tt};
+    for (int q = 0; q < 2; ++q) {
+        hipLaunchKernelGGL(radix_init_kernel, dim3(1), dim3(256), 0, s, sts[q], (unsigned)k, w.hist);
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            hipLaunchKernelGGL(radix_hist_kernel, dim3(nb), dim3(RB), 0, s, srcs[q], n, shift, sts[q], w.hist);
+            hipLaunchKernelGGL(radix_select_kernel, dim3(1), dim3(256), 0, s, sts[q], shift, w.hist);
+        }
+        hipLaunchKernelGGL(topk_sum_kernel, dim3(nb), dim3(RB), 0, s, srcs[q], n, sts[q], parts[q]);
+    }
+    if ((e = check_launch("edge_topk"))) return e;
+    hipLaunchKernelGGL(edge_final_kernel, dim3(1), dim3(64), 0, s, part_stats, nb, part_tp, nb, part_tt, nb, stp, stt, n,
+                       k, w.sc, out);
+    if (grad) {
+        hipLaunchKernelGGL(edge_grad_maps_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, pred, ep, w.sc, N, H, W,
+                           gx, gy);
+        hipLaunchKernelGGL(edge_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, gx, gy, N, H, W, grad);
+    }
+    return check_launch("loss_contrast_edge");
+}
+
+extern "C" int dcs_loss_ssim(const float* X, const float* Y, int N, int H, int W, float data_range, int win,
+                             float sigma, float k1, float k2, float* out, float* grad, void* ws, size_t ws_bytes,
+                             void* stream) {
+    if (!X || !Y || !out || N <= 0 || win <= 0 || win > 16 || (win & 1) == 0 || H < win || W < win)
+        return fail(DCS_E_INVALID, "loss_ssim: bad arguments (H, W >= win required)");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    Gauss G = make_gauss(win, sigma);
+    const int Hv = H - win + 1, Wv = W - win + 1;
+    const long long totv = (long long)N * Hv * W, tot = (long long)N * Hv * Wv;
+    float* V = w.maps;            // 5 * totv
+    float* D = V + 5 * totv;      // 3 * tot
+    float* T = V;                 // reuse V for the adjoint pass (3 * totv)
+    const float C1 = (k1 * data_range) * (k1 * data_range), C2 = (k2 * data_range) * (k2 * data_range);
+    hipLaunchKernelGGL(ssim_v_kernel, dim3((unsigned)cdiv(totv, 256)), dim3(256), 0, s, X, Y, N, H, W, win, G, V);
+    int nb = red_blocks(tot);
+    hipLaunchKernelGGL(ssim_h_kernel, dim3(nb), dim3(RB), 0, s, V, N, H, W, win, G, C1, C2, D, w.part);
+    hipLaunchKernelGGL(ssim_final, dim3(1), dim3(64), 0, s, w.part, nb, tot, out);
+    if (grad) {
+        hipLaunchKernelGGL(ssim_ht_kernel, dim3((unsigned)cdiv(totv, 256)), dim3(256), 0, s, D, N, H, W, win, G, T);
+        hipLaunchKernelGGL(ssim_vt_kernel, dim3((unsigned)cdiv((long long)N * H * W, 256)), dim3(256), 0, s, T, X, Y, N,
+                           H, W, win, G, grad);
+    }
+    return check_launch("loss_ssim");
+}

@@ -1,0 +1,156 @@
+// Error state, Adam (torch.optim.Adam semantics, modules/trainer.py:360-362) and small utilities.
+#include "common.hpp"
+
+namespace dcs {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+// One launch over the flat parameter buffer of an optimizer.  Matches torch's Adam
+// (amsgrad=False, weight_decay=0):
+//   m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
+//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long long n, float lr, float b1, float b2, float eps,
+                            float bc1, float bc2) {
+    const float step_size = lr / bc1;
+    const float bc2s = sqrtf(bc2);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        float gi = g[i];
+        float mi = m[i];
+        mi = mi + (1.f - b1) * (gi - mi);
+        float vi = fmaf(v[i], b2, (1.f - b2) * gi * gi);
+        m[i] = mi;
+        v[i] = vi;
+        float denom = sqrtf(vi) / bc2s + eps;
+        p[i] = p[i] - step_size * (mi / denom);
+    }
+}
+
+__global__ void scale_add_kernel(float* __restrict__ y, const float* __restrict__ x, float a, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        y[i] = fmaf(a, x[i], y[i]);
+}
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" const char* dcs_last_error(void) { return g_last_error.c_str(); }
+extern "C" int dcs_version(void) { return 1; }
+
+extern "C" int dcs_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                             float beta2, float eps, float bias_c1, float bias_c2, void* stream) {
+    if (!p || !g || !m || !v || n < 0) return fail(DCS_E_INVALID, "adam: bad arguments");
+    if (n == 0) return DCS_OK;
+    long long blocks = cdiv(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, g, m, v, (long long)n,
+                       lr, beta1, beta2, eps, bias_c1, bias_c2);
+    return check_launch("adam");
+}
+
+extern "C" int dcs_scale_add(float* y, const float* x, float a, int64_t n, void* stream) {
+    if (!y || !x || n < 0) return fail(DCS_E_INVALID, "scale_add: bad arguments");
+    if (n == 0) return DCS_OK;
+    long long blocks = cdiv(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(scale_add_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), y, x, a, (long long)n);
+    return check_launch("scale_add");
+}
+
+namespace dcs {
+
+// dy = da * act'(y) for a = act(y) given the PRE-activation y (relu/lrelu), or given the
+// OUTPUT y for tanh (a = tanh(.), da/dpre = 1 - a^2).
+__global__ void act_backward_kernel(const float* __restrict__ da, const float* __restrict__ y,
+                                    float* __restrict__ dy, long long n, int act) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        float v = y[i];
+        float g = act == DCS_ACT_TANH ? (1.f - v * v) : act_grad(v, act);
+        dy[i] = da[i] * g;
+    }
+}
+
+// out = x * (*s)   (s a device scalar: loss backward without a host sync)
+__global__ void scale_dev_kernel(const float* __restrict__ x, const float* __restrict__ s, float* __restrict__ out,
+                                 long long n) {
+    const float a = s[0];
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = x[i] * a;
+}
+
+// per-channel sums of an [P][C] tensor: partials over pixel chunks, fixed-order finalize
+__global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* __restrict__ x, long long P, int C,
+                                                                  int nchunk, float* __restrict__ part) {
+    const int chunk = blockIdx.y;
+    const long long per = (P + nchunk - 1) / nchunk;
+    const long long p0 = chunk * per;
+    const long long p1 = min(P, p0 + per);
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+        float s = 0.f;
+        for (long long p = p0; p < p1; ++p) s += x[p * C + c];
+        part[(long long)chunk * C + c] = s;
+    }
+}
+
+__global__ void channel_sum_final_kernel(const float* __restrict__ part, int C, int nchunk, float* __restrict__ out) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int k = 0; k < nchunk; ++k) s += part[(long long)k * C + c];
+    out[c] = (float)s;
+}
+
+static inline int csum_chunks(long long P) {
+    long long c = cdiv(P, 256);
+    if (c > 1024) c = 1024;
+    if (c < 1) c = 1;
+    return (int)c;
+}
+
+}  // namespace dcs
+
+extern "C" int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, void* stream) {
+    if (!da || !y || !dy || n < 0) return fail(DCS_E_INVALID, "act_backward: bad arguments");
+    if (n == 0) return DCS_OK;
+    long long blocks = cdiv(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(act_backward_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), da, y, dy,
+                       (long long)n, act);
+    return check_launch("act_backward");
+}
+
+extern "C" int dcs_scale_dev(const float* x, const float* s, float* out, int64_t n, void* stream) {
+    if (!x || !s || !out || n < 0) return fail(DCS_E_INVALID, "scale_dev: bad arguments");
+    if (n == 0) return DCS_OK;
+    long long blocks = cdiv(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(scale_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), x, s, out,
+                       (long long)n);
+    return check_launch("scale_dev");
+}
+
+extern "C" size_t dcs_channel_sum_workspace_size(int64_t P, int C) {
+    if (P <= 0 || C <= 0) return 0;
+    return (size_t)csum_chunks(P) * C * sizeof(float);
+}
+
+extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, void* ws, size_t ws_bytes,
+                               void* stream) {
+    if (!x || !out || !ws || P <= 0 || C <= 0) return fail(DCS_E_INVALID, "channel_sum: bad arguments");
+    if (ws_bytes < dcs_channel_sum_workspace_size(P, C)) return fail(DCS_E_WORKSPACE, "channel_sum: workspace too small");
+    int nch = csum_chunks(P);
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(channel_sum_partial_kernel, dim3((unsigned)cdiv(C, 256), nch), dim3(256), 0, s, x,
+                       (long long)P, C, nch, reinterpret_cast<float*>(ws));
+    int e = check_launch("channel_sum_partial");
+    if (e) return e;
+    hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(ws), C, nch, out);
+    return check_launch("channel_sum_final");
+}

@@ -1,0 +1,283 @@
+// InstanceNorm2d(affine=False, track_running_stats=False) on NHWC fp32 tensors
+// (modules/model.py:61-63, 75-79, 94, 97, 110, 124): per-(n,c) statistics, apply (+ReLU/LReLU),
+// and the fused activation+IN backward.  All reductions are two-level (per-chunk partials,
+// then a fixed-order merge) and therefore deterministic.
+#include "common.hpp"
+
+namespace dcs {
+
+struct Part {  // one chunk's statistics of one (n,c)
+    float cnt, mean, m2, mx;
+    int amax;
+    int pad[3];
+};
+
+static inline int stats_chunks(int N, int HW) {
+    int want = (int)cdiv(1024, N);
+    int maxc = (int)cdiv(HW, 64);
+    int c = want < maxc ? want : maxc;
+    if (c < 1) c = 1;
+    return c;
+}
+
+// grid (N, nchunk); 256 threads.  Thread layout: if C <= 256 and 256 % C == 0 → C channels x
+// (256/C) pixel lanes; otherwise each thread owns channels tid, tid+256, ... (one pixel lane).
+__global__ __launch_bounds__(256) void in_stats_partial_kernel(const float* __restrict__ x, int HW, int C,
+                                                                int nchunk, Part* __restrict__ parts) {
+    const int n = blockIdx.x, chunk = blockIdx.y;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const int tid = threadIdx.x;
+    const bool packed = (C <= 256) && (256 % C == 0);
+    const int lanes = packed ? 256 / C : 1;
+    const int plane = packed ? tid / C : 0;
+    __shared__ float s_cnt[256], s_mean[256], s_m2[256], s_mx[256];
+    __shared__ int s_am[256];
+    const float* xb = x + (long long)n * HW * C;
+    for (int cbase = 0; cbase < C; cbase += (packed ? C : 256)) {
+        const int c = packed ? (tid % C) : (cbase + tid);
+        float cnt = 0.f, mean = 0.f, m2 = 0.f, mx = -INFINITY;
+        int am = 0;
+        if (c < C) {
+            float K = 0.f, s1 = 0.f, s2 = 0.f;
+            bool first = true;
+            for (int p = p0 + plane; p < p1; p += lanes) {
+                float v = xb[(long long)p * C + c];
+                if (first) { K = v; first = false; }
+                float dv = v - K;
+                s1 += dv;
+                s2 = fmaf(dv, dv, s2);
+                cnt += 1.f;
+                if (v > mx) { mx = v; am = p; }
+            }
+            if (cnt > 0.f) {
+                float d1 = s1 / cnt;
+                mean = K + d1;
+                m2 = fmaxf(s2 - s1 * d1, 0.f);
+            }
+        }
+        if (packed) {
+            s_cnt[tid] = cnt; s_mean[tid] = mean; s_m2[tid] = m2; s_mx[tid] = mx; s_am[tid] = am;
+            __syncthreads();
+            if (plane == 0) {
+                for (int l = 1; l < lanes; ++l) {
+                    int o = l * C + c;
+                    float nb = s_cnt[o];
+                    if (nb <= 0.f) continue;
+                    float na = cnt, tot = na + nb;
+                    float dl = s_mean[o] - mean;
+                    mean = mean + dl * (nb / tot);
+                    m2 = m2 + s_m2[o] + dl * dl * (na * nb / tot);
+                    cnt = tot;
+                    if (s_mx[o] > mx || (s_mx[o] == mx && s_am[o] < am)) { mx = s_mx[o]; am = s_am[o]; }
+                }
+                Part pt;
+                pt.cnt = cnt; pt.mean = mean; pt.m2 = m2; pt.mx = mx; pt.amax = am;
+                parts[((long long)n * nchunk + chunk) * C + c] = pt;
+            }
+            __syncthreads();
+        } else if (c < C) {
+            Part pt;
+            pt.cnt = cnt; pt.mean = mean; pt.m2 = m2; pt.mx = mx; pt.amax = am;
+            parts[((long long)n * nchunk + chunk) * C + c] = pt;
+        }
+    }
+}
+
+__global__ void in_stats_finalize_kernel(const Part* __restrict__ parts, int N, int C, int nchunk, float eps,
+                                         float* __restrict__ scale, float* __restrict__ shift,
+                                         float* __restrict__ xmax, int* __restrict__ xam) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * C) return;
+    int n = idx / C, c = idx - n * C;
+    double cnt = 0.0, mean = 0.0, m2 = 0.0;
+    float mx = -INFINITY;
+    int am = 0;
+    for (int k = 0; k < nchunk; ++k) {
+        Part p = parts[((long long)n * nchunk + k) * C + c];
+        if (p.cnt <= 0.f) continue;
+        double nb = p.cnt, tot = cnt + nb;
+        double dl = (double)p.mean - mean;
+        mean += dl * nb / tot;
+        m2 += (double)p.m2 + dl * dl * cnt * nb / tot;
+        cnt = tot;
+        if (p.mx > mx) { mx = p.mx; am = p.amax; }
+    }
+    double var = m2 / cnt;  // biased (InstanceNorm)
+    float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    scale[idx] = rstd;
+    shift[idx] = (float)(-mean) * rstd;
+    if (xmax) xmax[idx] = mx;
+    if (xam) xam[idx] = am;
+}
+
+template <bool V4>
+__global__ void in_apply_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                const float* __restrict__ sh, float* __restrict__ out, long long total, int HW,
+                                int C, int act) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (V4) {
+        long long e = i * 4;
+        if (e >= total) return;
+        int c = (int)(e % C);
+        long long n = e / ((long long)HW * C);
+        float4 v = reinterpret_cast<const float4*>(x)[i];
+        const float* s = sc + n * C + c;
+        const float* b = sh + n * C + c;
+        v.x = act_apply(fmaf(v.x, s[0], b[0]), act);
+        v.y = act_apply(fmaf(v.y, s[1], b[1]), act);
+        v.z = act_apply(fmaf(v.z, s[2], b[2]), act);
+        v.w = act_apply(fmaf(v.w, s[3], b[3]), act);
+        reinterpret_cast<float4*>(out)[i] = v;
+    } else {
+        if (i >= total) return;
+        int c = (int)(i % C);
+        long long n = i / ((long long)HW * C);
+        out[i] = act_apply(fmaf(x[i], sc[n * C + c], sh[n * C + c]), act);
+    }
+}
+
+// ---- backward of a = act(IN(y)) -------------------------------------------------------
+struct Sum2 {
+    float a, b;
+};
+
+__global__ __launch_bounds__(256) void in_bwd_partial_kernel(const float* __restrict__ da, const float* __restrict__ y,
+                                                             const float* __restrict__ sc, const float* __restrict__ sh,
+                                                             int HW, int C, int act, int nchunk,
+                                                             Sum2* __restrict__ parts) {
+    const int n = blockIdx.x, chunk = blockIdx.y;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const int tid = threadIdx.x;
+    const bool packed = (C <= 256) && (256 % C == 0);
+    const int lanes = packed ? 256 / C : 1;
+    const int plane = packed ? tid / C : 0;
+    __shared__ float s_a[256], s_b[256];
+    const long long base = (long long)n * HW * C;
+    for (int cbase = 0; cbase < C; cbase += (packed ? C : 256)) {
+        const int c = packed ? (tid % C) : (cbase + tid);
+        float sa = 0.f, sb = 0.f;
+        if (c < C) {
+            const float s = sc[n * C + c], b = sh[n * C + c];
+            for (int p = p0 + plane; p < p1; p += lanes) {
+                long long o = base + (long long)p * C + c;
+                float xh = fmaf(y[o], s, b);
+                float g = da[o] * act_grad(xh, act);
+                sa += g;
+                sb = fmaf(g, xh, sb);
+            }
+        }
+        if (packed) {
+            s_a[tid] = sa; s_b[tid] = sb;
+            __syncthreads();
+            if (plane == 0) {
+                for (int l = 1; l < lanes; ++l) { sa += s_a[l * C + c]; sb += s_b[l * C + c]; }
+                parts[((long long)n * nchunk + chunk) * C + c] = Sum2{sa, sb};
+            }
+            __syncthreads();
+        } else if (c < C) {
+            parts[((long long)n * nchunk + chunk) * C + c] = Sum2{sa, sb};
+        }
+    }
+}
+
+__global__ void in_bwd_finalize_kernel(Sum2* __restrict__ parts, int N, int C, int nchunk, int HW,
+                                       Sum2* __restrict__ coef) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * C) return;
+    int n = idx / C, c = idx - n * C;
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nchunk; ++k) {
+        Sum2 p = parts[((long long)n * nchunk + k) * C + c];
+        a += p.a;
+        b += p.b;
+    }
+    coef[idx] = Sum2{(float)(a / HW), (float)(b / HW)};
+}
+
+__global__ void in_bwd_apply_kernel(const float* __restrict__ da, const float* __restrict__ y,
+                                    const float* __restrict__ sc, const float* __restrict__ sh,
+                                    const Sum2* __restrict__ coef, float* __restrict__ dy, long long total, int HW,
+                                    int C, int act) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int c = (int)(i % C);
+    long long n = i / ((long long)HW * C);
+    long long nc = n * C + c;
+    float s = sc[nc], b = sh[nc];
+    float xh = fmaf(y[i], s, b);
+    float g = da[i] * act_grad(xh, act);
+    Sum2 k = coef[nc];
+    dy[i] = s * (g - k.a - xh * k.b);
+}
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" size_t dcs_in_stats_workspace_size(int N, int HW, int C) {
+    if (N <= 0 || HW <= 0 || C <= 0) return 0;
+    int nchunk = stats_chunks(N, HW);
+    size_t a = (size_t)N * nchunk * C * sizeof(Part);
+    size_t b = align_up((size_t)N * nchunk * C * sizeof(Sum2), 256) + (size_t)N * C * sizeof(Sum2);
+    return a > b ? a : b;
+}
+
+extern "C" int dcs_in_stats(const float* x, int N, int HW, int C, float eps, float* scale, float* shift,
+                            float* xmax, int32_t* xargmax, void* ws, size_t ws_bytes, void* stream) {
+    if (!x || !scale || !shift || !ws || N <= 0 || HW <= 0 || C <= 0)
+        return fail(DCS_E_INVALID, "in_stats: bad arguments");
+    if (ws_bytes < dcs_in_stats_workspace_size(N, HW, C)) return fail(DCS_E_WORKSPACE, "in_stats: workspace too small");
+    int nchunk = stats_chunks(N, HW);
+    hipStream_t s = as_stream(stream);
+    Part* parts = reinterpret_cast<Part*>(ws);
+    hipLaunchKernelGGL(in_stats_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, x, HW, C, nchunk, parts);
+    int e = check_launch("in_stats_partial");
+    if (e) return e;
+    hipLaunchKernelGGL(in_stats_finalize_kernel, dim3((unsigned)cdiv((long long)N * C, 256)), dim3(256), 0, s, parts,
+                       N, C, nchunk, eps, scale, shift, xmax, xargmax);
+    return check_launch("in_stats_finalize");
+}
+
+extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW, int C,
+                            int act, void* stream) {
+    if (!x || !scale || !shift || !out || N <= 0 || HW <= 0 || C <= 0)
+        return fail(DCS_E_INVALID, "in_apply: bad arguments");
+    long long total = (long long)N * HW * C;
+    hipStream_t s = as_stream(stream);
+    if (C % 4 == 0)
+        hipLaunchKernelGGL(in_apply_kernel<true>, dim3((unsigned)cdiv(total / 4, 256)), dim3(256), 0, s, x, scale,
+                           shift, out, total, HW, C, act);
+    else
+        hipLaunchKernelGGL(in_apply_kernel<false>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, x, scale, shift,
+                           out, total, HW, C, act);
+    return check_launch("in_apply");
+}
+
+extern "C" int dcs_in_act_backward(const float* da, const float* y, const float* scale, const float* shift, float* dy,
+                                   int N, int HW, int C, int act, void* ws, size_t ws_bytes, void* stream) {
+    if (!da || !y || !scale || !shift || !dy || !ws || N <= 0 || HW <= 0 || C <= 0)
+        return fail(DCS_E_INVALID, "in_act_backward: bad arguments");
+    if (ws_bytes < dcs_in_stats_workspace_size(N, HW, C))
+        return fail(DCS_E_WORKSPACE, "in_act_backward: workspace too small");
+    int nchunk = stats_chunks(N, HW);
+    hipStream_t s = as_stream(stream);
+    Sum2* parts = reinterpret_cast<Sum2*>(ws);
+    Sum2* coef = reinterpret_cast<Sum2*>(reinterpret_cast<char*>(ws) +
+                                         align_up((size_t)N * nchunk * C * sizeof(Sum2), 256));
+    hipLaunchKernelGGL(in_bwd_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, da, y, scale, shift, HW, C, act,
+                       nchunk, parts);
+    int e = check_launch("in_bwd_partial");
+    if (e) return e;
+    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((unsigned)cdiv((long long)N * C, 256)), dim3(256), 0, s, parts, N,
+                       C, nchunk, HW, coef);
+    e = check_launch("in_bwd_finalize");
+    if (e) return e;
+    long long total = (long long)N * HW * C;
+    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
+                       coef, dy, total, HW, C, act);
+    return check_launch("in_bwd_apply");
+}

@@ -1,0 +1,119 @@
+"""ctypes binding of the C-ABI in include/ducosy_hip.h (lib/libducosy_hip.so).
+
+The product path has no fallback: if the library is missing, importing the ops raises.
+Build it with ``make -C ducosy-gan_amd`` (or ``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p, c_char_p
+
+PKG_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+LIB_PATH = os.environ.get("DUCOSY_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libducosy_hip.so"))
+
+DCS_PAD_ZERO, DCS_PAD_REFLECT = 0, 1
+ACT_NONE, ACT_AFFINE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3, 4
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of dcs_conv_desc (include/ducosy_hip.h)."""
+    _fields_ = [
+        ("N", c_int32), ("Hs", c_int32), ("Ws", c_int32), ("Cs", c_int32),
+        ("s_n", c_int64), ("s_c", c_int64), ("s_h", c_int64), ("s_w", c_int64),
+        ("csplit", c_int32), ("pad0", c_int32),
+        ("s2_n", c_int64), ("s2_c", c_int64), ("s2_h", c_int64), ("s2_w", c_int64),
+        ("up", c_int32), ("pad_mode", c_int32),
+        ("KH", c_int32), ("KW", c_int32), ("pt", c_int32), ("pl", c_int32),
+        ("stride", c_int32), ("parity", c_int32),
+        ("Ho", c_int32), ("Wo", c_int32), ("Co", c_int32),
+        ("ldb", c_int32), ("pro_act", c_int32), ("epi_act", c_int32),
+    ]
+
+
+P = c_void_p
+DP = POINTER(ConvDesc)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "dcs_last_error": (c_char_p, []),
+    "dcs_version": (c_int, []),
+    "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "dcs_conv_rows": (c_int, [DP, P, P, P, P, P, P, P, P]),
+    "dcs_conv_wgrad_workspace_size": (c_size_t, [DP]),
+    "dcs_conv_wgrad": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
+    "dcs_reflect_fold": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "dcs_upsample2_grad": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    "dcs_in_stats_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "dcs_in_stats": (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P, P, c_size_t, P]),
+    "dcs_in_apply": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "dcs_in_act_backward": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "dcs_conv_rows_narrow": (c_int, [DP, P, P, P, P, P, P, P, P]),
+    "dcs_conv_wgrad_narrow_workspace_size": (c_size_t, [DP]),
+    "dcs_conv_wgrad_narrow": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
+    "dcs_cbam_forward": (c_int, [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 P, P, P, P, P, P]),
+    "dcs_cbam_backward_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "dcs_cbam_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, P, P, P, P, P, c_size_t, P]),
+    "dcs_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "dcs_loss_l1": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
+    "dcs_loss_mse": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
+    "dcs_loss_mse_const": (c_int, [P, c_float, c_int64, P, P, P, c_size_t, P]),
+    "dcs_loss_gradient": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),
+    "dcs_loss_contrast_attention": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, c_float,
+                                            c_int, P, P, P, c_size_t, P]),
+    "dcs_loss_contrast_region": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, P, P, P,
+                                         c_size_t, P]),
+    "dcs_loss_contrast_edge": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),
+    "dcs_loss_ssim": (c_int, [P, P, c_int, c_int, c_int, c_float, c_int, c_float, c_float, c_float,
+                              P, P, P, c_size_t, P]),
+    "dcs_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_float,
+                              c_float, P]),
+    "dcs_scale_add": (c_int, [P, P, c_float, c_int64, P]),
+    "dcs_scale_dev": (c_int, [P, P, P, c_int64, P]),
+    "dcs_act_backward": (c_int, [P, P, P, c_int64, c_int, P]),
+    "dcs_channel_sum_workspace_size": (c_size_t, [c_int64, c_int]),
+    "dcs_channel_sum": (c_int, [P, c_int64, c_int, P, P, c_size_t, P]),
+}
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the kernel library (once).  Raises loudly when it is missing: no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise HipLibraryError(
+            f"HIP kernel library not found at {LIB_PATH}; build it with `make -C {PKG_ROOT}`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return sorted(SIGNATURES)
+
+
+def call(name: str, *args) -> None:
+    """Call an int-returning entry point and raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.dcs_last_error()
+        raise HipLibraryError(f"{name} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))

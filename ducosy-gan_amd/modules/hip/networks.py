@@ -1,0 +1,348 @@
+"""Fused forward/backward of the Generator and Discriminator on the HIP kernels.
+
+Each network is ONE torch.autograd.Function whose forward walks the layers of
+modules/model.py:90-131 with the gfx950 kernels and keeps exactly what its hand-written
+backward needs.  Fusions relative to the reference's op-by-op eager graph:
+  * ReflectionPad / ZeroPad / nearest Upsample / channel concat are folded into the conv
+    gathers (never materialised);
+  * InstanceNorm(+ReLU/LeakyReLU) of a layer is applied in the NEXT conv's prologue, so a
+    conv output is written once (raw) and read once;
+  * biases of convs followed by InstanceNorm are not added (IN removes any per-channel
+    constant, so outputs are unchanged) and their gradient is exactly zero;
+  * the CBAM tail (channel MLP, spatial attention, residual add) is 3 kernels forward and
+    7 backward (modules/hip/ops.py cbam_*).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+from .lib import ACT_AFFINE, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, DCS_PAD_REFLECT, DCS_PAD_ZERO
+from .ops import ConvGeom, Src
+
+# ---------------------------------------------------------------------------------------
+# Generator (modules/model.py:90-115)
+# ---------------------------------------------------------------------------------------
+
+
+def gen_layers(cin: int, nb: int):
+    return {
+        "stem": ConvGeom(cin, 64, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT),
+        "down1": ConvGeom(64, 128, 3, 2, (1, 1, 1, 1), DCS_PAD_ZERO),
+        "down2": ConvGeom(128, 256, 3, 2, (1, 1, 1, 1), DCS_PAD_ZERO),
+        "res": ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT),
+        "up1": ConvGeom(256, 128, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2),
+        "up2": ConvGeom(128, 64, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2),
+        "head": ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT),
+    }
+
+
+def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
+    n = {"stem.w": "model.1.weight", "stem.b": "model.1.bias",
+         "down1.w": "model.4.weight", "down1.b": "model.4.bias",
+         "down2.w": "model.7.weight", "down2.b": "model.7.bias"}
+    for b in range(nb):
+        p = f"model.{10 + b}"
+        n[f"r{b}.c1.w"] = f"{p}.block.1.weight"
+        n[f"r{b}.c1.b"] = f"{p}.block.1.bias"
+        n[f"r{b}.c2.w"] = f"{p}.block.5.weight"
+        n[f"r{b}.c2.b"] = f"{p}.block.5.bias"
+        if use_cbam:
+            n[f"r{b}.fc1"] = f"{p}.cbam.channel_attention.fc.0.weight"
+            n[f"r{b}.fc2"] = f"{p}.cbam.channel_attention.fc.2.weight"
+            n[f"r{b}.sa"] = f"{p}.cbam.spatial_attention.conv.weight"
+    u = 10 + nb
+    n.update({"up1.w": f"model.{u + 1}.weight", "up1.b": f"model.{u + 1}.bias",
+              "up2.w": f"model.{u + 5}.weight", "up2.b": f"model.{u + 5}.bias",
+              "head.w": f"model.{u + 9}.weight", "head.b": f"model.{u + 9}.bias"})
+    return n
+
+
+class _Block:
+    __slots__ = ("x", "y1", "s1", "y2", "s2", "cb")
+
+
+def _res_block_forward(L, W, b, x, use_cbam, keep):
+    """One ResidualBlock[WithCBAM] (modules/model.py:56-87) on NHWC x."""
+    res = L["res"]
+    y1 = res.forward(Src.nhwc(x), W["pk"][f"r{b}.c1.w"])
+    s1 = ops.in_stats(y1)
+    y2 = res.forward(Src.nhwc(y1), W["pk"][f"r{b}.c2.w"], pro=(s1.scale, s1.shift, ACT_RELU))
+    s2 = ops.in_stats(y2, want_max=use_cbam)
+    cb = None
+    if use_cbam:
+        w1, w2, wsa = W[f"r{b}.fc1"], W[f"r{b}.fc2"], W[f"r{b}.sa"]
+        out, cb = ops.cbam_forward(x, y2, s2, w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1),
+                                   wsa.reshape(2, wsa.shape[-2], wsa.shape[-1]))
+    else:
+        out = ops.in_apply(y2, s2, ACT_AFFINE)
+        ops.scale_add_(out, x)
+    blk = None
+    if keep:
+        blk = _Block()
+        blk.x, blk.y1, blk.s1, blk.y2, blk.s2, blk.cb = x, y1, s1, y2, s2, cb
+    return out, blk
+
+
+def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
+    res = L["res"]
+    if use_cbam:
+        w1, w2, wsa = W[f"r{b}.fc1"], W[f"r{b}.fc2"], W[f"r{b}.sa"]
+        dy2, dw1, dw2, dwsa = ops.cbam_backward(
+            dout, blk.y2, blk.s2, w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1),
+            wsa.reshape(2, wsa.shape[-2], wsa.shape[-1]), blk.cb)
+        grads[f"r{b}.fc1"] = dw1.view_as(w1)
+        grads[f"r{b}.fc2"] = dw2.view_as(w2)
+        grads[f"r{b}.sa"] = dwsa.view_as(wsa)
+    else:
+        dy2 = ops.in_act_backward(dout, blk.y2, blk.s2, ACT_AFFINE)
+    H, Wd = blk.x.shape[1], blk.x.shape[2]
+    grads[f"r{b}.c2.w"] = res.wgrad(dy2, Src.nhwc(blk.y1), pro=(blk.s1.scale, blk.s1.shift, ACT_RELU))
+    da1 = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd)
+    dy1 = ops.in_act_backward(da1, blk.y1, blk.s1, ACT_RELU)
+    del da1
+    grads[f"r{b}.c1.w"] = res.wgrad(dy1, Src.nhwc(blk.x))
+    # residual: dx = dout + dgrad(conv1)
+    return res.dgrad(dy1, res.pack_dgrad(W[f"r{b}.c1.w"]), H, Wd, addend=dout)
+
+
+def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[torch.Tensor],
+                      nb: int, use_cbam: bool, keep: bool):
+    """x: NCHW image (or full concat input); x2: optional NCHW mask channels (concat fused).
+    Returns (out [N,1,H,W], saved or None)."""
+    cin = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
+    L = gen_layers(cin, nb)
+    W = dict(W)
+    W["pk"] = pk = {}
+    for name in ("stem", "down1", "down2", "up1", "up2", "head"):
+        pk[f"{name}.w"] = L[name].pack_fwd(W[f"{name}.w"])
+    for b in range(nb):
+        pk[f"r{b}.c1.w"] = L["res"].pack_fwd(W[f"r{b}.c1.w"])
+        pk[f"r{b}.c2.w"] = L["res"].pack_fwd(W[f"r{b}.c2.w"])
+    xs = Src.nchw(x, x2)
+    N, H, Wd = xs.N, xs.H, xs.W
+    y0 = L["stem"].forward(xs, pk["stem.w"])
+    s0 = ops.in_stats(y0)
+    y1 = L["down1"].forward(Src.nhwc(y0), pk["down1.w"], pro=(s0.scale, s0.shift, ACT_RELU))
+    s1 = ops.in_stats(y1)
+    y2 = L["down2"].forward(Src.nhwc(y1), pk["down2.w"], pro=(s1.scale, s1.shift, ACT_RELU))
+    s2 = ops.in_stats(y2)
+    h = ops.in_apply(y2, s2, ACT_RELU)
+    blocks = []
+    for b in range(nb):
+        h, blk = _res_block_forward(L, W, b, h, use_cbam, keep)
+        blocks.append(blk)
+    yu1 = L["up1"].forward(Src.nhwc(h), pk["up1.w"])
+    su1 = ops.in_stats(yu1)
+    yu2 = L["up2"].forward(Src.nhwc(yu1), pk["up2.w"], pro=(su1.scale, su1.shift, ACT_RELU))
+    su2 = ops.in_stats(yu2)
+    out = L["head"].forward(Src.nhwc(yu2), pk["head.w"], bias=W["head.b"],
+                            pro=(su2.scale, su2.shift, ACT_RELU), epi_act=ACT_TANH)
+    out = out.view(N, 1, H, Wd)
+    saved = None
+    if keep:
+        saved = dict(L=L, W=W, xs=xs, y0=y0, s0=s0, y1=y1, s1=s1, y2=y2, s2=s2, blocks=blocks, h=h,
+                     yu1=yu1, su1=su1, yu2=yu2, su2=su2, nb=nb, use_cbam=use_cbam)
+    return out, saved
+
+
+def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int):
+    """Returns (dx NHWC [N,H,W,dx_channels] or None, grads dict keyed like gen_param_names)."""
+    L, W = S["L"], S["W"]
+    nb, use_cbam = S["nb"], S["use_cbam"]
+    grads: Dict[str, torch.Tensor] = {}
+    N, _, H, Wd = dout.shape
+    dout = dout.contiguous()
+    # head: tanh backward, bias, wgrad, dgrad
+    dpre = ops.act_backward(dout, S["out"], ACT_TANH).view(N, H, Wd, 1)
+    grads["head.b"] = ops.channel_sum(dpre)
+    su2, su1 = S["su2"], S["su1"]
+    grads["head.w"] = L["head"].wgrad(dpre, Src.nhwc(S["yu2"]), pro=(su2.scale, su2.shift, ACT_RELU))
+    da = L["head"].dgrad(dpre, L["head"].pack_dgrad(W["head.w"]), H, Wd)
+    del dpre
+    # up2
+    dy = ops.in_act_backward(da, S["yu2"], su2, ACT_RELU)
+    grads["up2.w"] = L["up2"].wgrad(dy, Src.nhwc(S["yu1"]), pro=(su1.scale, su1.shift, ACT_RELU))
+    da = L["up2"].dgrad(dy, L["up2"].pack_dgrad(W["up2.w"]), H // 2, Wd // 2)
+    # up1
+    dy = ops.in_act_backward(da, S["yu1"], su1, ACT_RELU)
+    grads["up1.w"] = L["up1"].wgrad(dy, Src.nhwc(S["h"]))
+    dh = L["up1"].dgrad(dy, L["up1"].pack_dgrad(W["up1.w"]), H // 4, Wd // 4)
+    del dy, da
+    # residual blocks
+    for b in reversed(range(nb)):
+        dh = _res_block_backward(L, W, b, S["blocks"][b], dh, use_cbam, grads)
+        S["blocks"][b] = None
+    # x0 = relu(IN(y2))
+    s2, s1, s0 = S["s2"], S["s1"], S["s0"]
+    dy = ops.in_act_backward(dh, S["y2"], s2, ACT_RELU)
+    grads["down2.w"] = L["down2"].wgrad(dy, Src.nhwc(S["y1"]), pro=(s1.scale, s1.shift, ACT_RELU))
+    da = L["down2"].dgrad(dy, L["down2"].pack_dgrad(W["down2.w"]), H // 2, Wd // 2)
+    dy = ops.in_act_backward(da, S["y1"], s1, ACT_RELU)
+    grads["down1.w"] = L["down1"].wgrad(dy, Src.nhwc(S["y0"]), pro=(s0.scale, s0.shift, ACT_RELU))
+    da = L["down1"].dgrad(dy, L["down1"].pack_dgrad(W["down1.w"]), H, Wd)
+    dy = ops.in_act_backward(da, S["y0"], s0, ACT_RELU)
+    del da
+    grads["stem.w"] = L["stem"].wgrad(dy, S["xs"])
+    dx = None
+    if need_dx:
+        stem = L["stem"]
+        dx = stem.dgrad(dy, stem.pack_dgrad(W["stem.w"], dx_channels), H, Wd, ci_count=dx_channels)
+    # biases feeding an InstanceNorm: exact zero gradient
+    for key in ("stem.b", "down1.b", "down2.b", "up1.b", "up2.b"):
+        grads[key] = torch.zeros_like(W[key])
+    for b in range(nb):
+        grads[f"r{b}.c1.b"] = torch.zeros_like(W[f"r{b}.c1.b"])
+        grads[f"r{b}.c2.b"] = torch.zeros_like(W[f"r{b}.c2.b"])
+    return dx, grads
+
+
+class GeneratorFunction(torch.autograd.Function):
+    """out = Generator(x [, x2]) with a fused hand-written backward."""
+
+    @staticmethod
+    def forward(ctx, x, x2, cfg, *params):
+        keys, nb, use_cbam = cfg
+        W = dict(zip(keys, params))
+        keep = any(ctx.needs_input_grad)
+        out, saved = generator_forward(W, x, x2, nb, use_cbam, keep)
+        ctx.saved = saved
+        if keep:
+            ctx.save_for_backward(out)  # tanh backward needs the output (no ctx attribute cycle)
+        ctx.keys = keys
+        ctx.x_channels = x.shape[1]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        S = ctx.saved
+        S["out"] = ctx.saved_tensors[0]
+        need_dx = ctx.needs_input_grad[0]
+        dx_nhwc, grads = generator_backward(S, dout, need_dx, ctx.x_channels)
+        ctx.saved = None
+        dx = None
+        if need_dx:
+            dx = dx_nhwc.permute(0, 3, 1, 2)
+            if ctx.x_channels > 1:
+                dx = dx.contiguous()
+        dparams = [grads[k] if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(ctx.keys)]
+        return (dx, None, None, *dparams)
+
+
+# ---------------------------------------------------------------------------------------
+# Discriminator (modules/model.py:118-131)
+# ---------------------------------------------------------------------------------------
+
+def disc_layers(cin: int):
+    return [ConvGeom(cin, 64, 4, 2, (1, 1, 1, 1)), ConvGeom(64, 128, 4, 2, (1, 1, 1, 1)),
+            ConvGeom(128, 256, 4, 2, (1, 1, 1, 1)), ConvGeom(256, 512, 4, 2, (1, 1, 1, 1)),
+            ConvGeom(512, 1, 4, 1, (2, 2, 1, 1))]  # ZeroPad2d((1,0,1,0)) + padding=1
+
+
+DISC_KEYS = ["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias", "model.5.weight",
+             "model.5.bias", "model.8.weight", "model.8.bias", "model.12.weight", "model.12.bias"]
+
+
+def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: bool):
+    L = disc_layers(x.shape[1])
+    ws = params[0::2]
+    bs = params[1::2]
+    pk = [g.pack_fwd(w) for g, w in zip(L, ws)]
+    N = x.shape[0]
+    dev = x.device
+    xs = Src.nchw(x)
+    # layer 0: conv + bias; its LeakyReLU is the next conv's prologue (scale 1, shift 0)
+    y0 = L[0].forward(xs, pk[0], bias=bs[0])
+    ones = torch.ones(N, 64, device=dev, dtype=torch.float32)
+    zeros = torch.zeros(N, 64, device=dev, dtype=torch.float32)
+    ys, sts = [y0], [ops.INStats(ones, zeros)]
+    h = y0
+    for i in (1, 2, 3):
+        st = sts[-1]
+        h = L[i].forward(Src.nhwc(h), pk[i], pro=(st.scale, st.shift, ACT_LRELU))
+        ys.append(h)
+        sts.append(ops.in_stats(h))
+    st = sts[-1]
+    out = L[4].forward(Src.nhwc(h), pk[4], bias=bs[4], pro=(st.scale, st.shift, ACT_LRELU))
+    H4, W4 = out.shape[1], out.shape[2]
+    out = out.view(N, 1, H4, W4)
+    saved = dict(L=L, ws=ws, xs=xs, ys=ys, sts=sts) if keep else None
+    return out, saved
+
+
+def discriminator_backward(S, dout, need_dx, need_w):
+    L, ws, ys, sts = S["L"], S["ws"], S["ys"], S["sts"]
+    N, _, H4, W4 = dout.shape
+    d = dout.contiguous().view(N, H4, W4, 1)
+    grads = [None] * 10
+    if need_w:
+        grads[9] = ops.channel_sum(d)
+        st = sts[3]
+        grads[8] = L[4].wgrad(d, Src.nhwc(ys[3]), pro=(st.scale, st.shift, ACT_LRELU))
+    da = L[4].dgrad(d, L[4].pack_dgrad(ws[4]), ys[3].shape[1], ys[3].shape[2])
+    for i in (3, 2, 1):
+        dy = ops.in_act_backward(da, ys[i], sts[i], ACT_LRELU)
+        if need_w:
+            st = sts[i - 1]
+            grads[2 * i] = L[i].wgrad(dy, Src.nhwc(ys[i - 1]), pro=(st.scale, st.shift, ACT_LRELU))
+            grads[2 * i + 1] = torch.zeros(L[i].cout, device=d.device, dtype=torch.float32)
+        da = L[i].dgrad(dy, L[i].pack_dgrad(ws[i]), ys[i - 1].shape[1], ys[i - 1].shape[2])
+    # layer 0: y0 includes the bias; a0 = lrelu(y0)
+    dy0 = ops.act_backward(da, ys[0], ACT_LRELU)
+    if need_w:
+        grads[1] = ops.channel_sum(dy0)
+        grads[0] = L[0].wgrad(dy0, S["xs"])
+    dx = None
+    if need_dx:
+        xs = S["xs"]
+        dx = L[0].dgrad(dy0, L[0].pack_dgrad(ws[0]), xs.H, xs.W)
+    return dx, grads
+
+
+class DiscriminatorFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *params):
+        keep = any(ctx.needs_input_grad)
+        out, saved = discriminator_forward(list(params), x, keep)
+        ctx.saved = saved
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        need_dx = ctx.needs_input_grad[0]
+        need_w = any(ctx.needs_input_grad[1:])
+        dx, grads = discriminator_backward(ctx.saved, dout, need_dx, need_w)
+        ctx.saved = None
+        if dx is not None:
+            dx = dx.permute(0, 3, 1, 2)
+            if dx.shape[1] > 1:
+                dx = dx.contiguous()
+        return (dx, *[g if ctx.needs_input_grad[1 + i] else None for i, g in enumerate(grads)])
+
+
+class ResBlockFunction(torch.autograd.Function):
+    """Standalone ResidualBlock[WithCBAM] (modules/model.py:56-87) on an NCHW tensor."""
+
+    @staticmethod
+    def forward(ctx, x, use_cbam, keys, *params):
+        W = dict(zip(keys, params))
+        L = {"res": ConvGeom(x.shape[1], x.shape[1], 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT)}
+        W["pk"] = {"r0.c1.w": L["res"].pack_fwd(W["r0.c1.w"]), "r0.c2.w": L["res"].pack_fwd(W["r0.c2.w"])}
+        xh = x.permute(0, 2, 3, 1).contiguous()
+        keep = any(ctx.needs_input_grad)
+        out, blk = _res_block_forward(L, W, 0, xh, use_cbam, keep)
+        ctx.state = (L, W, blk, use_cbam, keys) if keep else None
+        return out.permute(0, 3, 1, 2).contiguous()
+
+    @staticmethod
+    def backward(ctx, dout):
+        L, W, blk, use_cbam, keys = ctx.state
+        grads = {}
+        dx = _res_block_backward(L, W, 0, blk, dout.permute(0, 2, 3, 1).contiguous(), use_cbam, grads)
+        grads["r0.c1.b"] = torch.zeros_like(W["r0.c1.b"])
+        grads["r0.c2.b"] = torch.zeros_like(W["r0.c2.b"])
+        ctx.state = None
+        return (dx.permute(0, 3, 1, 2).contiguous(), None, None,
+                *[grads[k] if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(keys)])

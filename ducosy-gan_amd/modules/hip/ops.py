@@ -1,0 +1,441 @@
+"""Tensor-level wrappers over the C-ABI (device pointers, shapes, workspaces, streams).
+
+PyTorch is plumbing here: it owns device memory (caching allocator) and the stream; every
+arithmetic op on the hot path is one of the hand-written gfx950 kernels behind lib.py.
+Activations are NHWC fp32 contiguous tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import lib
+from .lib import ACT_AFFINE, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, DCS_PAD_REFLECT, DCS_PAD_ZERO
+
+IN_EPS = 1e-5
+
+
+def _p(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None:
+            if not t.is_cuda:
+                raise RuntimeError("ducosy HIP ops require device tensors (no CPU fallback)")
+            if t.dtype not in (torch.float32, torch.int32, torch.uint8):
+                raise RuntimeError(f"unsupported dtype {t.dtype}")
+
+
+# ---------------------------------------------------------------------------------------
+# workspace
+# ---------------------------------------------------------------------------------------
+_WS = {}
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Scratch buffer reused across calls (stream-ordered reuse is safe on one stream)."""
+    nbytes = max(int(nbytes), 256)
+    key = torch.device(device).index
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        size = max(nbytes, int(buf.numel() * 1.5) if buf is not None else 0)
+        buf = torch.empty(size, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+# ---------------------------------------------------------------------------------------
+# convolution geometry
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Src:
+    """A gathered operand: logical [N, H, W, C] with element strides; optional second
+    tensor supplying channels >= csplit (channel concat fused into the gather)."""
+    t: torch.Tensor
+    N: int
+    H: int
+    W: int
+    C: int
+    strides: Tuple[int, int, int, int]  # (n, c, h, w)
+    t2: Optional[torch.Tensor] = None
+    strides2: Tuple[int, int, int, int] = (0, 0, 0, 0)
+    csplit: Optional[int] = None
+
+    @staticmethod
+    def nhwc(t: torch.Tensor) -> "Src":
+        N, H, W, C = t.shape
+        return Src(t, N, H, W, C, (H * W * C, 1, W * C, C))
+
+    @staticmethod
+    def nchw(t: torch.Tensor, t2: Optional[torch.Tensor] = None) -> "Src":
+        """NCHW tensor (any strides), optionally concatenated with t2 along channels."""
+        N, C, H, W = t.shape
+        sn, sc, sh, sw = t.stride()
+        if t2 is None:
+            return Src(t, N, H, W, C, (sn, sc, sh, sw))
+        N2, C2, H2, W2 = t2.shape
+        assert (N2, H2, W2) == (N, H, W)
+        return Src(t, N, H, W, C + C2, (sn, sc, sh, sw), t2, tuple(t2.stride()), C)
+
+
+BN_MAX = 128
+
+
+def _bn_for(co: int) -> int:
+    return 128 if co > 64 else 64
+
+
+@dataclass
+class ConvGeom:
+    """One nn.Conv2d of the reference with its padding module folded in."""
+    cin: int
+    cout: int
+    k: int
+    stride: int = 1
+    pads: Tuple[int, int, int, int] = (0, 0, 0, 0)  # top, left, bottom, right
+    pad_mode: int = DCS_PAD_ZERO
+    up: int = 1  # nearest upsampling of the input before the conv
+
+    def out_hw(self, H, W):
+        Hv, Wv = H * self.up, W * self.up
+        t, l, b, r = self.pads
+        return (Hv + t + b - self.k) // self.stride + 1, (Wv + l + r - self.k) // self.stride + 1
+
+    @property
+    def narrow(self):
+        return self.cout <= 4
+
+    # ---- weight packing ------------------------------------------------------------
+    def pack_fwd(self, w: torch.Tensor) -> torch.Tensor:
+        K = self.k * self.k * self.cin
+        if self.narrow:
+            Kpad, ldb = K, (1 if self.cout == 1 else 4)
+        else:
+            Kpad, ldb = _round_up(K, 32), _round_up(self.cout, _bn_for(self.cout))
+        out = torch.empty(Kpad, ldb, device=w.device, dtype=torch.float32)
+        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, 0, self.cin, Kpad,
+                 ldb, _p(out), _stream())
+        return out
+
+    def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
+        ci = self.cin if ci_count is None else ci_count
+        kind = 2 if self.stride == 2 else 1
+        K = self.k * self.k * self.cout
+        if ci <= 4:
+            Kpad, ldb = K, (1 if ci == 1 else 4)
+        else:
+            Kpad, ldb = _round_up(K, 32), _round_up(ci, _bn_for(ci))
+        out = torch.empty(Kpad, ldb, device=w.device, dtype=torch.float32)
+        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci, Kpad, ldb,
+                 _p(out), _stream())
+        return out
+
+    # ---- descriptors ---------------------------------------------------------------
+    def _desc_fwd(self, s: Src, ldb: int, pro_act: int, epi_act: int) -> lib.ConvDesc:
+        Ho, Wo = self.out_hw(s.H, s.W)
+        d = lib.ConvDesc()
+        d.N, d.Hs, d.Ws, d.Cs = s.N, s.H, s.W, s.C
+        d.s_n, d.s_c, d.s_h, d.s_w = s.strides
+        d.csplit = s.C if s.csplit is None else s.csplit
+        d.s2_n, d.s2_c, d.s2_h, d.s2_w = s.strides2
+        d.up, d.pad_mode = self.up, self.pad_mode
+        d.KH = d.KW = self.k
+        d.pt, d.pl = self.pads[0], self.pads[1]
+        d.stride, d.parity = self.stride, 0
+        d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
+        d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
+        return d
+
+    # ---- forward -------------------------------------------------------------------
+    def forward(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
+                epi_act: int = ACT_NONE) -> torch.Tensor:
+        assert s.C == self.cin, (s.C, self.cin)
+        _check_dev(s.t, s.t2, wpack, bias)
+        Ho, Wo = self.out_hw(s.H, s.W)
+        pro_act = pro[2] if pro is not None else ACT_NONE
+        d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
+        out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
+        fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
+        lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
+                 _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
+        return out
+
+    # ---- data gradient ---------------------------------------------------------------
+    def dgrad(self, dy: torch.Tensor, wpack_d: torch.Tensor, H: int, W: int,
+              ci_count: Optional[int] = None, addend: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """dL/d(input) [N,H,W,ci] (NHWC) of this conv given dy [N,Ho,Wo,cout] (NHWC)."""
+        _check_dev(dy, wpack_d, addend)
+        N, Ho, Wo, Co = dy.shape
+        assert Co == self.cout
+        ci = self.cin if ci_count is None else ci_count
+        narrow = ci <= 4
+        fn = "dcs_conv_rows_narrow" if narrow else "dcs_conv_rows"
+        d = lib.ConvDesc()
+        d.N, d.Hs, d.Ws, d.Cs = N, Ho, Wo, Co
+        d.s_n, d.s_c, d.s_h, d.s_w = Ho * Wo * Co, 1, Wo * Co, Co
+        d.csplit = Co
+        d.up, d.pad_mode = 1, DCS_PAD_ZERO
+        d.KH = d.KW = self.k
+        d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
+        d.Co = ci
+        dev = dy.device
+        t, l, b, r = self.pads
+        if self.stride == 2:
+            assert self.up == 1 and self.pad_mode == DCS_PAD_ZERO
+            d.stride, d.parity, d.pt, d.pl = 2, 1, t, l
+            d.Ho, d.Wo = H, W
+            out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
+            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out),
+                     _stream())
+            if addend is not None:
+                lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
+            return out
+        d.stride, d.parity = 1, 0
+        Hv, Wv = H * self.up, W * self.up
+        if self.pad_mode == DCS_PAD_REFLECT:
+            assert self.up == 1 and t == b and l == r and t == l
+            p = t
+            d.pt = d.pl = self.k - 1
+            d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
+            dpad = torch.empty(N, d.Ho, d.Wo, ci, device=dev, dtype=torch.float32)
+            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad),
+                     _stream())
+            out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
+            lib.call("dcs_reflect_fold", _p(dpad), _p(addend), _p(out), N, H, W, ci, p, _stream())
+            return out
+        d.pt, d.pl = self.k - 1 - t, self.k - 1 - l
+        d.Ho, d.Wo = Hv, Wv
+        dv = torch.empty(N, Hv, Wv, ci, device=dev, dtype=torch.float32)
+        lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dv), _stream())
+        if self.up == 2:
+            out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
+            lib.call("dcs_upsample2_grad", _p(dv), _p(out), N, H, W, ci, _stream())
+        else:
+            out = dv
+        if addend is not None:
+            lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
+        return out
+
+    # ---- weight gradient ---------------------------------------------------------------
+    def wgrad(self, dy: torch.Tensor, s: Src,
+              pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """dL/dW in torch's OIHW layout."""
+        _check_dev(dy, s.t, s.t2)
+        pro_act = pro[2] if pro is not None else ACT_NONE
+        d = self._desc_fwd(s, 0, pro_act, ACT_NONE)
+        assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)
+        if out is None:
+            out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device,
+                              dtype=torch.float32)
+        if self.narrow:
+            nb = lib.query("dcs_conv_wgrad_narrow_workspace_size", ctypes.byref(d))
+            ws = workspace(nb, dy.device)
+            lib.call("dcs_conv_wgrad_narrow", ctypes.byref(d), _p(dy), _p(s.t), _p(s.t2),
+                     _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _p(ws),
+                     ws.numel(), _stream())
+        else:
+            nb = lib.query("dcs_conv_wgrad_workspace_size", ctypes.byref(d))
+            ws = workspace(nb, dy.device)
+            lib.call("dcs_conv_wgrad", ctypes.byref(d), _p(dy), _p(s.t), _p(s.t2),
+                     _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _p(ws),
+                     ws.numel(), _stream())
+        return out
+
+
+# ---------------------------------------------------------------------------------------
+# InstanceNorm
+# ---------------------------------------------------------------------------------------
+class INStats:
+    __slots__ = ("scale", "shift", "xmax", "xargmax")
+
+    def __init__(self, scale, shift, xmax=None, xargmax=None):
+        self.scale, self.shift, self.xmax, self.xargmax = scale, shift, xmax, xargmax
+
+
+def in_stats(x: torch.Tensor, want_max: bool = False) -> INStats:
+    _check_dev(x)
+    N, H, W, C = x.shape
+    dev = x.device
+    scale = torch.empty(N, C, device=dev, dtype=torch.float32)
+    shift = torch.empty(N, C, device=dev, dtype=torch.float32)
+    xmax = torch.empty(N, C, device=dev, dtype=torch.float32) if want_max else None
+    xam = torch.empty(N, C, device=dev, dtype=torch.int32) if want_max else None
+    nb = lib.query("dcs_in_stats_workspace_size", N, H * W, C)
+    ws = workspace(nb, dev)
+    lib.call("dcs_in_stats", _p(x), N, H * W, C, IN_EPS, _p(scale), _p(shift), _p(xmax), _p(xam),
+             _p(ws), ws.numel(), _stream())
+    return INStats(scale, shift, xmax, xam)
+
+
+def in_apply(x: torch.Tensor, st: INStats, act: int) -> torch.Tensor:
+    N, H, W, C = x.shape
+    out = torch.empty_like(x)
+    lib.call("dcs_in_apply", _p(x), _p(st.scale), _p(st.shift), _p(out), N, H * W, C, act, _stream())
+    return out
+
+
+def in_act_backward(da: torch.Tensor, y: torch.Tensor, st: INStats, act: int) -> torch.Tensor:
+    N, H, W, C = y.shape
+    dy = torch.empty_like(y)
+    nb = lib.query("dcs_in_stats_workspace_size", N, H * W, C)
+    ws = workspace(nb, y.device)
+    lib.call("dcs_in_act_backward", _p(da), _p(y), _p(st.scale), _p(st.shift), _p(dy), N, H * W, C,
+             act, _p(ws), ws.numel(), _stream())
+    return dy
+
+
+def act_backward(da: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
+    out = torch.empty_like(y)
+    lib.call("dcs_act_backward", _p(da.contiguous()), _p(y), _p(out), y.numel(), act, _stream())
+    return out
+
+
+def channel_sum(x: torch.Tensor) -> torch.Tensor:
+    C = x.shape[-1]
+    Pn = x.numel() // C
+    out = torch.empty(C, device=x.device, dtype=torch.float32)
+    ws = workspace(lib.query("dcs_channel_sum_workspace_size", Pn, C), x.device)
+    lib.call("dcs_channel_sum", _p(x), Pn, C, _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
+def scale_add_(y: torch.Tensor, x: torch.Tensor, a: float = 1.0) -> torch.Tensor:
+    assert y.numel() == x.numel() and y.is_contiguous() and x.is_contiguous()
+    lib.call("dcs_scale_add", _p(y), _p(x), float(a), y.numel(), _stream())
+    return y
+
+
+def scale_dev(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(x)
+    lib.call("dcs_scale_dev", _p(x), _p(s), _p(out), x.numel(), _stream())
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# CBAM
+# ---------------------------------------------------------------------------------------
+def cbam_forward(x, y, st: INStats, w1, w2, wsa):
+    N, H, W, C = y.shape
+    Cr = w1.shape[0]
+    ksa = wsa.shape[-1]
+    dev = y.device
+    ca = torch.empty(N, C, device=dev, dtype=torch.float32)
+    sin_ = torch.empty(N, H * W, 2, device=dev, dtype=torch.float32)
+    sarg = torch.empty(N, H * W, device=dev, dtype=torch.int32)
+    sa = torch.empty(N, H * W, device=dev, dtype=torch.float32)
+    out = torch.empty_like(x)
+    lib.call("dcs_cbam_forward", _p(x), _p(y), _p(st.scale), _p(st.shift), _p(st.xmax), _p(w1),
+             _p(w2), _p(wsa), N, H, W, C, Cr, ksa, _p(ca), _p(sin_), _p(sarg), _p(sa), _p(out),
+             _stream())
+    return out, (ca, sin_, sarg, sa)
+
+
+def cbam_backward(dout, y, st: INStats, w1, w2, wsa, saved):
+    ca, sin_, sarg, sa = saved
+    N, H, W, C = y.shape
+    Cr = w1.shape[0]
+    ksa = wsa.shape[-1]
+    dy = torch.empty_like(y)
+    dw1 = torch.empty_like(w1)
+    dw2 = torch.empty_like(w2)
+    dwsa = torch.empty_like(wsa)
+    nb = lib.query("dcs_cbam_backward_workspace_size", N, H, W, C, Cr, ksa)
+    ws = workspace(nb, y.device)
+    lib.call("dcs_cbam_backward", _p(dout), _p(y), _p(st.scale), _p(st.shift), _p(st.xmax),
+             _p(st.xargmax), _p(w1), _p(w2), _p(wsa), _p(ca), _p(sin_), _p(sarg), _p(sa), N, H, W,
+             C, Cr, ksa, _p(dy), _p(dw1), _p(dw2), _p(dwsa), _p(ws), ws.numel(), _stream())
+    return dy, dw1, dw2, dwsa
+
+
+# ---------------------------------------------------------------------------------------
+# losses: value (0-d tensor) and d value / d pred
+# ---------------------------------------------------------------------------------------
+def _plane_dims(t):
+    N, C, H, W = t.shape
+    assert C == 1, "losses operate on single-channel planes"
+    return N, H, W
+
+
+def _loss_call(name, pred, args, want_grad):
+    _check_dev(pred)
+    N, H, W = _plane_dims(pred)
+    dev = pred.device
+    out = torch.empty(1, device=dev, dtype=torch.float32)
+    grad = torch.empty_like(pred) if want_grad else None
+    ws = workspace(lib.query("dcs_loss_workspace_size", N, H, W), dev)
+    lib.call(name, *args(N, H, W), _p(out), _p(grad), _p(ws), ws.numel(), _stream())
+    return out.view(()), grad
+
+
+def loss_l1(pred, target, want_grad=True):
+    p, t = pred.contiguous(), target.contiguous()
+    return _loss_call("dcs_loss_l1", p, lambda N, H, W: (_p(p), _p(t), p.numel()), want_grad)
+
+
+def loss_mse(pred, target, want_grad=True):
+    p, t = pred.contiguous(), target.contiguous()
+    return _loss_call("dcs_loss_mse", p, lambda N, H, W: (_p(p), _p(t), p.numel()), want_grad)
+
+
+def loss_mse_const(pred, value: float, want_grad=True):
+    p = pred.contiguous()
+    return _loss_call("dcs_loss_mse_const", p, lambda N, H, W: (_p(p), float(value), p.numel()),
+                      want_grad)
+
+
+def loss_gradient(pred, target, want_grad=True):
+    p, t = pred.contiguous(), target.contiguous()
+    return _loss_call("dcs_loss_gradient", p, lambda N, H, W: (_p(p), _p(t), N, H, W), want_grad)
+
+
+def loss_contrast_attention(pred, target, source, sigma, min_w, max_w, k, want_grad=True):
+    p, t, s = pred.contiguous(), target.contiguous(), source.contiguous()
+    return _loss_call("dcs_loss_contrast_attention", p,
+                      lambda N, H, W: (_p(p), _p(t), _p(s), N, H, W, float(sigma), float(min_w),
+                                       float(max_w), int(k)), want_grad)
+
+
+def loss_contrast_region(pred, target, source, threshold, weight, want_grad=True):
+    p, t, s = pred.contiguous(), target.contiguous(), source.contiguous()
+    return _loss_call("dcs_loss_contrast_region", p,
+                      lambda N, H, W: (_p(p), _p(t), _p(s), N, H, W, float(threshold),
+                                       float(weight)), want_grad)
+
+
+def loss_contrast_edge(pred, target, want_grad=True):
+    p, t = pred.contiguous(), target.contiguous()
+    return _loss_call("dcs_loss_contrast_edge", p, lambda N, H, W: (_p(p), _p(t), N, H, W),
+                      want_grad)
+
+
+def loss_ssim(X, Y, data_range=1.0, win=11, sigma=1.5, K=(0.01, 0.03), want_grad=True):
+    x, y = X.contiguous(), Y.contiguous()
+    return _loss_call("dcs_loss_ssim", x,
+                      lambda N, H, W: (_p(x), _p(y), N, H, W, float(data_range), int(win),
+                                       float(sigma), float(K[0]), float(K[1])), want_grad)
+
+
+# ---------------------------------------------------------------------------------------
+# optimizer
+# ---------------------------------------------------------------------------------------
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    lib.call("dcs_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1),
+             float(beta2), float(eps), float(bc1), float(bc2), _stream())

@@ -1,0 +1,197 @@
+/*
+ * ducosy_hip.h — C-ABI of the MI355X (gfx950) kernel library behind the DuCoSy-GAN
+ * CycleGAN training hot path.
+ *
+ * The reference has no FFI: its de-facto operator boundary is the Python nn.Module /
+ * loss-module API of modules/model.py and modules/trainer.py, which reach ATen/cuDNN
+ * kernels through torch.nn.  Every entry point below replaces one such group of ATen
+ * calls (cited per function, paths relative to the reference repo).  The host side
+ * (ducosy-gan_amd/modules/hip/ Python modules) binds them with ctypes.
+ *
+ * Conventions
+ *   - Plain device pointers + int sizes; no torch types.  Activations are NHWC fp32
+ *     (channels innermost); single-channel planes are NCHW == NHWC.
+ *   - The caller owns every buffer (including workspaces, sized by *_workspace_size).
+ *     The library never allocates or frees device memory and never synchronises.
+ *   - Every call is enqueued on `stream` (a hipStream_t passed as void*).
+ *   - Every call returns 0 on success, a DCS_E_* code on an invalid argument, or the
+ *     hipError_t of a failed launch; dcs_last_error() returns a thread-local message.
+ */
+#ifndef DUCOSY_HIP_H
+#define DUCOSY_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCS_OK 0
+#define DCS_E_INVALID 1001
+#define DCS_E_WORKSPACE 1002
+
+#define DCS_PAD_ZERO 0
+#define DCS_PAD_REFLECT 1
+
+/* per-channel prologue transform applied to gathered source values:
+ * v -> act(v * scale[n,c] + shift[n,c]); padding stays zero (or mirrors transformed values) */
+#define DCS_ACT_NONE 0     /* no transform at all */
+#define DCS_ACT_AFFINE 1   /* affine only (InstanceNorm apply) */
+#define DCS_ACT_RELU 2     /* affine + ReLU                    */
+#define DCS_ACT_LRELU 3    /* affine + LeakyReLU(0.2)          */
+#define DCS_ACT_TANH 4     /* epilogue only                    */
+
+/*
+ * Geometry of one implicit-GEMM convolution pass.
+ *   source  : the tensor gathered into the GEMM reduction (forward: x, dgrad: dy)
+ *   output  : NHWC [N, Ho, Wo, Co]
+ * Regular rows (parity = 0): output pixel (oy, ox) reads virtual source coordinate
+ *   (oy*stride + ty - pt, ox*stride + tx - pl) for tap (ty, tx); the virtual source is
+ *   the source upsampled (nearest) by `up`, padded by pad_mode.
+ * Parity rows (parity = 1): stride-2 transposed convolution (dgrad of a stride-2
+ *   forward conv with kernel KH x KW and padding pt/pl): output pixel (2qy+ry, 2qx+rx)
+ *   reads dy at (qy + (ry+pt-ty)/2, qx + (rx+pl-tx)/2) for the taps of its parity class.
+ */
+typedef struct dcs_conv_desc {
+    int32_t N;
+    int32_t Hs, Ws, Cs;             /* source dims (Cs = reduction channels per tap)      */
+    int64_t s_n, s_c, s_h, s_w;     /* source element strides                             */
+    int32_t csplit;                 /* channels >= csplit come from src2 (concat fusion)  */
+    int32_t pad0;
+    int64_t s2_n, s2_c, s2_h, s2_w; /* src2 strides (channel index relative to csplit)   */
+    int32_t up;                     /* nearest-upsample factor of the source (1 or 2)     */
+    int32_t pad_mode;               /* DCS_PAD_ZERO / DCS_PAD_REFLECT                     */
+    int32_t KH, KW, pt, pl;         /* kernel, top/left padding                           */
+    int32_t stride;                 /* forward stride (1 or 2)                            */
+    int32_t parity;                 /* 0 regular rows, 1 stride-2 transposed parity rows  */
+    int32_t Ho, Wo, Co;             /* output dims                                        */
+    int32_t ldb;                    /* row stride of the packed weight matrix             */
+    int32_t pro_act;                /* DCS_ACT_* prologue on the source                   */
+    int32_t epi_act;                /* DCS_ACT_NONE / DCS_ACT_TANH / DCS_ACT_LRELU        */
+} dcs_conv_desc;
+
+const char* dcs_last_error(void);
+int dcs_version(void);
+
+/* ---- convolution family (modules/model.py:61-63,74-79,94-112,122-129 → aten conv) ---- */
+
+/* Pack OIHW weights into the GEMM B operand [Kpad][ldb] (zero padded).
+ * kind 0 forward   : B[(ty*KW+tx)*Cin + ci][co] = W[co][ci][ty][tx]
+ * kind 1 dgrad-flip: B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][KH-1-ty][KW-1-tx]  (stride-1 dgrad)
+ * kind 2 dgrad     : B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][ty][tx]              (stride-2 dgrad)
+ * ci_count limits the packed input channels (dgrad of a concat input needs only the first). */
+int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                     int Kpad, int ldb, float* out, void* stream);
+
+/* Forward / data-gradient pass: out = gather(src) x B (+ bias, epilogue act). */
+int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,
+                  const float* bias, const float* pro_scale, const float* pro_shift, float* out,
+                  void* stream);
+
+/* Weight gradient: dw (OIHW) = sum_pixels dy^T x gather(x).  `d` describes the FORWARD conv
+ * (source = x, output = dy).  ws must hold dcs_conv_wgrad_workspace_size(d) bytes. */
+size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* d);
+int dcs_conv_wgrad(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
+                   const float* pro_scale, const float* pro_shift, float* dw, void* ws,
+                   size_t ws_bytes, void* stream);
+
+/* Fold the gradient of a reflection-padded tensor back onto the tensor:
+ * dx[n,i,j,c] = addend[n,i,j,c] + sum over padded positions mirroring to (i,j). */
+int dcs_reflect_fold(const float* dxpad, const float* addend, float* dx, int N, int H, int W, int C,
+                     int pad, void* stream);
+
+/* Gradient of nearest x2 upsampling: dx[n,i,j,c] = sum_{a,b<2} dup[n,2i+a,2j+b,c]. */
+int dcs_upsample2_grad(const float* dup, float* dx, int N, int H, int W, int C, void* stream);
+
+/* ---- InstanceNorm2d(affine=False) (modules/model.py:61,94,97,110,124 → aten native_batch_norm) ---- */
+
+/* Per-(n,c) statistics of an NHWC tensor: scale = 1/sqrt(var+eps), shift = -mean*scale
+ * (so IN(x) = x*scale + shift), optional per-(n,c) max and argmax (pixel index) of x. */
+size_t dcs_in_stats_workspace_size(int N, int HW, int C);
+int dcs_in_stats(const float* x, int N, int HW, int C, float eps, float* scale, float* shift,
+                 float* xmax, int32_t* xargmax, void* ws, size_t ws_bytes, void* stream);
+
+/* out = act(x*scale + shift) */
+int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW,
+                 int C, int act, void* stream);
+
+/* Backward of a = act(IN(y)) given da: dy = scale*(g - mean(g) - xh*mean(g*xh)),
+ * g = da*act'(xh), xh = y*scale+shift.  ws: dcs_in_stats_workspace_size(N,HW,C). */
+int dcs_in_act_backward(const float* da, const float* y, const float* scale, const float* shift,
+                        float* dy, int N, int HW, int C, int act, void* ws, size_t ws_bytes,
+                        void* stream);
+
+/* ---- narrow-output convolutions (Co <= 4: Generator head, PatchGAN last layer, and the
+ *      input-image gradients of the stem and the first PatchGAN layer) ---- */
+int dcs_conv_rows_narrow(const dcs_conv_desc* d, const float* src, const float* src2,
+                         const float* wpack, const float* bias, const float* pro_scale,
+                         const float* pro_shift, float* out, void* stream);
+size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* d);
+int dcs_conv_wgrad_narrow(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
+                          const float* pro_scale, const float* pro_shift, float* dw, void* ws,
+                          size_t ws_bytes, void* stream);
+
+/* ---- CBAM tail of ResidualBlockWithCBAM (modules/model.py:6-52, 83-87) ----
+ * out = x + CBAM(IN(y)):  y is the raw conv2 output NHWC [N,H*W,C] with its InstanceNorm
+ * coefficients (scale, shift) and the per-(n,c) max / argmax of y from dcs_in_stats.
+ * w1: fc.0 [Cr][C], w2: fc.2 [C][Cr], wsa: [2][ksa][ksa] (spatial-attention conv, no bias).
+ * Saved for backward: ca [N][C], sin_ [N][HW][2] (channel mean/max), sarg [N][HW] (argmax
+ * channel), sa [N][HW]. */
+int dcs_cbam_forward(const float* x, const float* y, const float* scale, const float* shift,
+                     const float* ymax, const float* w1, const float* w2, const float* wsa,
+                     int N, int H, int W, int C, int Cr, int ksa,
+                     float* ca, float* sin_, int32_t* sarg, float* sa, float* out, void* stream);
+size_t dcs_cbam_backward_workspace_size(int N, int H, int W, int C, int Cr, int ksa);
+/* Given dout = dL/d(out): dy (gradient of the raw conv2 output y, InstanceNorm backward
+ * included) and the gradients of w1, w2, wsa (overwritten).  The residual gradient (dout
+ * itself, for x) is NOT added here. */
+int dcs_cbam_backward(const float* dout, const float* y, const float* scale, const float* shift,
+                      const float* ymax, const int32_t* yargmax, const float* w1, const float* w2,
+                      const float* wsa, const float* ca, const float* sin_, const int32_t* sarg,
+                      const float* sa, int N, int H, int W, int C, int Cr, int ksa, float* dy,
+                      float* dw1, float* dw2, float* dwsa, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- losses (modules/trainer.py:22-184, 347-351; pytorch_msssim.SSIM) ----
+ * All take single-channel planes [N,1,H,W]; each writes the loss value to out[0] and the
+ * gradient d(loss)/d(pred) (unscaled) to grad (may be NULL for value only). */
+size_t dcs_loss_workspace_size(int N, int H, int W);
+int dcs_loss_l1(const float* pred, const float* target, int64_t n, float* out, float* grad,
+                void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_mse(const float* pred, const float* target, int64_t n, float* out, float* grad,
+                 void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_mse_const(const float* pred, float target, int64_t n, float* out, float* grad,
+                       void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_gradient(const float* pred, const float* target, int N, int H, int W, float* out,
+                      float* grad, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_attention(const float* pred, const float* target, const float* source, int N,
+                                int H, int W, float sigma, float min_w, float max_w, int k,
+                                float* out, float* grad, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_region(const float* pred, const float* target, const float* source, int N,
+                             int H, int W, float threshold, float weight, float* out, float* grad,
+                             void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_edge(const float* pred, const float* target, int N, int H, int W, float* out,
+                           float* grad, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_ssim(const float* X, const float* Y, int N, int H, int W, float data_range,
+                  int win, float sigma, float k1, float k2, float* out, float* grad, void* ws,
+                  size_t ws_bytes, void* stream);
+
+/* ---- optimizer (torch.optim.Adam, modules/trainer.py:360-362, 514, 520, 525) ----
+ * One launch over a flat parameter buffer. */
+int dcs_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                  float beta2, float eps, float bias_c1, float bias_c2, void* stream);
+
+/* small utilities */
+int dcs_scale_add(float* y, const float* x, float a, int64_t n, void* stream); /* y += a*x */
+/* out = x * (*s) with s a device scalar (loss backward without a host sync) */
+int dcs_scale_dev(const float* x, const float* s, float* out, int64_t n, void* stream);
+/* dy = da * act'(y): relu/lrelu given the pre-activation y; tanh given the output y */
+int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, void* stream);
+/* out[c] = sum_p x[p][c] (conv bias gradients) */
+size_t dcs_channel_sum_workspace_size(int64_t P, int C);
+int dcs_channel_sum(const float* x, int64_t P, int C, float* out, void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DUCOSY_HIP_H */

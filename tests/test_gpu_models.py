@@ -1,0 +1,144 @@
+"""Network-level parity: HIP Generator / Discriminator / ResidualBlockWithCBAM vs the golden
+vectors produced by the reference (tests/golden/make_golden.py) and vs the oracle.
+Tolerance: 1e-3 relative (BASELINE.json north_star) on outputs, input grads and weight grads.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import prng
+from oracle import ref_torch as orc
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-3
+
+
+def rel(a, b):
+    """max-abs error relative to max |b| (forward activations)."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max(), 1e-12))
+
+
+def rel2(a, b):
+    """relative L2 error (gradients).  Backward passes cross ReLU/LeakyReLU kinks: an element
+    whose pre-activation is within fp32 rounding of 0 may take the other branch in any fp32
+    implementation (the reference's own fp32 CPU path included), changing that one gradient
+    entry by O(1) — a max-abs criterion would flag rounding, an L2 criterion does not."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+GTOL = 5e-3  # relative L2 on gradients (see rel2)
+
+
+def _check_grads(model, z, live_bias=()):
+    """live_bias: the biases NOT followed by an InstanceNorm (all others have exact gradient 0
+    here and rounding noise in the reference)."""
+    for name, p in model.named_parameters():
+        g = p.grad.detach().double().cpu().flatten().numpy()
+        gn = float(z[f"gnorm:{name}"])
+        if name.endswith(".bias") and name not in live_bias:
+            assert np.abs(g).max() == 0.0, name
+            continue
+        assert abs(np.linalg.norm(g) - gn) <= GTOL * gn + 1e-7, (name, np.linalg.norm(g), gn)
+        idx = z[f"gidx:{name}"]
+        scale = gn / np.sqrt(g.size) + 1e-30
+        assert np.abs(g[idx] - z[f"gval:{name}"]).max() / scale < 1e-2, name
+
+
+@pytest.mark.parametrize("fname", ["gen_cin3_nb1_32.npz", "gen_cin1_nb9_32.npz",
+                                   "gen_cin2_nb2_nocbam_32.npz", "gen_cin3_nb1_64.npz"])
+def test_generator_golden(fname):
+    from modules.model import Generator
+    z = np.load(os.path.join(GOLDEN, fname))
+    cin, nb, cbam, n, hw, seed = [int(v) for v in z["meta"]]
+    G = Generator(input_channels=cin, num_residual_blocks=nb, use_cbam=bool(cbam))
+    G.load_state_dict(_sd(orc.generator_param_shapes(cin, nb, bool(cbam)), seed))
+    G = G.to(DEV)
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_(True)
+    y = G(x)
+    assert rel(y, z["y"]) < TOL
+    (y * torch.from_numpy(z["R"]).to(DEV)).sum().backward()
+    assert rel2(x.grad, z["dx"]) < GTOL
+    _check_grads(G, z, live_bias=(f"model.{19 + nb}.bias",))
+
+
+def test_generator_split_masks_matches_concat():
+    """Concat fused into the stem gather == the reference's explicit torch.cat input."""
+    from modules.model import Generator
+    z = np.load(os.path.join(GOLDEN, "gen_cin3_nb1_32.npz"))
+    G = Generator(3, 1).to(DEV)
+    G.load_state_dict(_sd(orc.generator_param_shapes(3, 1, True), 101))
+    x = torch.from_numpy(z["x"]).to(DEV)
+    img = x[:, :1].contiguous().requires_grad_(True)
+    y = G(img, x[:, 1:].contiguous())
+    assert rel(y, z["y"]) < TOL
+    (y * torch.from_numpy(z["R"]).to(DEV)).sum().backward()
+    assert rel2(img.grad, z["dx"][:, :1]) < GTOL
+
+
+def test_resblock_golden():
+    from modules.model import ResidualBlockWithCBAM
+    z = np.load(os.path.join(GOLDEN, "resblock_cbam_16.npz"))
+    n, c, hw, seed = [int(v) for v in z["meta"]]
+    B = ResidualBlockWithCBAM(c)
+    shapes = {k: tuple(v.shape) for k, v in B.state_dict().items()}
+    B.load_state_dict(_sd(shapes, seed))
+    B = B.to(DEV)
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_(True)
+    y = B(x)
+    assert rel(y, z["y"]) < TOL
+    (y * torch.from_numpy(z["R"]).to(DEV)).sum().backward()
+    assert rel2(x.grad, z["dx"]) < GTOL
+    for name, p in B.named_parameters():
+        if p.dim() == 1:
+            continue
+        g = p.grad.detach().double().cpu().flatten().numpy()
+        gn = float(z[f"gnorm:{name}"])
+        assert abs(np.linalg.norm(g) - gn) <= GTOL * gn, name
+
+
+@pytest.mark.parametrize("fname", ["disc_64.npz", "disc_128.npz"])
+def test_discriminator_golden(fname):
+    from modules.model import Discriminator
+    z = np.load(os.path.join(GOLDEN, fname))
+    n, hw, seed = [int(v) for v in z["meta"]]
+    D = Discriminator()
+    D.load_state_dict(_sd(orc.discriminator_param_shapes(1), seed))
+    D = D.to(DEV)
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_(True)
+    y = D(x)
+    assert rel(y, z["y"]) < TOL
+    (y * torch.from_numpy(z["R"]).to(DEV)).sum().backward()
+    assert rel2(x.grad, z["dx"]) < GTOL
+    _check_grads(D, z, live_bias=("model.0.bias", "model.12.bias"))
+
+
+def test_generator_vs_oracle_128():
+    """A larger case than the fixtures: 128x128, cin 3, 2 blocks, batch 2 vs the oracle."""
+    from modules.model import Generator
+    torch.set_num_threads(8)
+    sd = _sd(orc.generator_param_shapes(3, 2, True), 77)
+    x = np.concatenate([prng.uniform(77, "x", (2, 1, 128, 128), -1, 1),
+                        prng.bernoulli(77, "m", (2, 2, 128, 128), 0.3)], 1)
+    pr = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    xr = torch.from_numpy(x)
+    yr = orc.generator_forward(pr, xr, 2, True)
+    R = torch.from_numpy(prng.normal(77, "R", tuple(yr.shape)))
+    (yr * R).sum().backward()
+    G = Generator(3, 2)
+    G.load_state_dict(sd)
+    G = G.to(DEV)
+    y = G(xr.to(DEV))
+    assert rel(y, yr) < TOL
+    (y * R.to(DEV)).sum().backward()
+    for name, p in G.named_parameters():
+        if p.dim() == 4:
+            assert rel2(p.grad, pr[name].grad) < GTOL, name

@@ -1,0 +1,219 @@
+"""Op-level parity of the HIP kernels against fp32 torch-CPU references of the same op.
+
+Every test here is @pytest.mark.gpu and calls the kernels through the C-ABI (ctypes).
+Tolerances: fp32 everywhere; max abs error / max |ref| <= 1e-4 for single ops (1e-3 rel for
+chained backward passes), following BASELINE.json's 1e-3 rel bar.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import prng
+from oracle import ref_torch as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max(), 1e-12))
+
+
+def rnd(shape, seed, name, lo=-1.0, hi=1.0):
+    return torch.from_numpy(prng.uniform(seed, name, shape, lo, hi))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from modules.hip import ops as o
+    return o
+
+
+def torch_conv(x_nchw, w, geom, bias=None):
+    """CPU reference of ConvGeom.forward: pad module (+upsample) + F.conv2d."""
+    from modules.hip.lib import DCS_PAD_REFLECT
+    x = x_nchw
+    if geom.up == 2:
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+    t, l, b, r = geom.pads
+    x = F.pad(x, (l, r, t, b), mode="reflect" if geom.pad_mode == DCS_PAD_REFLECT else "constant")
+    return F.conv2d(x, w, bias, stride=geom.stride)
+
+
+CONV_CASES = [
+    # cin, cout, k, stride, pads, mode, up, H
+    (3, 64, 7, 1, (3, 3, 3, 3), "reflect", 1, 20),      # stem (scalar gather, cin 3)
+    (64, 128, 3, 2, (1, 1, 1, 1), "zero", 1, 18),       # down1
+    (128, 256, 3, 2, (1, 1, 1, 1), "zero", 1, 10),      # down2
+    (256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, 9),    # residual
+    (256, 128, 3, 1, (1, 1, 1, 1), "zero", 2, 5),       # up1
+    (128, 64, 3, 1, (1, 1, 1, 1), "zero", 2, 6),        # up2
+    (64, 1, 7, 1, (3, 3, 3, 3), "reflect", 1, 12),      # head (narrow)
+    (1, 64, 4, 2, (1, 1, 1, 1), "zero", 1, 32),         # D layer 0 (cin 1)
+    (64, 128, 4, 2, (1, 1, 1, 1), "zero", 1, 16),       # D layer 1
+    (256, 512, 4, 2, (1, 1, 1, 1), "zero", 1, 8),       # D layer 3
+    (512, 1, 4, 1, (2, 2, 1, 1), "zero", 1, 4),         # D last (narrow, asymmetric pad)
+    # the layer shapes of a 64x64 generator at batch 1 (split-K wgrad, multi-tile rows)
+    (256, 128, 3, 1, (1, 1, 1, 1), "zero", 2, 16),
+    (128, 64, 3, 1, (1, 1, 1, 1), "zero", 2, 32),
+    (64, 1, 7, 1, (3, 3, 3, 3), "reflect", 1, 64),
+    (256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, 16),
+    (64, 128, 3, 2, (1, 1, 1, 1), "zero", 1, 64),
+]
+
+
+def _geom(case):
+    from modules.hip.ops import ConvGeom
+    from modules.hip.lib import DCS_PAD_REFLECT, DCS_PAD_ZERO
+    cin, cout, k, s, pads, mode, up, H = case
+    return ConvGeom(cin, cout, k, s, pads, DCS_PAD_REFLECT if mode == "reflect" else DCS_PAD_ZERO, up), H
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}" for c in CONV_CASES])
+def test_conv_fwd_dgrad_wgrad(ops, case):
+    torch.manual_seed(0)
+    g, H = _geom(case)
+    N = 2 if H < 16 else 1
+    x = rnd((N, g.cin, H, H + 1), 1, "x")
+    w = torch.from_numpy(prng.normal(2, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05))
+    bias = rnd((g.cout,), 3, "b")
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, g, bias)
+    R = torch.from_numpy(prng.normal(4, "R", tuple(yr.shape)))
+    (yr * R).sum().backward()
+
+    xd = x.to(DEV).permute(0, 2, 3, 1).contiguous()
+    wd, bd = w.to(DEV), bias.to(DEV)
+    y = g.forward(ops.Src.nhwc(xd), g.pack_fwd(wd), bias=bd)
+    assert rel(y.permute(0, 3, 1, 2), yr) < 1e-4
+    Rd = R.to(DEV).permute(0, 2, 3, 1).contiguous()
+    dw = g.wgrad(Rd, ops.Src.nhwc(xd))
+    assert rel(dw, wr.grad) < 1e-4
+    dx = g.dgrad(Rd, g.pack_dgrad(wd), H, H + 1)
+    assert rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-4
+
+
+def test_conv_prologue_and_concat(ops):
+    """IN+ReLU prologue and channel-concat of two NCHW sources fused in the gather."""
+    from modules.hip.ops import ConvGeom, Src
+    from modules.hip.lib import ACT_RELU, DCS_PAD_REFLECT
+    N, H, W = 2, 16, 12
+    img = rnd((N, 1, H, W), 5, "img")
+    masks = (rnd((N, 2, H, W), 6, "m", 0, 1) < 0.3).float()
+    g = ConvGeom(3, 64, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT)
+    w = torch.from_numpy(prng.normal(7, "w", (64, 3, 7, 7), 0, 0.05))
+    ref = torch_conv(torch.cat([img, masks], 1), w, g)
+    y = g.forward(Src.nchw(img.to(DEV), masks.to(DEV)), g.pack_fwd(w.to(DEV)))
+    assert rel(y.permute(0, 3, 1, 2), ref) < 1e-4
+    # prologue: next conv consumes relu(IN(y))
+    st = ops.in_stats(y)
+    g2 = ConvGeom(64, 128, 3, 2, (1, 1, 1, 1))
+    w2 = torch.from_numpy(prng.normal(8, "w2", (128, 64, 3, 3), 0, 0.05))
+    a = F.relu(F.instance_norm(ref, eps=1e-5))
+    ref2 = torch_conv(a, w2, g2)
+    y2 = g2.forward(Src.nhwc(y), g2.pack_fwd(w2.to(DEV)), pro=(st.scale, st.shift, ACT_RELU))
+    assert rel(y2.permute(0, 3, 1, 2), ref2) < 1e-4
+
+
+@pytest.mark.parametrize("N,C,H,W", [(3, 64, 17, 13), (3, 256, 8, 8), (3, 512, 4, 4), (3, 128, 32, 32),
+                                     (1, 128, 32, 32), (1, 64, 64, 64), (2, 256, 64, 64)])
+def test_instance_norm(ops, N, C, H, W):
+    from modules.hip.lib import ACT_LRELU, ACT_RELU
+    x = rnd((N, C, H, W), 9, "x", -2, 3)
+    xd = x.to(DEV).permute(0, 2, 3, 1).contiguous()
+    st = ops.in_stats(xd, want_max=True)
+    ref = F.instance_norm(x, eps=1e-5)
+    for act, fn in ((ACT_RELU, F.relu), (ACT_LRELU, lambda t: F.leaky_relu(t, 0.2))):
+        out = ops.in_apply(xd, st, act)
+        assert rel(out.permute(0, 3, 1, 2), fn(ref)) < 1e-5
+        xr = x.clone().requires_grad_(True)
+        yr = fn(F.instance_norm(xr, eps=1e-5))
+        R = torch.from_numpy(prng.normal(10, "R", tuple(yr.shape)))
+        (yr * R).sum().backward()
+        dy = ops.in_act_backward(R.to(DEV).permute(0, 2, 3, 1).contiguous(), xd, st, act)
+        assert rel(dy.permute(0, 3, 1, 2), xr.grad) < 1e-4
+    mx, am = x.flatten(2).max(-1)
+    assert torch.equal(st.xmax.cpu(), mx)
+    assert torch.equal(st.xargmax.cpu().long(), am)
+
+
+def test_cbam_tail(ops):
+    """out = x + CBAM(IN(y)) forward and backward (incl. IN backward) vs the oracle."""
+    N, C, H, W = 2, 256, 12, 10
+    x = torch.from_numpy(prng.normal(11, "x", (N, C, H, W)))
+    y = torch.from_numpy(prng.normal(12, "y", (N, C, H, W), 0.3, 1.7))
+    w1 = torch.from_numpy(prng.normal(13, "w1", (16, C, 1, 1), 0, 0.1))
+    w2 = torch.from_numpy(prng.normal(14, "w2", (C, 16, 1, 1), 0, 0.1))
+    wsa = torch.from_numpy(prng.normal(15, "wsa", (1, 2, 7, 7), 0, 0.1))
+    P = {"c.channel_attention.fc.0.weight": w1.clone().requires_grad_(True),
+         "c.channel_attention.fc.2.weight": w2.clone().requires_grad_(True),
+         "c.spatial_attention.conv.weight": wsa.clone().requires_grad_(True)}
+    xr, yr = x.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    z = F.instance_norm(yr, eps=1e-5)
+    z = orc.channel_attention(P, "c.channel_attention", z)
+    z = orc.spatial_attention(P, "c.spatial_attention", z)
+    outr = xr + z
+    R = torch.from_numpy(prng.normal(16, "R", tuple(outr.shape)))
+    (outr * R).sum().backward()
+
+    xd = x.to(DEV).permute(0, 2, 3, 1).contiguous()
+    yd = y.to(DEV).permute(0, 2, 3, 1).contiguous()
+    st = ops.in_stats(yd, want_max=True)
+    w1d, w2d, wsad = w1.to(DEV).view(16, C), w2.to(DEV).view(C, 16), wsa.to(DEV).view(2, 7, 7)
+    out, saved = ops.cbam_forward(xd, yd, st, w1d, w2d, wsad)
+    assert rel(out.permute(0, 3, 1, 2), outr) < 1e-4
+    dy, dw1, dw2, dwsa = ops.cbam_backward(R.to(DEV).permute(0, 2, 3, 1).contiguous(), yd, st, w1d,
+                                           w2d, wsad, saved)
+    assert rel(dy.permute(0, 3, 1, 2), yr.grad) < 1e-3
+    assert rel(dw1.view_as(w1), P["c.channel_attention.fc.0.weight"].grad) < 1e-3
+    assert rel(dw2.view_as(w2), P["c.channel_attention.fc.2.weight"].grad) < 1e-3
+    assert rel(dwsa.view_as(wsa), P["c.spatial_attention.conv.weight"].grad) < 1e-3
+
+
+LOSS_CASES = {
+    "l1": (lambda o, p, t, s: o.loss_l1(p, t), lambda p, t, s: orc.l1(p, t)),
+    "mse": (lambda o, p, t, s: o.loss_mse(p, t), lambda p, t, s: orc.mse(p, t)),
+    "mse_const": (lambda o, p, t, s: o.loss_mse_const(p, 1.0), lambda p, t, s: orc.mse(p, torch.ones_like(p))),
+    "gradient": (lambda o, p, t, s: o.loss_gradient(p, t), lambda p, t, s: orc.gradient_loss(p, t)),
+    "contrast_attention": (lambda o, p, t, s: o.loss_contrast_attention(p, t, s, 0.15, 1.0, 3.0, 7),
+                           lambda p, t, s: orc.contrast_attention_loss(p, t, s, 0.15, 1.0, 3.0, 7)),
+    "contrast_region": (lambda o, p, t, s: o.loss_contrast_region(p, t, s, 0.15, 1.5),
+                        lambda p, t, s: orc.contrast_region_loss(p, t, s, 0.15, 1.5)),
+    "contrast_edge": (lambda o, p, t, s: o.loss_contrast_edge(p, t),
+                      lambda p, t, s: orc.contrast_edge_loss(p, t, s)),
+    "ssim": (lambda o, p, t, s: o.loss_ssim(p, t, 1.0), lambda p, t, s: orc.ssim(p, t, 1.0)),
+}
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 64, 64), (1, 1, 48, 40), (3, 1, 33, 47)])
+@pytest.mark.parametrize("name", sorted(LOSS_CASES))
+def test_losses(ops, name, shape):
+    hip_fn, ref_fn = LOSS_CASES[name]
+    p = torch.tanh(torch.from_numpy(prng.normal(17, "p", shape)))
+    t = rnd(shape, 18, "t")
+    s = rnd(shape, 19, "s")
+    pr = p.clone().requires_grad_(True)
+    vr = ref_fn(pr, t, s)
+    vr.backward()
+    v, g = hip_fn(ops, p.to(DEV), t.to(DEV), s.to(DEV))
+    assert abs(float(v) - float(vr)) <= 1e-5 * max(1.0, abs(float(vr))), (name, float(v), float(vr))
+    assert rel(g, pr.grad) < 1e-4, name
+
+
+def test_adam_matches_torch(ops):
+    n = 10000
+    p0 = torch.from_numpy(prng.normal(20, "p", (n,)))
+    opt_p = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([opt_p], lr=2e-4, betas=(0.5, 0.999))
+    pd, md, vd = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        g = torch.from_numpy(prng.normal(21, f"g{step}", (n,)))
+        opt_p.grad = g.clone()
+        opt.step()
+        ops.adam_step(pd, g.to(DEV), md, vd, 2e-4, 0.5, 0.999, 1e-8, step)
+    assert rel(pd, opt_p.detach()) < 1e-6
