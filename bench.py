@@ -1,0 +1,165 @@
+"""Benchmark: CycleGAN train-step images/sec at 512x512, bs=8 per GPU (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one full pass of modules/trainer.py:463-525 (G step with all nine loss terms and
+its Adam, D_A step, D_B step) on the fused HIP path, over one synthetic batch of 8 slices per
+GPU that is already resident in HBM.  Data parallel: one process per GPU, each with its own
+shard; one RCCL all-reduce per optimizer (weak scaling).  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (implicit GEMM,
+conv_rows_kernel<128,128,true,1>, forward + data-gradient launches).  Its per-launch duration
+is measured live with HIP events on the launch stream over the timed steps; FLOPs are
+algorithmic (2*pixels*256*256*9 per launch).  Peak = 157.3 TFLOP/s (gfx950 f32 MFMA, dense).
+cpu_baseline: the oracle (oracle/ref_torch.py, the CPU restatement of the reference step)
+timed on this host on a bounded sample (one 512x512 slice, 9 blocks, one step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ducosy-gan_amd"))
+
+import torch  # noqa: E402
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def _synthetic(n, img, n_masks, device, seed):
+    g = torch.Generator(device=device).manual_seed(seed)
+    a = torch.rand(n, 1, img, img, generator=g, device=device) * 2 - 1
+    b = torch.rand(n, 1, img, img, generator=g, device=device) * 2 - 1
+    m = (torch.rand(n, n_masks, img, img, generator=g, device=device) < 0.3).float() if n_masks else None
+    return a, b, m
+
+
+def cpu_baseline(img, blocks, cin, threads):
+    """Time the oracle's CPU step (the reference algorithm restated) on one slice."""
+    sys.path.insert(0, ROOT)
+    from oracle import prng
+    from oracle import ref_torch as orc
+    torch.set_num_threads(threads)
+    gs, ds = orc.generator_param_shapes(cin, blocks, True), orc.discriminator_param_shapes(1)
+    sd = lambda shapes, s: {k: torch.from_numpy(v) for k, v in prng.init_state_dict(shapes, s).items()}
+    m = orc.OracleCycleGAN(sd(gs, 1), sd(gs, 2), sd(ds, 3), sd(ds, 4), blocks)
+    a = torch.from_numpy(prng.uniform(5, "A", (1, 1, img, img), -1, 1))
+    b = torch.from_numpy(prng.uniform(5, "B", (1, 1, img, img), -1, 1))
+    mk = torch.from_numpy(prng.bernoulli(5, "M", (1, cin - 1, img, img), 0.3)) if cin > 1 else None
+    t0 = time.perf_counter()
+    m.step(a, b, mk)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"1 full step (G+D_A+D_B, all losses, Adam) on 1 slice {img}x{img}, "
+                      f"{blocks} residual blocks, cin {cin}, oracle/ref_torch.py fp32 on CPU "
+                      f"({dt:.2f} s)"}
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
+    (profiles/pmc_resconv.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_resconv.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch")
+    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--blocks", type=int, default=9)
+    ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from modules import parallel
+    from modules.hip import ops
+    from modules.trainer import CycleGANSystem
+
+    rank, world, local = parallel.init_from_env()
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+    torch.manual_seed(1234)
+    system = CycleGANSystem(args.cin, args.blocks, True, device=device)
+    batches = [_synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i) for i in range(2)]
+
+    for i in range(args.warmup):
+        system.train_step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    ops.PROBE.reset()
+    ops.PROBE.active = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        system.train_step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.PROBE.active = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    n_launch, ms_launch, flop_launch = ops.PROBE.summary()
+
+    if rank == 0:
+        value = world * args.batch * args.steps / elapsed
+        achieved = flop_launch / (ms_launch * 1e-3) / 1e12 if ms_launch > 0 else 0.0
+        rec = {
+            "metric": "CycleGAN train-step images/sec at 512x512 bs=8/GPU",
+            "value": round(value, 4),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
+            "config": {
+                "workload": "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
+                            "9 G loss terms + 2 D losses, 3 Adam steps",
+                "img_size": args.img, "per_gpu_batch": args.batch, "global_batch": args.batch * world,
+                "residual_blocks": args.blocks, "input_channels": args.cin, "parallelism": f"dp{world}",
+            },
+            "roofline": {
+                "kernel": "conv_rows_kernel<128,128,true,1> (256-ch 3x3 residual conv, fwd+dgrad)",
+                "bound": "mfma",
+                "achieved": round(achieved, 3),
+                "peak": F32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": _pmc_traffic(),
+                "launches": n_launch,
+                "ms_per_launch": round(ms_launch, 4),
+                "gflop_per_launch": round(flop_launch / 1e9, 3),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            rec["cpu_baseline"] = cpu_baseline(args.img, args.blocks, args.cin, threads)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

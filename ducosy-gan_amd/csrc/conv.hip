@@ -182,7 +182,9 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
 // ---------------------------------------------------------------------------------------
 // rows pass: implicit GEMM on v_mfma_f32_32x32x2_f32
 // ---------------------------------------------------------------------------------------
-template <int BM, int BN, bool VEC>
+// TAG only separates instantiations in profiles: 1 = the 256-ch 3x3 residual-block conv
+// (forward and data-gradient), the north-star kernel.
+template <int BM, int BN, bool VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const dcs_conv_desc d, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
@@ -730,13 +732,16 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     }
     dim3 grid((unsigned)cdiv(Mmax, 128), (unsigned)cdiv(d.Co, BN), ncls);
     const bool vec = vec_ok(dp, src);
+    const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
+                     d.stride == 1;
     hipStream_t s = as_stream(stream);
     if (BN == 128) {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
     }
     return check_launch("conv_rows");
 }

@@ -59,6 +59,52 @@ def _round_up(x, m):
 
 
 # ---------------------------------------------------------------------------------------
+# kernel probe: HIP events around the north-star kernel's launches (bench.py roofline)
+# ---------------------------------------------------------------------------------------
+class KernelProbe:
+    """Records (start, end, algorithmic FLOPs) for every launch of the 256-channel 3x3
+    residual-block convolution (conv_rows_kernel<128,128,true,1>: forward and data-gradient)
+    on the stream it is launched on, while ``active``."""
+
+    def __init__(self):
+        self.active = False
+        self.records = []
+
+    def reset(self):
+        self.records = []
+
+    def begin(self):
+        if not self.active:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def end(self, e0, flops):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream())
+        self.records.append((e0, e1, flops))
+
+    def summary(self):
+        """(launches, mean ms per launch, mean algorithmic FLOP per launch)."""
+        if not self.records:
+            return 0, 0.0, 0.0
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return len(ms), sum(ms) / len(ms), sum(fl) / len(fl)
+
+
+PROBE = KernelProbe()
+
+
+def _is_res_geom(g) -> bool:
+    return g.cin == 256 and g.cout == 256 and g.k == 3 and g.stride == 1 and g.up == 1
+
+
+# ---------------------------------------------------------------------------------------
 # convolution geometry
 # ---------------------------------------------------------------------------------------
 @dataclass
@@ -171,8 +217,10 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
+        e0 = PROBE.begin() if _is_res_geom(self) else None
         lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
                  _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
+        PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
         return out
 
     # ---- data gradient ---------------------------------------------------------------
@@ -213,8 +261,10 @@ class ConvGeom:
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
             dpad = torch.empty(N, d.Ho, d.Wo, ci, device=dev, dtype=torch.float32)
+            e0 = PROBE.begin() if _is_res_geom(self) else None
             lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad),
                      _stream())
+            PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
             lib.call("dcs_reflect_fold", _p(dpad), _p(addend), _p(out), N, H, W, ci, p, _stream())
             return out

