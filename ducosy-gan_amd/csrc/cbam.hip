@@ -263,14 +263,15 @@ __global__ __launch_bounds__(256) void cb_bwd_sums_kernel(const float* __restric
     }
 }
 
-// b4: one block; channel-attention MLP backward + IN-backward coefficients per (n,c).
-// coef[n][c] = {mean(dz), mean(dz*z), dvmax}; dw1/dw2 summed over n in fixed order.
+// b4: one block per image: channel-attention MLP backward + IN-backward coefficients.
+// coef[n][c] = {mean(dz), mean(dz*z), dvmax}; per-image dw1/dw2 partials (summed over n by
+// cb_bwd_dw_reduce_kernel in fixed order).
 __global__ __launch_bounds__(256) void cb_bwd_ca_kernel(const Sum3* __restrict__ parts, int nchunk,
                                                         const float* __restrict__ ymax, const float* __restrict__ sc,
                                                         const float* __restrict__ sh, const float* __restrict__ ca,
                                                         const float* __restrict__ w1, const float* __restrict__ w2,
-                                                        int N, int HW, int C, int Cr, Sum3* __restrict__ coef,
-                                                        float* __restrict__ dw1, float* __restrict__ dw2) {
+                                                        int HW, int C, int Cr, Sum3* __restrict__ coef,
+                                                        float* __restrict__ dwpart) {
     extern __shared__ float sm[];
     float* vmax = sm;            // [C]
     float* dpc = vmax + C;       // [C] d(pre-sigmoid)
@@ -278,47 +279,63 @@ __global__ __launch_bounds__(256) void cb_bwd_ca_kernel(const Sum3* __restrict__
     float* dhm = hp + Cr;        // [Cr]
     float* S1 = dhm + Cr;        // [C] sum dz0
     float* S2 = S1 + C;          // [C] sum dz0*z
-    const int tid = threadIdx.x;
-    for (int i = tid; i < C * Cr; i += blockDim.x) { dw1[i] = 0.f; dw2[i] = 0.f; }
-    __syncthreads();
-    for (int n = 0; n < N; ++n) {
-        for (int c = tid; c < C; c += blockDim.x) {
-            const long long nc = (long long)n * C + c;
-            double A = 0.0, B = 0.0, Cc = 0.0;
-            for (int k = 0; k < nchunk; ++k) {
-                Sum3 p = parts[((long long)n * nchunk + k) * C + c];
-                A += p.a; B += p.b; Cc += p.c;
-            }
-            vmax[c] = fmaf(ymax[nc], sc[nc], sh[nc]);
-            float g = ca[nc];
-            dpc[c] = (float)A * g * (1.f - g);
-            S1[c] = (float)B;
-            S2[c] = (float)Cc;
+    __shared__ float red[2][4];
+    const int tid = threadIdx.x, n = blockIdx.x;
+    for (int c = tid; c < C; c += blockDim.x) {
+        const long long nc = (long long)n * C + c;
+        double A = 0.0, B = 0.0, Cc = 0.0;
+        for (int k = 0; k < nchunk; ++k) {
+            Sum3 p = parts[((long long)n * nchunk + k) * C + c];
+            A += p.a; B += p.b; Cc += p.c;
         }
+        vmax[c] = fmaf(ymax[nc], sc[nc], sh[nc]);
+        float g = ca[nc];
+        dpc[c] = (float)A * g * (1.f - g);
+        S1[c] = (float)B;
+        S2[c] = (float)Cc;
+    }
+    __syncthreads();
+    for (int j = 0; j < Cr; ++j) {
+        float a = 0.f, b = 0.f;
+        for (int c = tid; c < C; c += blockDim.x) {
+            a = fmaf(w1[j * C + c], vmax[c], a);
+            b = fmaf(w2[c * Cr + j], dpc[c], b);
+        }
+        a = wave_sum(a);
+        b = wave_sum(b);
+        if ((tid & 63) == 0) { red[0][tid >> 6] = a; red[1][tid >> 6] = b; }
         __syncthreads();
-        for (int j = tid; j < Cr; j += blockDim.x) {
-            float hpre = 0.f, dh = 0.f;
-            for (int c = 0; c < C; ++c) {
-                hpre = fmaf(w1[j * C + c], vmax[c], hpre);
-                dh = fmaf(w2[c * Cr + j], dpc[c], dh);
-            }
+        if (tid == 0) {
+            float hpre = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+            float dh = red[1][0] + red[1][1] + red[1][2] + red[1][3];
             hp[j] = hpre;
             dhm[j] = hpre > 0.f ? dh : 0.f;   // avg branch: relu'(0) = 0 -> no gradient
         }
         __syncthreads();
-        for (int c = tid; c < C; c += blockDim.x) {
-            float dvm = 0.f;
-            for (int j = 0; j < Cr; ++j) {
-                dvm = fmaf(w1[j * C + c], dhm[j], dvm);
-                dw2[c * Cr + j] += dpc[c] * (hp[j] > 0.f ? hp[j] : 0.f);
-                dw1[j * C + c] += dhm[j] * vmax[c];
-            }
-            // dz = dz0 + dvmax * [p == argmax]; sum_p z = 0 (IN output), z[argmax] = vmax
-            const float inv = 1.f / (float)HW;
-            coef[(long long)n * C + c] = Sum3{(S1[c] + dvm) * inv, (S2[c] + dvm * vmax[c]) * inv, dvm};
-        }
-        __syncthreads();
     }
+    float* dw1 = dwpart + (long long)n * 2 * C * Cr;
+    float* dw2 = dw1 + (long long)C * Cr;
+    const float inv = 1.f / (float)HW;
+    for (int c = tid; c < C; c += blockDim.x) {
+        float dvm = 0.f;
+        for (int j = 0; j < Cr; ++j) {
+            dvm = fmaf(w1[j * C + c], dhm[j], dvm);
+            dw2[c * Cr + j] = dpc[c] * (hp[j] > 0.f ? hp[j] : 0.f);
+            dw1[j * C + c] = dhm[j] * vmax[c];
+        }
+        // dz = dz0 + dvmax * [p == argmax]; sum_p z = 0 (IN output), z[argmax] = vmax
+        coef[(long long)n * C + c] = Sum3{(S1[c] + dvm) * inv, (S2[c] + dvm * vmax[c]) * inv, dvm};
+    }
+}
+
+__global__ void cb_bwd_dw_reduce_kernel(const float* __restrict__ dwpart, int N, int CCr, float* __restrict__ dw1,
+                                        float* __restrict__ dw2) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * CCr) return;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dwpart[(long long)n * 2 * CCr + i];
+    if (i < CCr) dw1[i] = s;
+    else dw2[i - CCr] = s;
 }
 
 // b5: dy = scale*(dz - mean(dz) - z*mean(dz*z))
@@ -364,9 +381,10 @@ struct CbWs {
     float* wpart;
     Sum3* parts;
     Sum3* coef;
+    float* dwpart;
     size_t total;
 };
-static CbWs cb_layout(void* base, int N, int H, int W, int C, int ksa) {
+static CbWs cb_layout(void* base, int N, int H, int W, int C, int Cr, int ksa) {
     CbWs w;
     long long P = (long long)N * H * W;
     size_t off = 0;
@@ -377,6 +395,7 @@ static CbWs cb_layout(void* base, int N, int H, int W, int C, int ksa) {
     int nch = cb_chunks(N, H * W);
     w.parts = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * nch * C * sizeof(Sum3), 256);
     w.coef = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * C * sizeof(Sum3), 256);
+    w.dwpart = reinterpret_cast<float*>(b + off); off = align_up(off + (size_t)N * 2 * C * Cr * sizeof(float), 256);
     w.total = off;
     return w;
 }
@@ -409,9 +428,8 @@ extern "C" int dcs_cbam_forward(const float* x, const float* y, const float* sca
 }
 
 extern "C" size_t dcs_cbam_backward_workspace_size(int N, int H, int W, int C, int Cr, int ksa) {
-    (void)Cr;
-    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || ksa <= 0) return 0;
-    return cb_layout(nullptr, N, H, W, C, ksa).total;
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cr <= 0 || ksa <= 0) return 0;
+    return cb_layout(nullptr, N, H, W, C, Cr, ksa).total;
 }
 
 extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float* scale, const float* shift,
@@ -426,7 +444,7 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
         return fail(DCS_E_INVALID, "cbam_backward: bad dims");
     if (ws_bytes < dcs_cbam_backward_workspace_size(N, H, W, C, Cr, ksa))
         return fail(DCS_E_WORKSPACE, "cbam_backward: workspace too small");
-    CbWs w = cb_layout(ws, N, H, W, C, ksa);
+    CbWs w = cb_layout(ws, N, H, W, C, Cr, ksa);
     hipStream_t s = as_stream(stream);
     const long long P = (long long)N * H * W;
     const int HW = H * W;
@@ -447,9 +465,12 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     hipLaunchKernelGGL(cb_bwd_sums_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin, sarg,
                        HW, C, nch, w.parts);
     if ((e = check_launch("cb_bwd_sums"))) return e;
-    hipLaunchKernelGGL(cb_bwd_ca_kernel, dim3(1), dim3(256), (size_t)(4 * C + 2 * Cr) * sizeof(float), s, w.parts, nch,
-                       ymax, scale, shift, ca, w1, w2, N, HW, C, Cr, w.coef, dw1, dw2);
+    hipLaunchKernelGGL(cb_bwd_ca_kernel, dim3(N), dim3(256), (size_t)(4 * C + 2 * Cr) * sizeof(float), s, w.parts, nch,
+                       ymax, scale, shift, ca, w1, w2, HW, C, Cr, w.coef, w.dwpart);
     if ((e = check_launch("cb_bwd_ca"))) return e;
+    hipLaunchKernelGGL(cb_bwd_dw_reduce_kernel, dim3((unsigned)cdiv(2LL * C * Cr, 256)), dim3(256), 0, s, w.dwpart, N,
+                       C * Cr, dw1, dw2);
+    if ((e = check_launch("cb_bwd_dw_reduce"))) return e;
     const long long total = P * C;
     hipLaunchKernelGGL(cb_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dout, y, scale, shift, ca,
                        sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy);

@@ -154,16 +154,20 @@ __device__ __forceinline__ float gather1(const dcs_conv_desc& d, const float* __
 // weight packing
 // ---------------------------------------------------------------------------------------
 __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
-                                    int kind, int ci_count, int Kpad, int ldb, float* __restrict__ out) {
+                                    int kind, int ci_count, int Kpad, int ncols, int nmajor,
+                                    float* __restrict__ out) {
+    // element (k, col) of the logical [Kpad][ncols] GEMM B matrix; stored N-major
+    // ([ncols][Kpad], MFMA rows pass) or K-major ([Kpad][ncols], narrow kernels)
     long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    long long total = (long long)Kpad * ldb;
+    long long total = (long long)Kpad * ncols;
     if (idx >= total) return;
-    int k = (int)(idx / ldb), col = (int)(idx - (long long)k * ldb);
+    int k, col;
+    if (nmajor) { col = (int)(idx / Kpad); k = (int)(idx - (long long)col * Kpad); }
+    else { k = (int)(idx / ncols); col = (int)(idx - (long long)k * ncols); }
     int taps = KH * KW;
     float v = 0.f;
     if (kind == 0) {  // B[(tap)*Cin + ci][co]
-        int cin_eff = ci_count;
-        int tap = k / cin_eff, ci = k - tap * cin_eff;
+        int tap = k / Cin, ci = k - tap * Cin;
         if (tap < taps && col < Cout) {
             int ty = tap / KW, tx = tap - ty * KW;
             v = w[(((long long)col * Cin + ci) * KH + ty) * KW + tx];
@@ -181,30 +185,83 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
 
 // ---------------------------------------------------------------------------------------
 // rows pass: implicit GEMM on v_mfma_f32_32x32x2_f32
+//
+// LDS holds both operands k-contiguous ([row][32 k + 4 pad], 144-B rows: conflict-free for
+// ds_read_b128).  A k-tile of 32 is consumed in 16 MFMA k-steps with a permuted k order:
+// at step s, lane half h (lanes 0-31 / 32-63) supplies k = 16h + s for both A and B, so each
+// lane fetches its whole k-tile of fragments with 4 ds_read_b128 per 32x32 block, issued
+// before the 64 MFMAs of the tile (no per-step lgkmcnt waits).  The global loads of the next
+// k-tile are in flight during the MFMAs (register staging, one barrier per k-tile).
+// Workgroups are remapped XCD-aware: each XCD walks a contiguous range of (M tile, N tile)
+// pairs with the N tiles of one M tile adjacent, so im2col re-reads hit the XCD's L2.
 // ---------------------------------------------------------------------------------------
-// TAG only separates instantiations in profiles: 1 = the 256-ch 3x3 residual-block conv
-// (forward and data-gradient), the north-star kernel.
+constexpr int LDK = BK + 4;  // padded k row (floats)
+
+__device__ __forceinline__ int xcd_remap(int L, int T) {
+    // bijective: blocks L, L+8, ... share an XCD under round-robin dispatch
+    const int xcd = L & 7, q = T >> 3, r = T & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (L >> 3);
+}
+
+// One k-tile (32 k) of MFMAs.  Two-level fp32 summation: the 16 k-steps of a tile chain into
+// a fresh accumulator that is then added to the running total, so a K-long reduction is a
+// 32-long chain plus a K/32-long chain instead of one K-long fma chain (K = 2304 for the
+// residual conv): ~4x smaller rounding growth for 64 extra VGPRs and 64 v_add per tile.
+template <int IM, int JN>
+__device__ __forceinline__ void mfma_ktile(const float4 (&af)[IM][4], const float4 (&bf)[JN][4],
+                                           floatx16 (&acc)[IM][JN]) {
+    floatx16 t[IM][JN];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    const float a = e == 0 ? af[i][q].x : e == 1 ? af[i][q].y : e == 2 ? af[i][q].z : af[i][q].w;
+                    const float b = e == 0 ? bf[j][q].x : e == 1 ? bf[j][q].y : e == 2 ? bf[j][q].z : bf[j][q].w;
+                    if (q == 0 && e == 0) {
+                        floatx16 zero = {};
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, zero, 0, 0, 0);
+                    } else {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, t[i][j], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] += t[i][j];
+}
+
 template <int BM, int BN, bool VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const dcs_conv_desc d, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
-    const float* __restrict__ psh, float* __restrict__ out) {
+    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy) {
     static_assert(BM == 128, "A loader assumes 128 rows (2 threads per row)");
     constexpr int WM = BM / 2, WN = BN / 2;        // per-wave tile
     constexpr int IM = WM / 32, JN = WN / 32;      // 32x32 blocks per wave
-    constexpr int LDA = BM + 4, LDB = BN + 4;
-    constexpr int BCH = (BK * BN / 4) / NT;        // float4 chunks of B per thread
+    constexpr int BTPR = NT / BN;                  // B loader threads per row (2 or 4)
+    constexpr int BKPT = BK / BTPR;                // k per B-loader thread (16 or 8)
+    constexpr int BCH = BKPT / 4;                  // float4 per B-loader thread
 
-    __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+    __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
     __shared__ long long rowoff[BM];
 
-    const int z = blockIdx.z;
+    const int T = gridDim.x;
+    const int L = xcd_remap(blockIdx.x, T);
+    const int ntile = L % gy;
+    const int rest = L / gy;
+    const int mtile = rest % gx;
+    const int z = rest / gx;
     const ClassGeom g = class_geom(d, z);
     const long long M = (long long)g.My * g.Mx * d.N;
-    const long long m0 = (long long)blockIdx.x * BM;
+    const long long m0 = (long long)mtile * BM;
     if (m0 >= M) return;
-    const int n0 = blockIdx.y * BN;
+    const int n0 = ntile * BN;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
@@ -214,6 +271,9 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const RowInfo ri = row_info(d, g, (int)(m0 + arow));
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     const bool rvalid = ri.out_off >= 0;
+    // B loader: one output channel row, BKPT consecutive k
+    const int brow = tid / BTPR, bkq = (tid % BTPR) * BKPT;
+    const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
     const int K = g.ntaps * d.Cs;
     const int nkt = (K + BK - 1) / BK;
@@ -253,36 +313,28 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
             }
         }
     };
-    // B loader: 8 threads per k-row, BN/8 consecutive columns each
-    const int bkr = tid >> 3, bc0 = (tid & 7) * (BN / 8);
     auto load_b = [&](int kt) {
-        const int k = kt * BK + bkr;
-        long long row;
+        const int k = kt * BK + bkq;
+        long long col;
         bool ok = true;
         if (!d.parity) {
-            row = k;
-        } else {
+            col = k;
+        } else {  // the BKPT k of this thread share one tap (Cs % 16 == 0)
             int j = k / d.Cs, c = k - j * d.Cs;
             ok = j < g.ntaps;
             int ady, adx, bt = 0;
             if (ok) tap_decode(d, g, j, ady, adx, bt);
-            row = (long long)bt * d.Cs + c;
+            col = (long long)bt * d.Cs + c;
         }
-        const float* bp = wp + row * d.ldb + n0 + bc0;
 #pragma unroll
         for (int i = 0; i < BCH; ++i)
-            rb[i] = ok ? *reinterpret_cast<const float4*>(bp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rb[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
     auto store_tiles = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            As[buf][akq + 4 * i + 0][arow] = ra[i].x;
-            As[buf][akq + 4 * i + 1][arow] = ra[i].y;
-            As[buf][akq + 4 * i + 2][arow] = ra[i].z;
-            As[buf][akq + 4 * i + 3][arow] = ra[i].w;
-        }
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][bkr][bc0 + 4 * i]) = rb[i];
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
     };
 
     floatx16 acc[IM][JN];
@@ -298,24 +350,22 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     store_tiles(0);
     __syncthreads();
 
-    const int l32 = lane & 31, lk = lane >> 5;
+    const int l32 = lane & 31, lk = (lane >> 5) * 16;
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
+        float4 af[IM][4], bf[JN][4];
 #pragma unroll
-        for (int ks = 0; ks < BK / 2; ++ks) {
-            const int k = 2 * ks + lk;
-            float a[IM], b[JN];
+        for (int i = 0; i < IM; ++i)
 #pragma unroll
-            for (int i = 0; i < IM; ++i) a[i] = As[cur][k][wm * WM + i * 32 + l32];
+            for (int q = 0; q < 4; ++q)
+                af[i][q] = *reinterpret_cast<const float4*>(&As[cur][wm * WM + i * 32 + l32][lk + 4 * q]);
 #pragma unroll
-            for (int j = 0; j < JN; ++j) b[j] = Bs[cur][k][wn * WN + j * 32 + l32];
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
-            for (int i = 0; i < IM; ++i)
-#pragma unroll
-                for (int j = 0; j < JN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-        }
+            for (int q = 0; q < 4; ++q)
+                bf[j][q] = *reinterpret_cast<const float4*>(&Bs[cur][wn * WN + j * 32 + l32][lk + 4 * q]);
+        mfma_ktile<IM, JN>(af, bf, acc);
         if (kt + 1 < nkt) store_tiles(cur ^ 1);
         __syncthreads();
     }
@@ -330,7 +380,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
         for (int i = 0; i < IM; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                const int row = wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 const long long off = rowoff[row];
                 if (off < 0) continue;
                 float v = acc[i][j][r] + bv;
@@ -344,26 +394,31 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 // ---------------------------------------------------------------------------------------
 // wgrad pass: dW[co][k] = sum_p dy[p][co] * A[p][k]  (split over pixels -> partial slabs)
 // ---------------------------------------------------------------------------------------
+// Same LDS layout and inner loop as the rows pass; both operands arrive pixel-major, so each
+// loader thread fetches the same 4 columns (float4) of BM/32 consecutive pixels and writes
+// them transposed as one vector per column (k = pixel contiguous in LDS).
 template <int BM, int BN, bool VEC>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     const dcs_conv_desc d, const float* __restrict__ dy, const float* __restrict__ src,
     const float* __restrict__ src2, const float* __restrict__ psc, const float* __restrict__ psh,
-    float* __restrict__ ws, int kt_per_split) {
+    float* __restrict__ ws, int kt_per_split, int gn, int gm) {
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int IM = WM / 32, JN = WN / 32;
-    constexpr int LDA = BM + 4, LDB = BN + 4;
-    constexpr int ACH = (BK * BM / 4) / NT;
-    constexpr int BCH = (BK * BN / 4) / NT;
+    constexpr int APT = BM / 32, BPT = BN / 32;   // pixels per loader thread
+    constexpr int AG = BM / 4, BG = BN / 4;       // float4 column groups
 
-    __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+    __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
 
     const ClassGeom g = class_geom(d, 0);
     const long long P = (long long)g.My * g.Mx * d.N;   // pixels (reduction)
     const int Ktot = g.ntaps * d.Cs;                    // GEMM N
-    const int m0 = blockIdx.y * BM;                     // output channel tile
-    const int n0 = blockIdx.x * BN;                     // (tap, ci) tile
-    const int split = blockIdx.z;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = L % gn;
+    const int mtile = (L / gn) % gm;
+    const int split = L / (gn * gm);
+    const int m0 = mtile * BM;                          // output channel tile
+    const int n0 = ntile * BN;                          // (tap, ci) tile
     const long long nkt_all = (P + BK - 1) / BK;
     const long long kt_beg = (long long)split * kt_per_split;
     long long kt_end = kt_beg + kt_per_split;
@@ -371,31 +426,29 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
+    const int ag = tid % AG, ap0 = (tid / AG) * APT;
+    const int bg = tid % BG, bp0 = (tid / BG) * BPT;
 
-    float4 ra[ACH];
-    float4 rb[BCH];
+    float4 ra[APT];
+    float4 rb[BPT];
 
-    // both loaders: 8 threads per k-row (pixel), each a run of consecutive columns
-    const int kr = tid >> 3;
-    const int ac0 = (tid & 7) * (BM / 8), bc0 = (tid & 7) * (BN / 8);
-    auto load_a = [&](long long kt) {  // dy rows: [p][co]
-        const long long p = kt * BK + kr;
-        const int co = m0 + ac0;
-        const bool ok = p < P;
+    auto load_a = [&](long long kt) {  // dy[p][m0 + 4ag .. +3]
+        const int co = m0 + ag * 4;
 #pragma unroll
-        for (int i = 0; i < ACH; ++i)
-            ra[i] = (ok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
-                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < APT; ++i) {
+            const long long p = kt * BK + ap0 + i;
+            ra[i] = (p < P && co < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     };
-    auto load_b = [&](long long kt) {  // gathered source rows: [p][(tap, ci)]
-        const long long p = kt * BK + kr;
-        const RowInfo ri = row_info(d, g, (int)(p < P ? p : P));
-        const bool ok = ri.out_off >= 0;
+    auto load_b = [&](long long kt) {  // gathered source columns n0 + 4bg .. +3 of pixels
+        const int nn = n0 + bg * 4;
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) {
-            const int nn = n0 + bc0 + 4 * i;
+        for (int i = 0; i < BPT; ++i) {
+            const long long p = kt * BK + bp0 + i;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (ok) {
+            if (p < P) {
+                const RowInfo ri = row_info(d, g, (int)p);
                 if (VEC) {
                     if (nn < Ktot) {
                         int j = nn / d.Cs, c = nn - j * d.Cs;
@@ -423,10 +476,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         }
     };
     auto store_tiles = [&](int buf) {
+        // column e of the float4 group -> LDS row (4g+e), pixels ap0..ap0+APT-1 contiguous
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * i]) = ra[i];
+        for (int e = 0; e < 4; ++e) {
+            float* a = &As[buf][ag * 4 + e][ap0];
+            float* b = &Bs[buf][bg * 4 + e][bp0];
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * i]) = rb[i];
+            for (int i = 0; i < APT; ++i) a[i] = e == 0 ? ra[i].x : e == 1 ? ra[i].y : e == 2 ? ra[i].z : ra[i].w;
+#pragma unroll
+            for (int i = 0; i < BPT; ++i) b[i] = e == 0 ? rb[i].x : e == 1 ? rb[i].y : e == 2 ? rb[i].z : rb[i].w;
+        }
     };
 
     floatx16 acc[IM][JN];
@@ -443,24 +502,22 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         store_tiles(0);
     }
     __syncthreads();
-    const int l32 = lane & 31, lk = lane >> 5;
+    const int l32 = lane & 31, lk = (lane >> 5) * 16;
     for (long long kt = kt_beg; kt < kt_end; ++kt) {
         const int cur = (int)((kt - kt_beg) & 1);
         if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
+        float4 af[IM][4], bf[JN][4];
 #pragma unroll
-        for (int ks = 0; ks < BK / 2; ++ks) {
-            const int k = 2 * ks + lk;
-            float a[IM], b[JN];
+        for (int i = 0; i < IM; ++i)
 #pragma unroll
-            for (int i = 0; i < IM; ++i) a[i] = As[cur][k][wm * WM + i * 32 + l32];
+            for (int q = 0; q < 4; ++q)
+                af[i][q] = *reinterpret_cast<const float4*>(&As[cur][wm * WM + i * 32 + l32][lk + 4 * q]);
 #pragma unroll
-            for (int j = 0; j < JN; ++j) b[j] = Bs[cur][k][wn * WN + j * 32 + l32];
+        for (int j = 0; j < JN; ++j)
 #pragma unroll
-            for (int i = 0; i < IM; ++i)
-#pragma unroll
-                for (int j = 0; j < JN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-        }
+            for (int q = 0; q < 4; ++q)
+                bf[j][q] = *reinterpret_cast<const float4*>(&Bs[cur][wn * WN + j * 32 + l32][lk + 4 * q]);
+        mfma_ktile<IM, JN>(af, bf, acc);
         if (kt + 1 < kt_end) store_tiles(cur ^ 1);
         __syncthreads();
     }
@@ -474,7 +531,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         for (int i = 0; i < IM; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 if (row < d.Co) slab[(long long)row * Ktot + col] = acc[i][j][r];
             }
     }
@@ -697,18 +754,27 @@ static bool vec_ok(const dcs_conv_desc* d, const float* src) {
            ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
 }
 
+// LDS-tiled single-output-channel kernels (conv_narrow.hip)
+bool narrow_tiled_ok(const dcs_conv_desc& d, const float* src);
+int launch_narrow_rows_tiled(const dcs_conv_desc& d, const float* src, const float* wp, const float* bias,
+                             const float* psc, const float* psh, float* out, hipStream_t s);
+bool narrow_wgrad_tiled_ok(const dcs_conv_desc& d, const float* src);
+int narrow_wgrad_tiled_blocks(const dcs_conv_desc& d);
+int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const float* src, const float* psc,
+                              const float* psh, float* part, hipStream_t s);
+
 }  // namespace dcs
 
 using namespace dcs;
 
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
-                                int Kpad, int ldb, float* out, void* stream) {
-    if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ldb <= 0 || ci_count <= 0 ||
+                                int Kpad, int ncols, int nmajor, float* out, void* stream) {
+    if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
         ci_count > Cin || kind < 0 || kind > 2)
         return fail(DCS_E_INVALID, "pack_weights: bad arguments");
-    long long total = (long long)Kpad * ldb;
+    long long total = (long long)Kpad * ncols;
     hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
-                       Cout, Cin, KH, KW, kind, ci_count, Kpad, ldb, out);
+                       Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
     return check_launch("pack_weights");
 }
 
@@ -721,7 +787,8 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     if (d.pro_act != DCS_ACT_NONE && (!psc || !psh)) return fail(DCS_E_INVALID, "conv_rows: missing prologue");
     if (d.csplit < d.Cs && !src2) return fail(DCS_E_INVALID, "conv_rows: missing src2");
     const int BN = d.Co > 64 ? 128 : 64;
-    if (d.ldb % BN != 0 || d.ldb < d.Co) return fail(DCS_E_INVALID, "conv_rows: ldb must be a multiple of the N tile");
+    if (d.ldb % BK != 0) return fail(DCS_E_INVALID, "conv_rows: ldb (packed K) must be a multiple of 32");
+    if (d.parity && d.Cs % 16 != 0) return fail(DCS_E_INVALID, "conv_rows: parity rows need Cs % 16 == 0");
     if (d.Co % 4 != 0) return fail(DCS_E_INVALID, "conv_rows: Co must be a multiple of 4 (use the narrow path)");
     long long Mmax = 0;
     const int ncls = d.parity ? 4 : 1;
@@ -730,18 +797,19 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
         long long M = (long long)g.My * g.Mx * d.N;
         if (M > Mmax) Mmax = M;
     }
-    dim3 grid((unsigned)cdiv(Mmax, 128), (unsigned)cdiv(d.Co, BN), ncls);
+    const int gx = (int)cdiv(Mmax, 128), gy = (int)cdiv(d.Co, BN);
+    dim3 grid((unsigned)(gx * gy * ncls));
     const bool vec = vec_ok(dp, src);
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
                      d.stride == 1;
     hipStream_t s = as_stream(stream);
     if (BN == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
-        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
     }
     return check_launch("conv_rows");
 }
@@ -788,16 +856,17 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     if (d.Co % 4 != 0) return fail(DCS_E_INVALID, "conv_wgrad: Co must be a multiple of 4");
     if (ws_bytes < dcs_conv_wgrad_workspace_size(dp)) return fail(DCS_E_WORKSPACE, "conv_wgrad: workspace too small");
     WgradPlan p = wgrad_plan(d);
-    dim3 grid((unsigned)cdiv(p.Ktot, p.BN), (unsigned)cdiv(d.Co, p.BM), p.nsplit);
+    const int gn = (int)cdiv(p.Ktot, p.BN), gm = (int)cdiv(d.Co, p.BM);
+    dim3 grid((unsigned)(gn * gm * p.nsplit));
     const bool vec = vec_ok(dp, x);
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
     if (p.BM == 128) {
-        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split);
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     }
     e = check_launch("conv_wgrad");
     if (e) return e;
@@ -827,9 +896,10 @@ extern "C" int dcs_conv_rows_narrow(const dcs_conv_desc* dp, const float* src, c
         long long M = (long long)g.My * g.Mx * d.N;
         if (M > Mmax) Mmax = M;
     }
+    hipStream_t s = as_stream(stream);
+    if (narrow_tiled_ok(d, src)) return launch_narrow_rows_tiled(d, src, wpack, bias, psc, psh, out, s);
     dim3 grid((unsigned)cdiv(Mmax, 256), ncls);
     const bool vec = vec_ok(dp, src);
-    hipStream_t s = as_stream(stream);
     // the kernel reads wp[k*ldb + o] for o < NO: ldb must cover NO columns
     if (d.ldb < NO) return fail(DCS_E_INVALID, "conv_rows_narrow: ldb must be >= 4 when Co > 1");
     if (NO == 1) {
@@ -863,7 +933,9 @@ extern "C" size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* dp) 
     int ns;
     narrow_pix_per_split(*dp, &ns);
     ClassGeom g = class_geom(*dp, 0);
-    return (size_t)ns * dp->Co * g.ntaps * dp->Cs * sizeof(float);
+    size_t naive = (size_t)ns * dp->Co * g.ntaps * dp->Cs * sizeof(float);
+    size_t tiled = (size_t)narrow_wgrad_tiled_blocks(*dp) * g.ntaps * dp->Cs * sizeof(float);
+    return naive > tiled ? naive : tiled;
 }
 
 extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, const float* x, const float* x2,
@@ -882,6 +954,13 @@ extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, c
     dim3 grid((unsigned)cdiv(Ktot, 256), ns);
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
+    if (narrow_wgrad_tiled_ok(d, x)) {
+        e = launch_narrow_wgrad_tiled(d, dy, x, psc, psh, w, s);
+        if (e) return e;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(Ktot, 256)), dim3(256), 0, s, w,
+                           narrow_wgrad_tiled_blocks(d), 1, d.Cs, d.KH, d.KW, dw);
+        return check_launch("narrow_wgrad_tiled_reduce");
+    }
     if (d.Co == 1) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<1, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
     else if (d.Co == 2) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<2, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
     else if (d.Co == 3) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<3, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);

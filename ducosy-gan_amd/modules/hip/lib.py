@@ -38,7 +38,7 @@ DP = POINTER(ConvDesc)
 SIGNATURES = {
     "dcs_last_error": (c_char_p, []),
     "dcs_version": (c_int, []),
-    "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "dcs_conv_rows": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_wgrad_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
@@ -106,13 +106,24 @@ def exported_symbols():
     return sorted(SIGNATURES)
 
 
+_SYNC_CHECK = os.environ.get("DUCOSY_SYNC_CHECK", "0") == "1"
+
+
 def call(name: str, *args) -> None:
-    """Call an int-returning entry point and raise on a non-zero status."""
+    """Call an int-returning entry point and raise on a non-zero status.  With
+    DUCOSY_SYNC_CHECK=1 every call is followed by a device synchronisation so an
+    asynchronous fault is attributed to the entry point that launched it (debug only)."""
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.dcs_last_error()
         raise HipLibraryError(f"{name} failed (status {rc}): {msg.decode() if msg else ''}")
+    if _SYNC_CHECK:
+        import torch
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:  # pragma: no cover - debug path
+            raise HipLibraryError(f"device fault after {name}: {e}") from e
 
 
 def query(name: str, *args) -> int:

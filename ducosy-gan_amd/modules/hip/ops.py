@@ -167,28 +167,31 @@ class ConvGeom:
 
     # ---- weight packing ------------------------------------------------------------
     def pack_fwd(self, w: torch.Tensor) -> torch.Tensor:
+        """B operand of the forward GEMM: N-major [Np][Kpad] for the MFMA rows pass (ldb =
+        Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns)."""
         K = self.k * self.k * self.cin
-        if self.narrow:
-            Kpad, ldb = K, (1 if self.cout == 1 else 4)
-        else:
-            Kpad, ldb = _round_up(K, 32), _round_up(self.cout, _bn_for(self.cout))
-        out = torch.empty(Kpad, ldb, device=w.device, dtype=torch.float32)
-        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, 0, self.cin, Kpad,
-                 ldb, _p(out), _stream())
-        return out
+        return self._pack(w, 0, self.cin, K, self.cout)
 
     def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
         ci = self.cin if ci_count is None else ci_count
         kind = 2 if self.stride == 2 else 1
         K = self.k * self.k * self.cout
-        if ci <= 4:
-            Kpad, ldb = K, (1 if ci == 1 else 4)
+        return self._pack(w, kind, ci, K, ci)
+
+    def _pack(self, w, kind, ci_count, K, ncols):
+        if ncols <= 4:
+            Kpad, cols, nmajor = K, (1 if ncols == 1 else 4), 0
+            out = torch.empty(Kpad, cols, device=w.device, dtype=torch.float32)
         else:
-            Kpad, ldb = _round_up(K, 32), _round_up(ci, _bn_for(ci))
-        out = torch.empty(Kpad, ldb, device=w.device, dtype=torch.float32)
-        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci, Kpad, ldb,
-                 _p(out), _stream())
+            Kpad, cols, nmajor = _round_up(K, 32), _round_up(ncols, _bn_for(ncols)), 1
+            out = torch.empty(cols, Kpad, device=w.device, dtype=torch.float32)
+        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
+                 cols, nmajor, _p(out), _stream())
         return out
+
+    @staticmethod
+    def _ldb(wpack: torch.Tensor, narrow: bool) -> int:
+        return wpack.shape[1]  # Kpad (N-major) or columns (K-major): always the inner dim
 
     # ---- descriptors ---------------------------------------------------------------
     def _desc_fwd(self, s: Src, ldb: int, pro_act: int, epi_act: int) -> lib.ConvDesc:

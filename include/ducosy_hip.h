@@ -66,7 +66,7 @@ typedef struct dcs_conv_desc {
     int32_t stride;                 /* forward stride (1 or 2)                            */
     int32_t parity;                 /* 0 regular rows, 1 stride-2 transposed parity rows  */
     int32_t Ho, Wo, Co;             /* output dims                                        */
-    int32_t ldb;                    /* row stride of the packed weight matrix             */
+    int32_t ldb;                    /* packed weights: Kpad (rows pass) / ncols (narrow)  */
     int32_t pro_act;                /* DCS_ACT_* prologue on the source                   */
     int32_t epi_act;                /* DCS_ACT_NONE / DCS_ACT_TANH / DCS_ACT_LRELU        */
 } dcs_conv_desc;
@@ -76,13 +76,15 @@ int dcs_version(void);
 
 /* ---- convolution family (modules/model.py:61-63,74-79,94-112,122-129 → aten conv) ---- */
 
-/* Pack OIHW weights into the GEMM B operand [Kpad][ldb] (zero padded).
+/* Pack OIHW weights into the GEMM B operand, logically [Kpad][ncols] (zero padded), stored
+ * N-major ([ncols][Kpad]; nmajor=1, for dcs_conv_rows, ldb = Kpad) or K-major ([Kpad][ncols];
+ * nmajor=0, for the narrow kernels, ldb = ncols).
  * kind 0 forward   : B[(ty*KW+tx)*Cin + ci][co] = W[co][ci][ty][tx]
  * kind 1 dgrad-flip: B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][KH-1-ty][KW-1-tx]  (stride-1 dgrad)
  * kind 2 dgrad     : B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][ty][tx]              (stride-2 dgrad)
  * ci_count limits the packed input channels (dgrad of a concat input needs only the first). */
 int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
-                     int Kpad, int ldb, float* out, void* stream);
+                     int Kpad, int ncols, int nmajor, float* out, void* stream);
 
 /* Forward / data-gradient pass: out = gather(src) x B (+ bias, epilogue act). */
 int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,
