@@ -208,6 +208,53 @@ __device__ __forceinline__ int xcd_remap(int L, int T) {
 // a fresh accumulator that is then added to the running total, so a K-long reduction is a
 // 32-long chain plus a K/32-long chain instead of one K-long fma chain (K = 2304 for the
 // residual conv): ~4x smaller rounding growth for 64 extra VGPRs and 64 v_add per tile.
+template <int IM, int JN, int Q0 = 0, int Q1 = 4>
+__device__ __forceinline__ void mfma_steps(const float4 (&af)[IM][4], const float4 (&bf)[JN][4],
+                                           floatx16 (&t)[IM][JN]) {
+#pragma unroll
+    for (int q = Q0; q < Q1; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    const float a = e == 0 ? af[i][q].x : e == 1 ? af[i][q].y : e == 2 ? af[i][q].z : af[i][q].w;
+                    const float b = e == 0 ? bf[j][q].x : e == 1 ? bf[j][q].y : e == 2 ? bf[j][q].z : bf[j][q].w;
+                    if (q == 0 && e == 0) {
+                        floatx16 zero = {};
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, zero, 0, 0, 0);
+                    } else {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, t[i][j], 0, 0, 0);
+                    }
+                }
+}
+
+template <int IM, int JN, int Q0, int Q1>
+__device__ __forceinline__ void mfma_chain(const float4 (&af)[IM][4], const float4 (&bf)[JN][4],
+                                           floatx16 (&t)[IM][JN]) {
+#pragma unroll
+    for (int q = Q0; q < Q1; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    const float a = e == 0 ? af[i][q].x : e == 1 ? af[i][q].y : e == 2 ? af[i][q].z : af[i][q].w;
+                    const float b = e == 0 ? bf[j][q].x : e == 1 ? bf[j][q].y : e == 2 ? bf[j][q].z : bf[j][q].w;
+                    t[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, t[i][j], 0, 0, 0);
+                }
+}
+
+template <int IM, int JN>
+__device__ __forceinline__ void acc_add(floatx16 (&acc)[IM][JN], const floatx16 (&t)[IM][JN]) {
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) acc[i][j] += t[i][j];
+}
+
 template <int IM, int JN>
 __device__ __forceinline__ void mfma_ktile(const float4 (&af)[IM][4], const float4 (&bf)[JN][4],
                                            floatx16 (&acc)[IM][JN]) {
@@ -246,6 +293,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     constexpr int BTPR = NT / BN;                  // B loader threads per row (2 or 4)
     constexpr int BKPT = BK / BTPR;                // k per B-loader thread (16 or 8)
     constexpr int BCH = BKPT / 4;                  // float4 per B-loader thread
+    constexpr int KT2 = 4;                         // k-tiles per inner accumulation chain
 
     __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
@@ -266,7 +314,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
 
-    // A loader: one row, 16 consecutive k
+    // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap)
     const int arow = tid >> 1, akq = (tid & 1) * 16;
     const RowInfo ri = row_info(d, g, (int)(m0 + arow));
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
@@ -277,23 +325,40 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 
     const int K = g.ntaps * d.Cs;
     const int nkt = (K + BK - 1) / BK;
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    const float* srow = src + ri.n * d.s_n;
+    const long long so = (long long)ri.n * d.Cs;
+
+    // incremental (tap, channel) state of the next k-tile to load, for A and B
+    int aj = akq / d.Cs, ac = akq - (akq / d.Cs) * d.Cs;
+    int bj = bkq / d.Cs, bc = bkq - (bkq / d.Cs) * d.Cs;
+    auto advance = [&](int& j, int& c) {
+        c += BK;
+        while (c >= d.Cs) { c -= d.Cs; ++j; }
+    };
 
     float4 ra[4];
     float4 rb[BCH];
 
     auto load_a = [&](int kt) {
         if (VEC) {
+            ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rvalid && aj < g.ntaps) {
+                int ady, adx, bt;
+                tap_decode(d, g, aj, ady, adx, bt);
+                int sy, sx;
+                if (map_coord(ri.by + ady, Hv, d.up, d.pad_mode, sy) &&
+                    map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx)) {
+                    const float* sp = srow + sy * d.s_h + sx * d.s_w + ac;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                int k = kt * BK + akq + 4 * i;
-                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-                int j = k / d.Cs, c = k - j * d.Cs;
-                if (rvalid && j < g.ntaps) {
-                    int ady, adx, bt;
-                    tap_decode(d, g, j, ady, adx, bt);
-                    ra[i] = gather4(d, src, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                    for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
+                    if (d.pro_act != DCS_ACT_NONE) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
+                    }
                 }
             }
+            advance(aj, ac);
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -314,17 +379,16 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
         }
     };
     auto load_b = [&](int kt) {
-        const int k = kt * BK + bkq;
         long long col;
         bool ok = true;
         if (!d.parity) {
-            col = k;
+            col = kt * BK + bkq;
         } else {  // the BKPT k of this thread share one tap (Cs % 16 == 0)
-            int j = k / d.Cs, c = k - j * d.Cs;
-            ok = j < g.ntaps;
+            ok = bj < g.ntaps;
             int ady, adx, bt = 0;
-            if (ok) tap_decode(d, g, j, ady, adx, bt);
-            col = (long long)bt * d.Cs + c;
+            if (ok) tap_decode(d, g, bj, ady, adx, bt);
+            col = (long long)bt * d.Cs + bc;
+            advance(bj, bc);
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i)
@@ -337,13 +401,13 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
         for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
     };
 
-    floatx16 acc[IM][JN];
+    floatx16 acc[IM][JN], t[IM][JN];
 #pragma unroll
     for (int i = 0; i < IM; ++i)
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
     load_a(0);
     load_b(0);
@@ -353,7 +417,6 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const int l32 = lane & 31, lk = (lane >> 5) * 16;
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
         float4 af[IM][4], bf[JN][4];
 #pragma unroll
         for (int i = 0; i < IM; ++i)
@@ -365,7 +428,21 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 bf[j][q] = *reinterpret_cast<const float4*>(&Bs[cur][wn * WN + j * 32 + l32][lk + 4 * q]);
-        mfma_ktile<IM, JN>(af, bf, acc);
+        // MFMAs of the tile in two halves with the next tile's gather in between; the inner
+        // chain t spans KT2 k-tiles (two-level summation, see mfma_ktile)
+        mfma_chain<IM, JN, 0, 2>(af, bf, t);
+        if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
+        mfma_chain<IM, JN, 2, 4>(af, bf, t);
+        if ((kt % KT2) == KT2 - 1 || kt + 1 == nkt) {
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    acc[i][j] += t[i][j];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                }
+        }
         if (kt + 1 < nkt) store_tiles(cur ^ 1);
         __syncthreads();
     }
@@ -394,9 +471,11 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 // ---------------------------------------------------------------------------------------
 // wgrad pass: dW[co][k] = sum_p dy[p][co] * A[p][k]  (split over pixels -> partial slabs)
 // ---------------------------------------------------------------------------------------
-// Same LDS layout and inner loop as the rows pass; both operands arrive pixel-major, so each
-// loader thread fetches the same 4 columns (float4) of BM/32 consecutive pixels and writes
-// them transposed as one vector per column (k = pixel contiguous in LDS).
+// Both operands arrive pixel-major (k-major), so LDS keeps them as [k][m] / [k][n] rows
+// (m/n contiguous, padded by 4): every loader thread moves float4 runs straight from global
+// to LDS (8 threads per pixel row, one pixel decode per thread per k-tile).  A lane's MFMA
+// operands are single floats down a column ([2s+h][m]); all 16 k-steps of a tile are read
+// into registers before the tile's MFMAs so LDS latency is paid once per tile.
 template <int BM, int BN, bool VEC>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     const dcs_conv_desc d, const float* __restrict__ dy, const float* __restrict__ src,
@@ -404,11 +483,12 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     float* __restrict__ ws, int kt_per_split, int gn, int gm) {
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int IM = WM / 32, JN = WN / 32;
-    constexpr int APT = BM / 32, BPT = BN / 32;   // pixels per loader thread
-    constexpr int AG = BM / 4, BG = BN / 4;       // float4 column groups
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int ACH = (BK * BM / 4) / NT;
+    constexpr int BCH = (BK * BN / 4) / NT;
 
-    __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
+    __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
 
     const ClassGeom g = class_geom(d, 0);
     const long long P = (long long)g.My * g.Mx * d.N;   // pixels (reduction)
@@ -426,75 +506,107 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int ag = tid % AG, ap0 = (tid / AG) * APT;
-    const int bg = tid % BG, bp0 = (tid / BG) * BPT;
+    const int kr = tid >> 3;
+    const int ac0 = (tid & 7) * (BM / 8), bc0 = (tid & 7) * (BN / 8);
 
-    float4 ra[APT];
-    float4 rb[BPT];
+    float4 ra[ACH];
+    float4 rb[BCH];
 
-    auto load_a = [&](long long kt) {  // dy[p][m0 + 4ag .. +3]
-        const int co = m0 + ag * 4;
-#pragma unroll
-        for (int i = 0; i < APT; ++i) {
-            const long long p = kt * BK + ap0 + i;
-            ra[i] = (p < P && co < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    // B columns of this thread are fixed for the whole kernel: with VEC (Cs % 16 == 0) its
+    // BN/8 consecutive columns share one tap -> decode once.
+    const int nb0 = n0 + bc0;
+    const bool bcol_ok = nb0 < Ktot;
+    int bady = 0, badx = 0, bchan = 0;
+    if (VEC && bcol_ok) {
+        const int j = nb0 / d.Cs;
+        bchan = nb0 - j * d.Cs;
+        int bt;
+        tap_decode(d, g, j, bady, badx, bt);
+    }
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    // incremental pixel state of the NEXT k-tile row this thread loads (p = kt*BK + kr)
+    int pn = 0, pqy = 0, pqx = 0;
+    {
+        const long long p = kt_beg * BK + kr;
+        if (p < P) {
+            const int per = g.My * g.Mx;
+            pn = (int)(p / per);
+            const int rem = (int)(p - (long long)pn * per);
+            pqy = rem / g.Mx;
+            pqx = rem - pqy * g.Mx;
         }
+    }
+    auto advance_pix = [&]() {
+        pqx += BK;
+        while (pqx >= g.Mx) { pqx -= g.Mx; if (++pqy == g.My) { pqy = 0; ++pn; } }
     };
-    auto load_b = [&](long long kt) {  // gathered source columns n0 + 4bg .. +3 of pixels
-        const int nn = n0 + bg * 4;
+
+    auto load_a = [&](long long kt) {  // dy rows: [p][co]
+        const long long p = kt * BK + kr;
+        const int co = m0 + ac0;
+        const bool ok = p < P;
 #pragma unroll
-        for (int i = 0; i < BPT; ++i) {
-            const long long p = kt * BK + bp0 + i;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (p < P) {
-                const RowInfo ri = row_info(d, g, (int)p);
-                if (VEC) {
-                    if (nn < Ktot) {
-                        int j = nn / d.Cs, c = nn - j * d.Cs;
-                        int ady, adx, bt;
-                        tap_decode(d, g, j, ady, adx, bt);
-                        v = gather4(d, src, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
-                    }
-                } else {
-                    float e[4];
+        for (int i = 0; i < ACH; ++i)
+            ra[i] = (ok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto load_b = [&](long long kt) {  // gathered source rows: [p][(tap, ci)]
+        const long long p = kt * BK + kr;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        e[q] = 0.f;
-                        int n1 = nn + q;
-                        if (n1 < Ktot) {
-                            int j = n1 / d.Cs, c = n1 - j * d.Cs;
-                            int ady, adx, bt;
-                            tap_decode(d, g, j, ady, adx, bt);
-                            e[q] = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+        for (int i = 0; i < BCH; ++i) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (VEC) {
+            if (p < P && bcol_ok) {
+                const int vy = pqy * d.stride - d.pt + bady, vx = pqx * d.stride - d.pl + badx;
+                int sy, sx;
+                if (map_coord(vy, Hv, d.up, d.pad_mode, sy) && map_coord(vx, Wv, d.up, d.pad_mode, sx)) {
+                    const float* sp = src + pn * d.s_n + sy * d.s_h + sx * d.s_w + bchan;
+                    const long long o = (long long)pn * d.Cs + bchan;
+#pragma unroll
+                    for (int i = 0; i < BCH; ++i) {
+                        if (nb0 + 4 * i < Ktot) {
+                            rb[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
+                            if (d.pro_act != DCS_ACT_NONE)
+                                rb[i] = affine_act4(rb[i], psc + o + 4 * i, psh + o + 4 * i, d.pro_act);
                         }
                     }
-                    v = make_float4(e[0], e[1], e[2], e[3]);
                 }
             }
-            rb[i] = v;
+            advance_pix();
+        } else if (p < P) {
+            const RowInfo ri = row_info(d, g, (int)p);
+#pragma unroll
+            for (int i = 0; i < BCH; ++i) {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    e[q] = 0.f;
+                    const int n1 = nb0 + 4 * i + q;
+                    if (n1 < Ktot) {
+                        int j = n1 / d.Cs, c = n1 - j * d.Cs;
+                        int ady, adx, bt;
+                        tap_decode(d, g, j, ady, adx, bt);
+                        e[q] = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
+                    }
+                }
+                rb[i] = make_float4(e[0], e[1], e[2], e[3]);
+            }
         }
     };
     auto store_tiles = [&](int buf) {
-        // column e of the float4 group -> LDS row (4g+e), pixels ap0..ap0+APT-1 contiguous
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float* a = &As[buf][ag * 4 + e][ap0];
-            float* b = &Bs[buf][bg * 4 + e][bp0];
+        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * i]) = ra[i];
 #pragma unroll
-            for (int i = 0; i < APT; ++i) a[i] = e == 0 ? ra[i].x : e == 1 ? ra[i].y : e == 2 ? ra[i].z : ra[i].w;
-#pragma unroll
-            for (int i = 0; i < BPT; ++i) b[i] = e == 0 ? rb[i].x : e == 1 ? rb[i].y : e == 2 ? rb[i].z : rb[i].w;
-        }
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * i]) = rb[i];
     };
 
-    floatx16 acc[IM][JN];
+    constexpr int KT2 = 4;  // k-tiles per inner accumulation chain (two-level summation)
+    floatx16 acc[IM][JN], t[IM][JN];
 #pragma unroll
     for (int i = 0; i < IM; ++i)
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
     if (kt_beg < kt_end) {
         load_a(kt_beg);
@@ -502,22 +614,44 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         store_tiles(0);
     }
     __syncthreads();
-    const int l32 = lane & 31, lk = (lane >> 5) * 16;
+    const int l32 = lane & 31, lh = lane >> 5;
     for (long long kt = kt_beg; kt < kt_end; ++kt) {
         const int cur = (int)((kt - kt_beg) & 1);
-        if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
+        // fragments of all 16 k-steps (lane half h takes k = 2s + h)
         float4 af[IM][4], bf[JN][4];
 #pragma unroll
         for (int i = 0; i < IM; ++i)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                af[i][q] = *reinterpret_cast<const float4*>(&As[cur][wm * WM + i * 32 + l32][lk + 4 * q]);
+            for (int q = 0; q < 4; ++q) {
+                const float* a = &As[cur][8 * q + lh][wm * WM + i * 32 + l32];
+                af[i][q] = make_float4(a[0], a[2 * LDA], a[4 * LDA], a[6 * LDA]);
+            }
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                bf[j][q] = *reinterpret_cast<const float4*>(&Bs[cur][wn * WN + j * 32 + l32][lk + 4 * q]);
-        mfma_ktile<IM, JN>(af, bf, acc);
+            for (int q = 0; q < 4; ++q) {
+                const float* b = &Bs[cur][8 * q + lh][wn * WN + j * 32 + l32];
+                bf[j][q] = make_float4(b[0], b[2 * LDB], b[4 * LDB], b[6 * LDB]);
+            }
+        if constexpr (VEC) {
+            mfma_chain<IM, JN, 0, 2>(af, bf, t);
+            if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
+            mfma_chain<IM, JN, 2, 4>(af, bf, t);
+            const long long rel = kt - kt_beg;
+            if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        acc[i][j] += t[i][j];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
+        } else {  // small-Cs gathers (stem, first PatchGAN layer): short K chains, one level
+            mfma_chain<IM, JN, 0, 4>(af, bf, acc);
+            if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
+        }
         if (kt + 1 < kt_end) store_tiles(cur ^ 1);
         __syncthreads();
     }
@@ -749,7 +883,7 @@ static int validate(const dcs_conv_desc* d, bool rows) {
 }
 
 static bool vec_ok(const dcs_conv_desc* d, const float* src) {
-    return (d->Cs % 4 == 0) && d->s_c == 1 && d->csplit == d->Cs &&
+    return (d->Cs % 16 == 0) && d->s_c == 1 && d->csplit == d->Cs &&
            (d->s_w % 4 == 0) && (d->s_h % 4 == 0) && (d->s_n % 4 == 0) &&
            ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
 }

@@ -1,0 +1,83 @@
+"""Per-layer kernel timings at the production shapes (512x512 slices, batch 8).
+
+    python scripts/kbench.py [--batch 8] [--reps 5] [--only res]
+
+For every convolution of the Generator / Discriminator: forward, data-gradient and
+weight-gradient launch time (HIP events, median of reps) and algorithmic TFLOP/s
+(2 * out_pixels * Cout * Cin * k * k per pass).  Product code only (no oracle).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(ROOT, "ducosy-gan_amd"))
+
+import torch  # noqa: E402
+
+from modules.hip import ops  # noqa: E402
+from modules.hip.lib import ACT_RELU, DCS_PAD_REFLECT, DCS_PAD_ZERO  # noqa: E402
+from modules.hip.ops import ConvGeom, Src  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+LAYERS = [
+    # name, geom, input H, pro
+    ("stem", ConvGeom(3, 64, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT), 512, False),
+    ("down1", ConvGeom(64, 128, 3, 2, (1, 1, 1, 1)), 512, True),
+    ("down2", ConvGeom(128, 256, 3, 2, (1, 1, 1, 1)), 256, True),
+    ("res", ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT), 128, True),
+    ("up1", ConvGeom(256, 128, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 128, False),
+    ("up2", ConvGeom(128, 64, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 256, True),
+    ("head", ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT), 512, True),
+    ("d1", ConvGeom(64, 128, 4, 2, (1, 1, 1, 1)), 256, True),
+    ("d2", ConvGeom(128, 256, 4, 2, (1, 1, 1, 1)), 128, True),
+    ("d3", ConvGeom(256, 512, 4, 2, (1, 1, 1, 1)), 64, True),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    N = a.batch
+    print(f"{'layer':8s} {'pass':6s} {'ms':>9s} {'TFLOP/s':>9s}")
+    for name, g, H, pro in LAYERS:
+        if a.only and name not in a.only.split(","):
+            continue
+        x = torch.randn(N, H, H, g.cin, device=dev)
+        w = torch.randn(g.cout, g.cin, g.k, g.k, device=dev) * 0.02
+        st = ops.in_stats(x) if pro else None
+        p = (st.scale, st.shift, ACT_RELU) if pro else None
+        Ho, Wo = g.out_hw(H, H)
+        flop = 2.0 * N * Ho * Wo * g.cout * g.cin * g.k * g.k
+        wp = g.pack_fwd(w)
+        t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p), a.reps)
+        print(f"{name:8s} {'fwd':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
+        dy = torch.randn(N, Ho, Wo, g.cout, device=dev)
+        wd = g.pack_dgrad(w)
+        t = timeit(lambda: g.dgrad(dy, wd, H, H), a.reps)
+        print(f"{name:8s} {'dgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
+        t = timeit(lambda: g.wgrad(dy, Src.nhwc(x), pro=p), a.reps)
+        print(f"{name:8s} {'wgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,13 @@
+# PMC counters for the residual conv (kbench --only res), separate passes.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/gpurun_out
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES" \
+           "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp -d $R/gpurun_out/pmc_res_$i -o p --output-format csv \
+    -- python3 $R/scripts/kbench.py --only ${1:-res} --reps 2 > $R/gpurun_out/pmc_res_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+done
+echo pmc done
