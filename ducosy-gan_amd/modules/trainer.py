@@ -285,20 +285,7 @@ def train_cycle_gan(args, target_range):
     ckpt_path = os.path.join(saved_models_dir, args.resume) if args.resume else None
     if ckpt_path and os.path.isfile(ckpt_path):
         print(f"=> Loading checkpoint '{ckpt_path}'")
-        # our own / the reference's checkpoint: it pickles the args Namespace (trainer.py:594)
-        ck = torch.load(ckpt_path, map_location=device, weights_only=False)
-        for key, m in zip(("G_A2B", "G_B2A", "D_A", "D_B"), system.models):
-            sd = ck[f"{key}_state_dict"]
-            if all(k.startswith("module.") for k in sd):
-                sd = {k[len("module."):]: v for k, v in sd.items()}
-            m.load_state_dict(sd)
-        for key, o in zip(("G", "D_A", "D_B"), system.optimizers):
-            o.load_state_dict(ck[f"optimizer_{key}_state_dict"])
-        for key, s in zip(("G", "D_A", "D_B"), schedulers):
-            s.load_state_dict(ck[f"scheduler_{key}_state_dict"])
-        start_epoch = ck["epoch"] + 1
-        best_val_loss = ck.get("best_val_loss", float("inf"))
-        best_epoch = ck.get("best_epoch", -1)
+        start_epoch, best_val_loss, best_epoch = _load_checkpoint(ckpt_path, system, schedulers, device)
     elif ckpt_path:
         print(f"=> No checkpoint found at '{ckpt_path}'")
 
@@ -342,6 +329,27 @@ def train_cycle_gan(args, target_range):
         if val_loss < best_val_loss:
             best_val_loss, best_epoch = val_loss, epoch + 1
     return system
+
+
+def _load_checkpoint(path, system, schedulers, device):
+    """Resume from checkpoint.pth.tar (trainer.py:374-405 layout).  The file pickles the args
+    Namespace (trainer.py:594); it is read with the weights-only unpickler with
+    argparse.Namespace allow-listed, so loading never executes code from the file.  Accepts
+    the reference's DataParallel ``module.``-prefixed state_dicts.  Returns
+    (start_epoch, best_val_loss, best_epoch)."""
+    import argparse
+    with torch.serialization.safe_globals([argparse.Namespace]):
+        ck = torch.load(path, map_location=device, weights_only=True)
+    for key, m in zip(("G_A2B", "G_B2A", "D_A", "D_B"), system.models):
+        sd = ck[f"{key}_state_dict"]
+        if all(k.startswith("module.") for k in sd):
+            sd = {k[len("module."):]: v for k, v in sd.items()}
+        m.load_state_dict(sd)
+    for key, o in zip(("G", "D_A", "D_B"), system.optimizers):
+        o.load_state_dict(ck[f"optimizer_{key}_state_dict"])
+    for key, s in zip(("G", "D_A", "D_B"), schedulers):
+        s.load_state_dict(ck[f"scheduler_{key}_state_dict"])
+    return ck["epoch"] + 1, ck.get("best_val_loss", float("inf")), ck.get("best_epoch", -1)
 
 
 def _save_epoch(system, schedulers, args, saved_models_dir, epoch, val_loss, best_val_loss, best_epoch):
