@@ -4,6 +4,7 @@ Every test here is @pytest.mark.gpu and calls the kernels through the C-ABI (cty
 Tolerances: fp32 everywhere; max abs error / max |ref| <= 1e-4 for single ops (1e-3 rel for
 chained backward passes), following BASELINE.json's 1e-3 rel bar.
 """
+import os
 import numpy as np
 import pytest
 import torch
@@ -217,3 +218,22 @@ def test_adam_matches_torch(ops):
         opt.step()
         ops.adam_step(pd, g.to(DEV), md, vd, 2e-4, 0.5, 0.999, 1e-8, step)
     assert rel(pd, opt_p.detach()) < 1e-6
+
+
+def test_integration_md_ctypes_example(ops):
+    """The stand-alone ctypes snippet in INTEGRATION.md runs as written (from the repo root) and
+    matches torch's reflect-padded conv on the CPU."""
+    import re
+    import torch.nn.functional as F
+    from conftest import ROOT
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    code = re.search(r"```python\n(.*?)```", text, re.S).group(1)
+    code = code.replace("N, H, W, C = 8, 128, 128, 256", "N, H, W, C = 2, 16, 16, 256")
+    code = code.replace('"ducosy-gan_amd/lib/libducosy_hip.so"', repr(os.path.join(ROOT, "ducosy-gan_amd", "lib",
+                                                                                 "libducosy_hip.so")))
+    env = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), env)
+    torch.cuda.synchronize()
+    x, w, y = env["x"].cpu(), env["w"].cpu(), env["y"].cpu()
+    ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect"), w).permute(0, 2, 3, 1)
+    assert float((y - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
