@@ -592,11 +592,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
             }
         }
     };
+    // LDS column swizzle phys(c) = c ^ (((c >> 5) & 3) << 2): the 8 lanes of a ds_write_b128
+    // group store columns 16t + 4i (t = 0..7), which would hit only two 4-bank slots; XOR-ing
+    // bits 2-3 with (c >> 5) spreads them over all 8 slots.  A fragment read (32 consecutive
+    // columns of one 32-aligned group) sees a fixed permutation, so it stays conflict-free.
+    const int wsw = ((tid & 7) >> 1) & 3;  // (c >> 5) & 3 for this thread's store columns
     auto store_tiles = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * i]) = ra[i];
+        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * (i ^ wsw)]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * i]) = rb[i];
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * (i ^ wsw)]) = rb[i];
     };
 
     constexpr int KT2 = 4;  // k-tiles per inner accumulation chain (two-level summation)
@@ -615,6 +620,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     }
     __syncthreads();
     const int l32 = lane & 31, lh = lane >> 5;
+    // swizzled fragment columns (see store_tiles): group g = c >> 5 permutes l32 by XOR
+    int acol[IM], bcol[JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i) {
+        const int c = wm * WM + i * 32;
+        acol[i] = c + (l32 ^ (((c >> 5) & 3) << 2));
+    }
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int c = wn * WN + j * 32;
+        bcol[j] = c + (l32 ^ (((c >> 5) & 3) << 2));
+    }
     for (long long kt = kt_beg; kt < kt_end; ++kt) {
         const int cur = (int)((kt - kt_beg) & 1);
         // fragments of all 16 k-steps (lane half h takes k = 2s + h)
@@ -623,14 +640,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         for (int i = 0; i < IM; ++i)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float* a = &As[cur][8 * q + lh][wm * WM + i * 32 + l32];
+                const float* a = &As[cur][8 * q + lh][acol[i]];
                 af[i][q] = make_float4(a[0], a[2 * LDA], a[4 * LDA], a[6 * LDA]);
             }
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float* b = &Bs[cur][8 * q + lh][wn * WN + j * 32 + l32];
+                const float* b = &Bs[cur][8 * q + lh][bcol[j]];
                 bf[j][q] = make_float4(b[0], b[2 * LDB], b[4 * LDB], b[6 * LDB]);
             }
         if constexpr (VEC) {
