@@ -596,12 +596,17 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     // group store columns 16t + 4i (t = 0..7), which would hit only two 4-bank slots; XOR-ing
     // bits 2-3 with (c >> 5) spreads them over all 8 slots.  A fragment read (32 consecutive
     // columns of one 32-aligned group) sees a fixed permutation, so it stays conflict-free.
-    const int wsw = ((tid & 7) >> 1) & 3;  // (c >> 5) & 3 for this thread's store columns
+    auto swz = [](int c) { return c ^ (((c >> 5) & 3) << 2); };
+    int aoff[ACH], boff[BCH];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) aoff[i] = swz(ac0 + 4 * i);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) boff[i] = swz(bc0 + 4 * i);
     auto store_tiles = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][ac0 + 4 * (i ^ wsw)]) = ra[i];
+        for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][kr][aoff[i]]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][bc0 + 4 * (i ^ wsw)]) = rb[i];
+        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][kr][boff[i]]) = rb[i];
     };
 
     constexpr int KT2 = 4;  // k-tiles per inner accumulation chain (two-level summation)
@@ -625,12 +630,12 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
 #pragma unroll
     for (int i = 0; i < IM; ++i) {
         const int c = wm * WM + i * 32;
-        acol[i] = c + (l32 ^ (((c >> 5) & 3) << 2));
+        acol[i] = swz(c + l32);
     }
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
         const int c = wn * WN + j * 32;
-        bcol[j] = c + (l32 ^ (((c >> 5) & 3) << 2));
+        bcol[j] = swz(c + l32);
     }
     for (long long kt = kt_beg; kt < kt_end; ++kt) {
         const int cur = (int)((kt - kt_beg) & 1);

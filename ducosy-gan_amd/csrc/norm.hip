@@ -138,6 +138,34 @@ __global__ void in_apply_kernel(const float* __restrict__ x, const float* __rest
     }
 }
 
+// Vectorised apply for power-of-two C (every Generator/PatchGAN layer): grid.y = sample, so the
+// per-element index math is 32-bit shifts and masks; each thread streams 4 float4.
+template <int ACT>
+__global__ __launch_bounds__(256) void in_apply_pow2_kernel(const float4* __restrict__ x,
+                                                            const float* __restrict__ sc,
+                                                            const float* __restrict__ sh,
+                                                            float4* __restrict__ out, int per_n4, int cmask) {
+    const int n = blockIdx.y;
+    const float* s = sc + (long long)n * (cmask + 1);
+    const float* b = sh + (long long)n * (cmask + 1);
+    const float4* xs = x + (long long)n * per_n4;
+    float4* os = out + (long long)n * per_n4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
+        if (i >= per_n4) return;
+        const int c = (i * 4) & cmask;
+        float4 v = xs[i];
+        const float4 s4 = *reinterpret_cast<const float4*>(s + c);
+        const float4 b4 = *reinterpret_cast<const float4*>(b + c);
+        v.x = act_apply(fmaf(v.x, s4.x, b4.x), ACT);
+        v.y = act_apply(fmaf(v.y, s4.y, b4.y), ACT);
+        v.z = act_apply(fmaf(v.z, s4.z, b4.z), ACT);
+        v.w = act_apply(fmaf(v.w, s4.w, b4.w), ACT);
+        os[i] = v;
+    }
+}
+
 // ---- backward of a = act(IN(y)) -------------------------------------------------------
 struct Sum2 {
     float a, b;
@@ -248,7 +276,21 @@ extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shi
         return fail(DCS_E_INVALID, "in_apply: bad arguments");
     long long total = (long long)N * HW * C;
     hipStream_t s = as_stream(stream);
-    if (C % 4 == 0)
+    const bool pow2 = C >= 4 && (C & (C - 1)) == 0 && ((long long)HW * C) / 4 < (1ll << 30) &&
+                      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                        reinterpret_cast<uintptr_t>(scale) | reinterpret_cast<uintptr_t>(shift)) & 15) == 0;
+    if (pow2 && (act == DCS_ACT_RELU || act == DCS_ACT_LRELU || act == DCS_ACT_AFFINE)) {
+        const int per_n4 = (int)((long long)HW * C / 4);
+        dim3 grid((unsigned)cdiv(per_n4, 1024), (unsigned)N);
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        float4* o4 = reinterpret_cast<float4*>(out);
+        if (act == DCS_ACT_RELU)
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_RELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+        else if (act == DCS_ACT_LRELU)
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_LRELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+        else
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_AFFINE>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+    } else if (C % 4 == 0)
         hipLaunchKernelGGL(in_apply_kernel<true>, dim3((unsigned)cdiv(total / 4, 256)), dim3(256), 0, s, x, scale,
                            shift, out, total, HW, C, act);
     else

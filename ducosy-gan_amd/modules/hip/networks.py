@@ -5,8 +5,10 @@ modules/model.py:90-131 with the gfx950 kernels and keeps exactly what its hand-
 backward needs.  Fusions relative to the reference's op-by-op eager graph:
   * ReflectionPad / ZeroPad / nearest Upsample / channel concat are folded into the conv
     gathers (never materialised);
-  * InstanceNorm(+ReLU/LeakyReLU) of a layer is applied in the NEXT conv's prologue, so a
-    conv output is written once (raw) and read once;
+  * InstanceNorm(+ReLU/LeakyReLU) of a layer is either materialised once (in_apply) for the
+    MFMA convs that consume it in forward AND weight-gradient passes (a per-element prologue
+    inside the gather costs those kernels 20-25 %), or applied in the next conv's prologue
+    where that is cheap (the LDS-staged narrow head / PatchGAN kernels);
   * biases of convs followed by InstanceNorm are not added (IN removes any per-channel
     constant, so outputs are unchanged) and their gradient is exactly zero;
   * the CBAM tail (channel MLP, spatial attention, residual add) is 3 kernels forward and
@@ -61,7 +63,7 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
 
 
 class _Block:
-    __slots__ = ("x", "y1", "s1", "y2", "s2", "cb")
+    __slots__ = ("x", "y1", "s1", "a1", "y2", "s2", "cb")
 
 
 def _res_block_forward(L, W, b, x, use_cbam, keep):
@@ -69,7 +71,8 @@ def _res_block_forward(L, W, b, x, use_cbam, keep):
     res = L["res"]
     y1 = res.forward(Src.nhwc(x), W["pk"][f"r{b}.c1.w"])
     s1 = ops.in_stats(y1)
-    y2 = res.forward(Src.nhwc(y1), W["pk"][f"r{b}.c2.w"], pro=(s1.scale, s1.shift, ACT_RELU))
+    a1 = ops.in_apply(y1, s1, ACT_RELU)
+    y2 = res.forward(Src.nhwc(a1), W["pk"][f"r{b}.c2.w"])
     s2 = ops.in_stats(y2, want_max=use_cbam)
     cb = None
     if use_cbam:
@@ -82,7 +85,7 @@ def _res_block_forward(L, W, b, x, use_cbam, keep):
     blk = None
     if keep:
         blk = _Block()
-        blk.x, blk.y1, blk.s1, blk.y2, blk.s2, blk.cb = x, y1, s1, y2, s2, cb
+        blk.x, blk.y1, blk.s1, blk.a1, blk.y2, blk.s2, blk.cb = x, y1, s1, a1, y2, s2, cb
     return out, blk
 
 
@@ -99,7 +102,7 @@ def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
     else:
         dy2 = ops.in_act_backward(dout, blk.y2, blk.s2, ACT_AFFINE)
     H, Wd = blk.x.shape[1], blk.x.shape[2]
-    grads[f"r{b}.c2.w"] = res.wgrad(dy2, Src.nhwc(blk.y1), pro=(blk.s1.scale, blk.s1.shift, ACT_RELU))
+    grads[f"r{b}.c2.w"] = res.wgrad(dy2, Src.nhwc(blk.a1))
     da1 = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd)
     dy1 = ops.in_act_backward(da1, blk.y1, blk.s1, ACT_RELU)
     del da1
@@ -125,9 +128,11 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     N, H, Wd = xs.N, xs.H, xs.W
     y0 = L["stem"].forward(xs, pk["stem.w"])
     s0 = ops.in_stats(y0)
-    y1 = L["down1"].forward(Src.nhwc(y0), pk["down1.w"], pro=(s0.scale, s0.shift, ACT_RELU))
+    a0 = ops.in_apply(y0, s0, ACT_RELU)
+    y1 = L["down1"].forward(Src.nhwc(a0), pk["down1.w"])
     s1 = ops.in_stats(y1)
-    y2 = L["down2"].forward(Src.nhwc(y1), pk["down2.w"], pro=(s1.scale, s1.shift, ACT_RELU))
+    a1 = ops.in_apply(y1, s1, ACT_RELU)
+    y2 = L["down2"].forward(Src.nhwc(a1), pk["down2.w"])
     s2 = ops.in_stats(y2)
     h = ops.in_apply(y2, s2, ACT_RELU)
     blocks = []
@@ -136,15 +141,18 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
         blocks.append(blk)
     yu1 = L["up1"].forward(Src.nhwc(h), pk["up1.w"])
     su1 = ops.in_stats(yu1)
-    yu2 = L["up2"].forward(Src.nhwc(yu1), pk["up2.w"], pro=(su1.scale, su1.shift, ACT_RELU))
+    au1 = ops.in_apply(yu1, su1, ACT_RELU)
+    yu2 = L["up2"].forward(Src.nhwc(au1), pk["up2.w"])
     su2 = ops.in_stats(yu2)
     out = L["head"].forward(Src.nhwc(yu2), pk["head.w"], bias=W["head.b"],
                             pro=(su2.scale, su2.shift, ACT_RELU), epi_act=ACT_TANH)
     out = out.view(N, 1, H, Wd)
     saved = None
     if keep:
-        saved = dict(L=L, W=W, xs=xs, y0=y0, s0=s0, y1=y1, s1=s1, y2=y2, s2=s2, blocks=blocks, h=h,
-                     yu1=yu1, su1=su1, yu2=yu2, su2=su2, nb=nb, use_cbam=use_cbam)
+        saved = dict(L=L, W=W, xs=xs, y0=y0, s0=s0, a0=a0, y1=y1, s1=s1, a1=a1, y2=y2, s2=s2, blocks=blocks,
+                     h=h, yu1=yu1, su1=su1, au1=au1, yu2=yu2, su2=su2, nb=nb, use_cbam=use_cbam)
+    else:
+        del a0, a1, au1
     return out, saved
 
 
@@ -164,7 +172,7 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int):
     del dpre
     # up2
     dy = ops.in_act_backward(da, S["yu2"], su2, ACT_RELU)
-    grads["up2.w"] = L["up2"].wgrad(dy, Src.nhwc(S["yu1"]), pro=(su1.scale, su1.shift, ACT_RELU))
+    grads["up2.w"] = L["up2"].wgrad(dy, Src.nhwc(S["au1"]))
     da = L["up2"].dgrad(dy, L["up2"].pack_dgrad(W["up2.w"]), H // 2, Wd // 2)
     # up1
     dy = ops.in_act_backward(da, S["yu1"], su1, ACT_RELU)
@@ -178,10 +186,10 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int):
     # x0 = relu(IN(y2))
     s2, s1, s0 = S["s2"], S["s1"], S["s0"]
     dy = ops.in_act_backward(dh, S["y2"], s2, ACT_RELU)
-    grads["down2.w"] = L["down2"].wgrad(dy, Src.nhwc(S["y1"]), pro=(s1.scale, s1.shift, ACT_RELU))
+    grads["down2.w"] = L["down2"].wgrad(dy, Src.nhwc(S["a1"]))
     da = L["down2"].dgrad(dy, L["down2"].pack_dgrad(W["down2.w"]), H // 2, Wd // 2)
     dy = ops.in_act_backward(da, S["y1"], s1, ACT_RELU)
-    grads["down1.w"] = L["down1"].wgrad(dy, Src.nhwc(S["y0"]), pro=(s0.scale, s0.shift, ACT_RELU))
+    grads["down1.w"] = L["down1"].wgrad(dy, Src.nhwc(S["a0"]))
     da = L["down1"].dgrad(dy, L["down1"].pack_dgrad(W["down1.w"]), H, Wd)
     dy = ops.in_act_backward(da, S["y0"], s0, ACT_RELU)
     del da

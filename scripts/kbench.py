@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--nopro", action="store_true", help="drop the IN+ReLU gather prologue (cost probe)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N = a.batch
@@ -64,6 +65,7 @@ def main():
             continue
         x = torch.randn(N, H, H, g.cin, device=dev)
         w = torch.randn(g.cout, g.cin, g.k, g.k, device=dev) * 0.02
+        pro = pro and not a.nopro
         st = ops.in_stats(x) if pro else None
         p = (st.scale, st.shift, ACT_RELU) if pro else None
         Ho, Wo = g.out_hw(H, H)
