@@ -75,6 +75,32 @@ __device__ __forceinline__ bool map_coord(int v, int Hv, int up, int mode, int& 
     return true;
 }
 
+// Branch-free variant for the vectorised gathers: returns validity, writes the source coordinate.
+__device__ __forceinline__ bool map_coord_sel(int v, int Hv, int up, int mode, int& s) {
+    const bool inside = (unsigned)v < (unsigned)Hv;
+    const int r = v < 0 ? -v : 2 * (Hv - 1) - v;
+    const int c = inside ? v : r;
+    s = up == 2 ? (c >> 1) : c;
+    return inside || mode == DCS_PAD_REFLECT;
+}
+
+// Source reads of the vectorised gathers go through a raw buffer descriptor: a 32-bit byte
+// offset per lane, and the hardware range check returns zeros for offset OOB_OFF, so zero
+// padding and rows past the end need no branches (the host keeps every source < 2 GiB).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int OOB_OFF = 0x7fffffff - 64;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffff00, 0x00020000);
+}
+
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+    float4 f;
+    __builtin_memcpy(&f, &v, 16);
+    return f;
+}
+
 struct RowInfo {
     int n, by, bx;        // image, base virtual source coords
     long long out_off;    // element offset of the output pixel (channel 0), -1 if invalid
@@ -282,11 +308,26 @@ __device__ __forceinline__ void mfma_ktile(const float4 (&af)[IM][4], const floa
         for (int j = 0; j < JN; ++j) acc[i][j] += t[i][j];
 }
 
+// TAG 1: the residual-block geometry (3x3, stride 1, no upsampling, regular rows, 256 source
+// channels) is compiled in, so the per-k-tile tap decode and coordinate mapping fold to
+// constants; the padding mode (reflect forward, zero for the dgrad) stays a runtime value.
+template <int TAG>
+__device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
+#ifndef DCS_NO_SPECIALISE
+    if constexpr (TAG == 1) {
+        d.KH = 3; d.KW = 3; d.stride = 1; d.up = 1; d.parity = 0;
+        d.Cs = 256; d.csplit = 256; d.s_c = 1;
+    }
+#endif
+    return d;
+}
+
 template <int BM, int BN, bool VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
-    const dcs_conv_desc d, const float* __restrict__ src, const float* __restrict__ src2,
+    const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy) {
+    const dcs_conv_desc d = specialise<TAG>(din);
     static_assert(BM == 128, "A loader assumes 128 rows (2 threads per row)");
     constexpr int WM = BM / 2, WN = BN / 2;        // per-wave tile
     constexpr int IM = WM / 32, JN = WN / 32;      // 32x32 blocks per wave
@@ -342,6 +383,8 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 
     auto load_a = [&](int kt) {
         if (VEC) {
+            // (a buffer-descriptor variant of this gather, as in the wgrad pass, measured 3-7 %
+            //  slower here: invalid taps would issue loads that the branch now skips)
             ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid && aj < g.ntaps) {
                 int ady, adx, bt;
@@ -476,11 +519,12 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 // to LDS (8 threads per pixel row, one pixel decode per thread per k-tile).  A lane's MFMA
 // operands are single floats down a column ([2s+h][m]); all 16 k-steps of a tile are read
 // into registers before the tile's MFMAs so LDS latency is paid once per tile.
-template <int BM, int BN, bool VEC>
+template <int BM, int BN, bool VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
-    const dcs_conv_desc d, const float* __restrict__ dy, const float* __restrict__ src,
+    const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
     const float* __restrict__ src2, const float* __restrict__ psc, const float* __restrict__ psh,
     float* __restrict__ ws, int kt_per_split, int gn, int gm) {
+    const dcs_conv_desc d = specialise<TAG>(din);
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int IM = WM / 32, JN = WN / 32;
     constexpr int LDA = BM + 4, LDB = BN + 4;
@@ -524,6 +568,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         tap_decode(d, g, j, bady, badx, bt);
     }
     const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    const __amdgpu_buffer_rsrc_t rsrc = src_rsrc(src);
     // incremental pixel state of the NEXT k-tile row this thread loads (p = kt*BK + kr)
     int pn = 0, pqy = 0, pqx = 0;
     {
@@ -555,20 +600,21 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
 #pragma unroll
         for (int i = 0; i < BCH; ++i) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (VEC) {
-            if (p < P && bcol_ok) {
-                const int vy = pqy * d.stride - d.pt + bady, vx = pqx * d.stride - d.pl + badx;
-                int sy, sx;
-                if (map_coord(vy, Hv, d.up, d.pad_mode, sy) && map_coord(vx, Wv, d.up, d.pad_mode, sx)) {
-                    const float* sp = src + pn * d.s_n + sy * d.s_h + sx * d.s_w + bchan;
-                    const long long o = (long long)pn * d.Cs + bchan;
+            // the thread's BN/8 columns share one tap (Cs % 16 == 0); bcol_ok covers all of them
+            const int vy = pqy * d.stride - d.pt + bady, vx = pqx * d.stride - d.pl + badx;
+            int sy, sx;
+            const bool yok = map_coord_sel(vy, Hv, d.up, d.pad_mode, sy);
+            const bool xok = map_coord_sel(vx, Wv, d.up, d.pad_mode, sx);
+            const bool ok = p < P && bcol_ok && yok && xok;
+            const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
 #pragma unroll
-                    for (int i = 0; i < BCH; ++i) {
-                        if (nb0 + 4 * i < Ktot) {
-                            rb[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
-                            if (d.pro_act != DCS_ACT_NONE)
-                                rb[i] = affine_act4(rb[i], psc + o + 4 * i, psh + o + 4 * i, d.pro_act);
-                        }
-                    }
+            for (int i = 0; i < BCH; ++i) rb[i] = buf_load4(rsrc, off + 16 * i);
+            if (d.pro_act != DCS_ACT_NONE) {
+                const long long o = (long long)pn * d.Cs + bchan;
+#pragma unroll
+                for (int i = 0; i < BCH; ++i) {
+                    const float4 v = affine_act4(rb[i], psc + o + 4 * i, psh + o + 4 * i, d.pro_act);
+                    rb[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
             advance_pix();
@@ -905,9 +951,14 @@ static int validate(const dcs_conv_desc* d, bool rows) {
 }
 
 static bool vec_ok(const dcs_conv_desc* d, const float* src) {
+    // the vectorised gathers address the source through a buffer descriptor with 32-bit byte
+    // offsets: every element they can touch must lie below 2 GiB (minus the OOB sentinel)
+    const long long extent = (long long)(d->N - 1) * d->s_n + (long long)(d->Hs - 1) * d->s_h +
+                             (long long)(d->Ws - 1) * d->s_w + d->Cs;
     return (d->Cs % 16 == 0) && d->s_c == 1 && d->csplit == d->Cs &&
            (d->s_w % 4 == 0) && (d->s_h % 4 == 0) && (d->s_n % 4 == 0) &&
-           ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+           ((reinterpret_cast<uintptr_t>(src) & 15) == 0) && extent * 4 < (long long)OOB_OFF - 64 &&
+           d->s_n >= 0 && d->s_h >= 0 && d->s_w >= 0;
 }
 
 // LDS-tiled single-output-channel kernels (conv_narrow.hip)
@@ -1017,12 +1068,14 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     const bool vec = vec_ok(dp, x);
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
+    const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1;
     if (p.BM == 128) {
-        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     }
     e = check_launch("conv_wgrad");
     if (e) return e;
