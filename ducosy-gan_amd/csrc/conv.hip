@@ -739,7 +739,9 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     }
 }
 
-// dw[co][ci][ty][tx] = sum_s ws[s][co][(ty*KW+tx)*Cs + ci]
+// dw[co][ci][ty][tx] = sum_s ws[s][co][(ty*KW+tx)*Cs + ci].  Threads walk the slabs in
+// their own (co, tap, ci) order so the nsplit reads per output are coalesced; each output is
+// written once (scattered into OIHW).  Fixed split order: deterministic.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int Co, int Cs, int KH,
                                     int KW, float* __restrict__ dw) {
     long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -747,15 +749,12 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, in
     const long long Ktot = (long long)taps * Cs;
     const long long total = (long long)Co * Ktot;
     if (idx >= total) return;
-    // idx enumerates the OIHW output
-    int tap = (int)(idx % taps);
-    long long t2 = idx / taps;
-    int ci = (int)(t2 % Cs);
-    int co = (int)(t2 / Cs);
-    long long src = (long long)co * Ktot + (long long)tap * Cs + ci;
+    const int co = (int)(idx / Ktot);
+    const int k = (int)(idx - (long long)co * Ktot);
+    const int tap = k / Cs, ci = k - tap * Cs;
     float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += ws[(long long)k * total + src];
-    dw[idx] = s;
+    for (int q = 0; q < nsplit; ++q) s += ws[(long long)q * total + idx];
+    dw[((long long)co * Cs + ci) * taps + tap] = s;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -53,11 +53,12 @@ __device__ __forceinline__ void block_partials(double (&v)[K], double* part) {
     }
 }
 
-// sum of partials of quantity q over nb blocks, in block order (called by one thread)
+// sum of partials of quantity q over nb blocks, by one full wave: lane l sums blocks l, l+64, ...
+// in order, then a fixed butterfly combines the lanes (deterministic; every lane gets the total)
 __device__ __forceinline__ double sum_parts(const double* part, int nb, int q) {
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += part[(long long)b * 8 + q];
-    return s;
+    for (int b = threadIdx.x & 63; b < nb; b += 64) s += part[(long long)b * 8 + q];
+    return wave_sum_d(s);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -83,7 +84,8 @@ __global__ __launch_bounds__(RB) void pointwise_kernel(const float* __restrict__
 }
 
 __global__ void finalize_mean_kernel(const double* part, int nb, long long n, float* out) {
-    if (threadIdx.x == 0) out[0] = (float)(sum_parts(part, nb, 0) / (double)n);
+    const double v = sum_parts(part, nb, 0);
+    if (threadIdx.x == 0) out[0] = (float)(v / (double)n);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -129,10 +131,8 @@ __global__ __launch_bounds__(RB) void gradient_loss_kernel(const float* __restri
 }
 
 __global__ void gradient_loss_final(const double* part, int nb, int N, int H, int W, float* out) {
-    if (threadIdx.x == 0) {
-        double sx = sum_parts(part, nb, 0), sy = sum_parts(part, nb, 1);
-        out[0] = (float)(sx / ((double)N * H * (W - 1)) + sy / ((double)N * (H - 1) * W));
-    }
+    double sx = sum_parts(part, nb, 0), sy = sum_parts(part, nb, 1);
+    if (threadIdx.x == 0) out[0] = (float)(sx / ((double)N * H * (W - 1)) + sy / ((double)N * (H - 1) * W));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -223,10 +223,10 @@ __global__ __launch_bounds__(RB) void cr_loss_kernel(const float* __restrict__ p
 
 __global__ void cr_loss_final(const double* part, int nb, long long n, long long nq, float weight, float* sc,
                               float* out) {
-    if (threadIdx.x != 0) return;
     double reg = sum_parts(part, nb, 0);
     double s1 = sum_parts(part, nb, 1), s2 = sum_parts(part, nb, 2);
     double t1 = sum_parts(part, nb, 3), t2 = sum_parts(part, nb, 4);
+    if (threadIdx.x != 0) return;
     double mp = s1 / n, mt = t1 / n;
     double sp = sqrt(fmax((s2 - n * mp * mp) / (n - 1), 0.0));
     double st = sqrt(fmax((t2 - n * mt * mt) / (n - 1), 0.0));
@@ -351,16 +351,17 @@ __global__ __launch_bounds__(RB) void topk_sum_kernel(const float* __restrict__ 
 __global__ void edge_final_kernel(const double* part_stats, int nb_stats, const double* part_tp, int nb_tp,
                                   const double* part_tt, int nb_tt, const unsigned* st_p, const unsigned* st_t,
                                   long long n, long long k, float* sc, float* out) {
-    if (threadIdx.x != 0) return;
     double s1 = sum_parts(part_stats, nb_stats, 0), s2 = sum_parts(part_stats, nb_stats, 1);
     double t1 = sum_parts(part_stats, nb_stats, 2), t2 = sum_parts(part_stats, nb_stats, 3);
+    const double ptp = sum_parts(part_tp, nb_tp, 0), ptt = sum_parts(part_tt, nb_tt, 0);
+    const double eqp = sum_parts(part_tp, nb_tp, 1);
+    if (threadIdx.x != 0) return;
     double mp = s1 / n, mt = t1 / n;
     double sp = sqrt(fmax((s2 - n * mp * mp) / (n - 1), 0.0));
     double st = sqrt(fmax((t2 - n * mt * mt) / (n - 1), 0.0));
     double taup = (double)__uint_as_float(st_p[0]), taut = (double)__uint_as_float(st_t[0]);
-    double tkp = (sum_parts(part_tp, nb_tp, 0) + (double)st_p[1] * taup) / (double)k;
-    double tkt = (sum_parts(part_tt, nb_tt, 0) + (double)st_t[1] * taut) / (double)k;
-    double eqp = sum_parts(part_tp, nb_tp, 1);
+    double tkp = (ptp + (double)st_p[1] * taup) / (double)k;
+    double tkt = (ptt + (double)st_t[1] * taut) / (double)k;
     out[0] = (float)(fabs(mp - mt) + fabs(sp - st) + fabs(tkp - tkt));
     double sg1 = (mp > mt) ? 1.0 : ((mp < mt) ? -1.0 : 0.0);
     double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
@@ -498,7 +499,8 @@ __global__ __launch_bounds__(RB) void ssim_h_kernel(const float* __restrict__ V,
 }
 
 __global__ void ssim_final(const double* part, int nb, long long tot, float* out) {
-    if (threadIdx.x == 0) out[0] = (float)(sum_parts(part, nb, 0) / (double)tot);
+    const double v = sum_parts(part, nb, 0);
+    if (threadIdx.x == 0) out[0] = (float)(v / (double)tot);
 }
 
 // adjoint horizontal: T[3][N][Hv][W] = sum_b g[b] D[.][i][v-b]

@@ -98,12 +98,14 @@ __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* _
     }
 }
 
-__global__ void channel_sum_final_kernel(const float* __restrict__ part, int C, int nchunk, float* __restrict__ out) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// one wave per channel: lane l sums chunks l, l+64, ... in order, then a fixed butterfly
+__global__ __launch_bounds__(64) void channel_sum_final_kernel(const float* __restrict__ part, int C, int nchunk,
+                                                               float* __restrict__ out) {
+    const int c = blockIdx.x;
     double s = 0.0;
-    for (int k = 0; k < nchunk; ++k) s += part[(long long)k * C + c];
-    out[c] = (float)s;
+    for (int k = threadIdx.x; k < nchunk; k += 64) s += part[(long long)k * C + c];
+    s = wave_sum_d(s);
+    if (threadIdx.x == 0) out[c] = (float)s;
 }
 
 static inline int csum_chunks(long long P) {
@@ -150,7 +152,7 @@ extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, voi
                        (long long)P, C, nch, reinterpret_cast<float*>(ws));
     int e = check_launch("channel_sum_partial");
     if (e) return e;
-    hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
                        reinterpret_cast<const float*>(ws), C, nch, out);
     return check_launch("channel_sum_final");
 }

@@ -20,6 +20,11 @@ static inline int stats_chunks(int N, int HW) {
     return c;
 }
 
+// float4 path: C % 4 == 0, C/4 divides 256, 16-byte aligned pointer
+static inline bool v4_ok(int C, const void* p) {
+    return C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+}
+
 // grid (N, nchunk); 256 threads.  Thread layout: if C <= 256 and 256 % C == 0 → C channels x
 // (256/C) pixel lanes; otherwise each thread owns channels tid, tid+256, ... (one pixel lane).
 __global__ __launch_bounds__(256) void in_stats_partial_kernel(const float* __restrict__ x, int HW, int C,
@@ -85,27 +90,124 @@ __global__ __launch_bounds__(256) void in_stats_partial_kernel(const float* __re
     }
 }
 
-__global__ void in_stats_finalize_kernel(const Part* __restrict__ parts, int N, int C, int nchunk, float eps,
-                                         float* __restrict__ scale, float* __restrict__ shift,
-                                         float* __restrict__ xmax, int* __restrict__ xam) {
-    int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= N * C) return;
-    int n = idx / C, c = idx - n * C;
+
+// Vectorised partial statistics for C % 4 == 0 with 256 % (C/4) == 0 (every layer here): a
+// thread owns 4 consecutive channels (float4 loads) and one of 256/(C/4) pixel lanes; the lanes
+// are merged in a fixed order (deterministic).  Same Part layout as in_stats_partial_kernel.
+__global__ __launch_bounds__(256) void in_stats_partial_v4_kernel(const float4* __restrict__ x, int HW, int C,
+                                                                   int nchunk, Part* __restrict__ parts) {
+    const int n = blockIdx.x, chunk = blockIdx.y;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const int cq = C >> 2, lanes = 256 / cq;
+    const int tid = threadIdx.x, c4 = tid % cq, plane = tid / cq;
+    __shared__ float s_mean[4][256], s_m2[4][256], s_mx[4][256];
+    __shared__ int s_am[4][256];
+    __shared__ float s_cnt[256];
+    const float4* xb = x + (long long)n * HW * cq + c4;
+    float K[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int am[4] = {0, 0, 0, 0};
+    float cnt = 0.f;
+    int p = p0 + plane;
+    if (p < p1) {
+        const float4 v = xb[(long long)p * cq];
+        K[0] = v.x; K[1] = v.y; K[2] = v.z; K[3] = v.w;
+    }
+    for (; p < p1; p += lanes) {
+        const float4 v4 = xb[(long long)p * cq];
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float dv = v[e] - K[e];
+            s1[e] += dv;
+            s2[e] = fmaf(dv, dv, s2[e]);
+            if (v[e] > mx[e]) { mx[e] = v[e]; am[e] = p; }
+        }
+        cnt += 1.f;
+    }
+    s_cnt[tid] = cnt;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float mean = 0.f, m2 = 0.f;
+        if (cnt > 0.f) {
+            const float d1 = s1[e] / cnt;
+            mean = K[e] + d1;
+            m2 = fmaxf(s2[e] - s1[e] * d1, 0.f);
+        }
+        s_mean[e][tid] = mean; s_m2[e][tid] = m2; s_mx[e][tid] = mx[e]; s_am[e][tid] = am[e];
+    }
+    __syncthreads();
+    if (plane != 0) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float c0 = s_cnt[tid], mean = s_mean[e][tid], m2 = s_m2[e][tid], m = s_mx[e][tid];
+        int a = s_am[e][tid];
+        for (int l = 1; l < lanes; ++l) {
+            const int o = l * cq + c4;
+            const float nb = s_cnt[o];
+            if (nb <= 0.f) continue;
+            const float tot = c0 + nb, dl = s_mean[e][o] - mean;
+            mean = mean + dl * (nb / tot);
+            m2 = m2 + s_m2[e][o] + dl * dl * (c0 * nb / tot);
+            c0 = tot;
+            if (s_mx[e][o] > m || (s_mx[e][o] == m && s_am[e][o] < a)) { m = s_mx[e][o]; a = s_am[e][o]; }
+        }
+        Part pt;
+        pt.cnt = c0; pt.mean = mean; pt.m2 = m2; pt.mx = m; pt.amax = a;
+        parts[((long long)n * nchunk + chunk) * C + 4 * c4 + e] = pt;
+    }
+}
+
+// finalize with 8 sub-lanes per (n,c): sub-lane s merges chunks s, s+8, ... in order, then a
+// fixed xor-butterfly merges the sub-lanes (deterministic, 8x shorter dependent chain)
+__device__ __forceinline__ void chan_merge(double& cnt, double& mean, double& m2, float& mx, int& am,
+                                           double nb, double mb, double m2b, float mxb, int amb) {
+    if (nb > 0.0) {
+        const double tot = cnt + nb, dl = mb - mean;
+        mean += dl * nb / tot;
+        m2 += m2b + dl * dl * cnt * nb / tot;
+        cnt = tot;
+    }
+    if (mxb > mx || (mxb == mx && amb < am)) { mx = mxb; am = amb; }
+}
+
+__global__ __launch_bounds__(256) void in_stats_finalize8_kernel(const Part* __restrict__ parts, int N, int C,
+                                                                  int nchunk, float eps, float* __restrict__ scale,
+                                                                  float* __restrict__ shift, float* __restrict__ xmax,
+                                                                  int* __restrict__ xam) {
+    const int idx = blockIdx.x * 32 + (threadIdx.x >> 3), sub = threadIdx.x & 7;
+    const bool live = idx < N * C;
+    const int n = live ? idx / C : 0, c = live ? idx - n * C : 0;
     double cnt = 0.0, mean = 0.0, m2 = 0.0;
     float mx = -INFINITY;
-    int am = 0;
-    for (int k = 0; k < nchunk; ++k) {
-        Part p = parts[((long long)n * nchunk + k) * C + c];
-        if (p.cnt <= 0.f) continue;
-        double nb = p.cnt, tot = cnt + nb;
-        double dl = (double)p.mean - mean;
-        mean += dl * nb / tot;
-        m2 += (double)p.m2 + dl * dl * cnt * nb / tot;
-        cnt = tot;
-        if (p.mx > mx) { mx = p.mx; am = p.amax; }
+    int am = 0x7fffffff;
+    if (live) {
+        for (int k = sub; k < nchunk; k += 8) {
+            const Part p = parts[((long long)n * nchunk + k) * C + c];
+            chan_merge(cnt, mean, m2, mx, am, p.cnt, p.mean, p.m2, p.mx, p.amax);
+        }
     }
-    double var = m2 / cnt;  // biased (InstanceNorm)
-    float rstd = (float)(1.0 / sqrt(var + (double)eps));
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        const double nb = __shfl_xor(cnt, o, 64), mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+        const float mxb = __shfl_xor(mx, o, 64);
+        const int amb = __shfl_xor(am, o, 64);
+        // merge in a lane-order-independent way: the lower sub-lane is always the left operand
+        if ((sub & o) == 0) {
+            chan_merge(cnt, mean, m2, mx, am, nb, mb, m2b, mxb, amb);
+        } else {
+            double c2 = nb, me2 = mb, mm2 = m2b;
+            float mx2 = mxb;
+            int am2 = amb;
+            chan_merge(c2, me2, mm2, mx2, am2, cnt, mean, m2, mx, am);
+            cnt = c2; mean = me2; m2 = mm2; mx = mx2; am = am2;
+        }
+    }
+    if (!live || sub != 0) return;
+    const double var = m2 / cnt;  // biased (InstanceNorm)
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
     scale[idx] = rstd;
     shift[idx] = (float)(-mean) * rstd;
     if (xmax) xmax[idx] = mx;
@@ -212,19 +314,96 @@ __global__ __launch_bounds__(256) void in_bwd_partial_kernel(const float* __rest
     }
 }
 
-__global__ void in_bwd_finalize_kernel(Sum2* __restrict__ parts, int N, int C, int nchunk, int HW,
-                                       Sum2* __restrict__ coef) {
-    int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= N * C) return;
-    int n = idx / C, c = idx - n * C;
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < nchunk; ++k) {
-        Sum2 p = parts[((long long)n * nchunk + k) * C + c];
-        a += p.a;
-        b += p.b;
+template <int ACT>
+__global__ __launch_bounds__(256) void in_bwd_partial_v4_kernel(const float4* __restrict__ da, const float4* __restrict__ y,
+                                                                 const float* __restrict__ sc, const float* __restrict__ sh,
+                                                                 int HW, int C, int nchunk, Sum2* __restrict__ parts) {
+    const int n = blockIdx.x, chunk = blockIdx.y;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const int cq = C >> 2, lanes = 256 / cq;
+    const int tid = threadIdx.x, c4 = tid % cq, plane = tid / cq;
+    __shared__ float s_a[4][256], s_b[4][256];
+    const float4 s4 = *reinterpret_cast<const float4*>(sc + n * C + 4 * c4);
+    const float4 b4 = *reinterpret_cast<const float4*>(sh + n * C + 4 * c4);
+    const float s[4] = {s4.x, s4.y, s4.z, s4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
+    const long long base = (long long)n * HW * cq + c4;
+    float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = p0 + plane; p < p1; p += lanes) {
+        const float4 g4 = da[base + (long long)p * cq], y4 = y[base + (long long)p * cq];
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float xh = fmaf(yv[e], s[e], b[e]);
+            const float g = gv[e] * act_grad(xh, ACT);
+            sa[e] += g;
+            sb[e] = fmaf(g, xh, sb[e]);
+        }
     }
-    coef[idx] = Sum2{(float)(a / HW), (float)(b / HW)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { s_a[e][tid] = sa[e]; s_b[e][tid] = sb[e]; }
+    __syncthreads();
+    if (plane != 0) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float a = s_a[e][tid], bb = s_b[e][tid];
+        for (int l = 1; l < lanes; ++l) { a += s_a[e][l * cq + c4]; bb += s_b[e][l * cq + c4]; }
+        parts[((long long)n * nchunk + chunk) * C + 4 * c4 + e] = Sum2{a, bb};
+    }
 }
+
+__global__ __launch_bounds__(256) void in_bwd_finalize8_kernel(const Sum2* __restrict__ parts, int N, int C, int nchunk,
+                                                                int HW, Sum2* __restrict__ coef) {
+    const int idx = blockIdx.x * 32 + (threadIdx.x >> 3), sub = threadIdx.x & 7;
+    const bool live = idx < N * C;
+    const int n = live ? idx / C : 0, c = live ? idx - n * C : 0;
+    double a = 0.0, b = 0.0;
+    if (live)
+        for (int k = sub; k < nchunk; k += 8) {
+            const Sum2 p = parts[((long long)n * nchunk + k) * C + c];
+            a += p.a;
+            b += p.b;
+        }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        a += __shfl_xor(a, o, 64);  // same operand pair on both lanes of a pair: order-free
+        b += __shfl_xor(b, o, 64);
+    }
+    if (live && sub == 0) coef[idx] = Sum2{(float)(a / HW), (float)(b / HW)};
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256) void in_bwd_apply_pow2_kernel(const float4* __restrict__ da, const float4* __restrict__ y,
+                                                                 const float* __restrict__ sc, const float* __restrict__ sh,
+                                                                 const Sum2* __restrict__ coef, float4* __restrict__ dy,
+                                                                 int per_n4, int cmask) {
+    const int n = blockIdx.y;
+    const int C = cmask + 1;
+    const long long off = (long long)n * per_n4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
+        if (i >= per_n4) return;
+        const int c = (i * 4) & cmask;
+        const float4 g4 = da[off + i], y4 = y[off + i];
+        const float4 s4 = *reinterpret_cast<const float4*>(sc + n * C + c);
+        const float4 b4 = *reinterpret_cast<const float4*>(sh + n * C + c);
+        const Sum2* k = coef + n * C + c;
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
+        const float s[4] = {s4.x, s4.y, s4.z, s4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float xh = fmaf(yv[e], s[e], b[e]);
+            const float g = gv[e] * act_grad(xh, ACT);
+            const Sum2 kk = k[e];
+            o[e] = s[e] * (g - kk.a - xh * kk.b);
+        }
+        dy[off + i] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 
 __global__ void in_bwd_apply_kernel(const float* __restrict__ da, const float* __restrict__ y,
                                     const float* __restrict__ sc, const float* __restrict__ sh,
@@ -262,10 +441,14 @@ extern "C" int dcs_in_stats(const float* x, int N, int HW, int C, float eps, flo
     int nchunk = stats_chunks(N, HW);
     hipStream_t s = as_stream(stream);
     Part* parts = reinterpret_cast<Part*>(ws);
-    hipLaunchKernelGGL(in_stats_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, x, HW, C, nchunk, parts);
+    if (v4_ok(C, x))
+        hipLaunchKernelGGL(in_stats_partial_v4_kernel, dim3(N, nchunk), dim3(256), 0, s,
+                           reinterpret_cast<const float4*>(x), HW, C, nchunk, parts);
+    else
+        hipLaunchKernelGGL(in_stats_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, x, HW, C, nchunk, parts);
     int e = check_launch("in_stats_partial");
     if (e) return e;
-    hipLaunchKernelGGL(in_stats_finalize_kernel, dim3((unsigned)cdiv((long long)N * C, 256)), dim3(256), 0, s, parts,
+    hipLaunchKernelGGL(in_stats_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts,
                        N, C, nchunk, eps, scale, shift, xmax, xargmax);
     return check_launch("in_stats_finalize");
 }
@@ -310,16 +493,43 @@ extern "C" int dcs_in_act_backward(const float* da, const float* y, const float*
     Sum2* parts = reinterpret_cast<Sum2*>(ws);
     Sum2* coef = reinterpret_cast<Sum2*>(reinterpret_cast<char*>(ws) +
                                          align_up((size_t)N * nchunk * C * sizeof(Sum2), 256));
-    hipLaunchKernelGGL(in_bwd_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, da, y, scale, shift, HW, C, act,
-                       nchunk, parts);
+    const bool v4 = v4_ok(C, da) && v4_ok(C, y) && v4_ok(C, dy) && v4_ok(C, scale) && v4_ok(C, shift) &&
+                    (act == DCS_ACT_RELU || act == DCS_ACT_LRELU || act == DCS_ACT_AFFINE);
+    const float4* da4 = reinterpret_cast<const float4*>(da);
+    const float4* y4 = reinterpret_cast<const float4*>(y);
+    if (v4) {
+        dim3 g(N, nchunk);
+        if (act == DCS_ACT_RELU)
+            hipLaunchKernelGGL(in_bwd_partial_v4_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, HW, C, nchunk, parts);
+        else if (act == DCS_ACT_LRELU)
+            hipLaunchKernelGGL(in_bwd_partial_v4_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, HW, C, nchunk, parts);
+        else
+            hipLaunchKernelGGL(in_bwd_partial_v4_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, HW, C, nchunk, parts);
+    } else {
+        hipLaunchKernelGGL(in_bwd_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, da, y, scale, shift, HW, C, act,
+                           nchunk, parts);
+    }
     int e = check_launch("in_bwd_partial");
     if (e) return e;
-    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((unsigned)cdiv((long long)N * C, 256)), dim3(256), 0, s, parts, N,
+    hipLaunchKernelGGL(in_bwd_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts, N,
                        C, nchunk, HW, coef);
     e = check_launch("in_bwd_finalize");
     if (e) return e;
     long long total = (long long)N * HW * C;
-    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
-                       coef, dy, total, HW, C, act);
+    const bool pow2 = v4 && (C & (C - 1)) == 0 && (long long)HW * C / 4 < (1ll << 30);
+    if (pow2) {
+        const int per_n4 = (int)((long long)HW * C / 4);
+        dim3 g((unsigned)cdiv(per_n4, 1024), (unsigned)N);
+        float4* dy4 = reinterpret_cast<float4*>(dy);
+        if (act == DCS_ACT_RELU)
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+        else if (act == DCS_ACT_LRELU)
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+        else
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+    } else {
+        hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
+                           coef, dy, total, HW, C, act);
+    }
     return check_launch("in_bwd_apply");
 }
