@@ -37,6 +37,9 @@ __device__ __host__ inline ClassGeom class_geom(const dcs_conv_desc& d, int z) {
     ClassGeom g;
     if (!d.parity) {
         g.My = d.Ho; g.Mx = d.Wo; g.ntaps = d.KH * d.KW; g.ry = 0; g.rx = 0;
+    } else if (d.parity == 2) {  // sub-pixel phases of nearest-x2 upsample + 3x3 conv
+        g.ry = z >> 1; g.rx = z & 1;
+        g.My = d.Hs; g.Mx = d.Ws; g.ntaps = 4;
     } else {
         g.ry = z >> 1; g.rx = z & 1;
         g.My = (d.Ho - g.ry + 1) >> 1;
@@ -54,6 +57,10 @@ __device__ __forceinline__ void tap_decode(const dcs_conv_desc& d, const ClassGe
     if (!d.parity) {
         int ty = j / d.KW, tx = j - ty * d.KW;
         ady = ty; adx = tx; btap = j;
+    } else if (d.parity == 2) {  // phase (ry, rx), 2x2 taps at source offsets r-1+{0,1}
+        const int jy = j >> 1, jx = j & 1;
+        ady = g.ry - 1 + jy; adx = g.rx - 1 + jx;
+        btap = (2 * g.ry + g.rx) * 4 + j;
     } else {
         int ty0 = (g.ry + d.pt) & 1, tx0 = (g.rx + d.pl) & 1;
         int ntx = (d.KW - tx0 + 1) >> 1;
@@ -192,7 +199,41 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
     else { k = (int)(idx / ncols); col = (int)(idx - (long long)k * ncols); }
     int taps = KH * KW;
     float v = 0.f;
-    if (kind == 0) {  // B[(tap)*Cin + ci][co]
+    if (kind == 3 || kind == 4) {
+        // nearest-x2 upsample + 3x3 conv (zero pad 1) split into sub-pixel phases; each
+        // phase/tap weight is a sum of original taps.  Row sets per (phase r, tap a):
+        //   kind 3 (forward, class z = 2ry+rx, tap j = 2a+b): S(0,0)={0} S(0,1)={1,2} S(1,0)={0,1} S(1,1)={2}
+        //   kind 4 (adjoint = 4x4 stride-2 pad-1 conv over dy, tap u): T(0)={2} T(1)={1,2} T(2)={0,1} T(3)={0}
+        // encoded as [first, last] original-tap ranges.
+        const int C1 = kind == 3 ? Cin : Cout;   // reduction channels per packed tap
+        const int pt = k / C1, c1 = k - pt * C1;
+        int y0, y1, x0, x1;
+        bool ok;
+        if (kind == 3) {
+            const int z = pt >> 2, j = pt & 3;
+            const int ry = z >> 1, rx = z & 1, a = j >> 1, b = j & 1;
+            ok = pt < 16 && col < Cout;
+            y0 = ry == 0 ? (a == 0 ? 0 : 1) : (a == 0 ? 0 : 2);
+            y1 = ry == 0 ? (a == 0 ? 0 : 2) : (a == 0 ? 1 : 2);
+            x0 = rx == 0 ? (b == 0 ? 0 : 1) : (b == 0 ? 0 : 2);
+            x1 = rx == 0 ? (b == 0 ? 0 : 2) : (b == 0 ? 1 : 2);
+        } else {
+            const int u = pt >> 2, vv = pt & 3;
+            ok = pt < 16 && col < ci_count;
+            y0 = u == 0 ? 2 : (u == 1 ? 1 : 0);
+            y1 = u == 0 ? 2 : (u == 3 ? 0 : (u == 1 ? 2 : 1));
+            x0 = vv == 0 ? 2 : (vv == 1 ? 1 : 0);
+            x1 = vv == 0 ? 2 : (vv == 3 ? 0 : (vv == 1 ? 2 : 1));
+        }
+        if (ok) {
+            const int co = kind == 3 ? col : c1, ci = kind == 3 ? c1 : col;
+            const float* wp = w + ((long long)co * Cin + ci) * 9;
+            float acc = 0.f;
+            for (int ty = y0; ty <= y1; ++ty)
+                for (int tx = x0; tx <= x1; ++tx) acc += wp[ty * 3 + tx];
+            v = acc;
+        }
+    } else if (kind == 0) {  // B[(tap)*Cin + ci][co]
         int tap = k / Cin, ci = k - tap * Cin;
         if (tap < taps && col < Cout) {
             int ty = tap / KW, tx = tap - ty * KW;
@@ -534,13 +575,17 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
     __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
 
-    const ClassGeom g = class_geom(d, 0);
-    const long long P = (long long)g.My * g.Mx * d.N;   // pixels (reduction)
-    const int Ktot = g.ntaps * d.Cs;                    // GEMM N
+    // sub-pixel descriptors (parity 2, VEC only) run one GEMM per phase z: dy rows are the
+    // phase's output pixels (2qy+ry, 2qx+rx), columns its 4 taps x Cs
+    const int ncls = d.parity == 2 ? 4 : 1;
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int ntile = L % gn;
     const int mtile = (L / gn) % gm;
-    const int split = L / (gn * gm);
+    const int z = (L / (gn * gm)) % ncls;
+    const int split = L / (gn * gm * ncls);
+    const ClassGeom g = class_geom(d, z);
+    const long long P = (long long)g.My * g.Mx * d.N;   // pixels (reduction)
+    const int Ktot = g.ntaps * d.Cs;                    // GEMM N
     const int m0 = mtile * BM;                          // output channel tile
     const int n0 = ntile * BN;                          // (tap, ci) tile
     const long long nkt_all = (P + BK - 1) / BK;
@@ -587,9 +632,10 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     };
 
     auto load_a = [&](long long kt) {  // dy rows: [p][co]
-        const long long p = kt * BK + kr;
+        long long p = kt * BK + kr;
         const int co = m0 + ac0;
         const bool ok = p < P;
+        if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;
 #pragma unroll
         for (int i = 0; i < ACH; ++i)
             ra[i] = (ok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
@@ -601,7 +647,9 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         for (int i = 0; i < BCH; ++i) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (VEC) {
             // the thread's BN/8 columns share one tap (Cs % 16 == 0); bcol_ok covers all of them
-            const int vy = pqy * d.stride - d.pt + bady, vx = pqx * d.stride - d.pl + badx;
+            // sub-pixel phases: the tap offsets already include the padding
+            const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
+            const int vx = d.parity == 2 ? pqx + badx : pqx * d.stride - d.pl + badx;
             int sy, sx;
             const bool yok = map_coord_sel(vy, Hv, d.up, d.pad_mode, sy);
             const bool xok = map_coord_sel(vx, Wv, d.up, d.pad_mode, sx);
@@ -724,7 +772,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         __syncthreads();
     }
 
-    float* slab = ws + (long long)split * d.Co * Ktot;
+    float* slab = ws + ((long long)split * ncls + z) * d.Co * Ktot;
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
         const int col = n0 + wn * WN + j * 32 + l32;
@@ -935,8 +983,12 @@ static int validate(const dcs_conv_desc* d, bool rows) {
     if (d->KH <= 0 || d->KW <= 0 || d->KH * d->KW > 64) return fail(DCS_E_INVALID, "conv: bad kernel");
     if (d->up != 1 && d->up != 2) return fail(DCS_E_INVALID, "conv: up must be 1 or 2");
     if (d->stride != 1 && d->stride != 2) return fail(DCS_E_INVALID, "conv: stride must be 1 or 2");
-    if (d->parity && (d->stride != 2 || d->up != 1 || d->pad_mode != DCS_PAD_ZERO))
+    if (d->parity < 0 || d->parity > 2) return fail(DCS_E_INVALID, "conv: parity must be 0, 1 or 2");
+    if (d->parity == 1 && (d->stride != 2 || d->up != 1 || d->pad_mode != DCS_PAD_ZERO))
         return fail(DCS_E_INVALID, "conv: parity rows need stride 2, no upsample, zero pad");
+    if (d->parity == 2 && (d->stride != 1 || d->up != 1 || d->pad_mode != DCS_PAD_ZERO || d->KH != 3 ||
+                           d->KW != 3 || d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws))
+        return fail(DCS_E_INVALID, "conv: sub-pixel rows describe nearest-x2 + 3x3 zero-pad conv (up=1, Ho=2Hs)");
     if (d->pad_mode == DCS_PAD_REFLECT && (d->pt >= d->Hs * d->up || d->pl >= d->Ws * d->up))
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
@@ -976,8 +1028,9 @@ using namespace dcs;
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                 int Kpad, int ncols, int nmajor, float* out, void* stream) {
     if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
-        ci_count > Cin || kind < 0 || kind > 2)
+        ci_count > Cin || kind < 0 || kind > 4)
         return fail(DCS_E_INVALID, "pack_weights: bad arguments");
+    if (kind >= 3 && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
     long long total = (long long)Kpad * ncols;
     hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
                        Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
@@ -1021,6 +1074,29 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
 }
 
 namespace {
+// sub-pixel wgrad: dW[co][ci][ty][tx] = sum over splits and the 4 phases z of the phase tap
+// (jy, jx) whose weight sum contains (ty, tx): jy = ry ? (ty == 2) : (ty > 0), same for x.
+__global__ void wgrad_subpixel_fold_kernel(const float* __restrict__ ws, int nsplit, int Co, int Cs,
+                                           float* __restrict__ dw) {
+    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = (long long)Co * Cs * 9;
+    if (idx >= total) return;
+    const int t = (int)(idx % 9);
+    const long long r = idx / 9;
+    const int ci = (int)(r % Cs), co = (int)(r / Cs);
+    const int ty = t / 3, tx = t - 3 * ty;
+    const long long Ktot = 4ll * Cs, slab = (long long)Co * Ktot;
+    float s = 0.f;
+    for (int q = 0; q < nsplit; ++q)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+            const int ry = z >> 1, rx = z & 1;
+            const int jy = ry ? (ty == 2) : (ty > 0), jx = rx ? (tx == 2) : (tx > 0);
+            s += ws[((long long)q * 4 + z) * slab + (long long)co * Ktot + (jy * 2 + jx) * Cs + ci];
+        }
+    dw[idx] = s;
+}
+
 struct WgradPlan {
     int BM, BN, nsplit, kt_per_split;
     long long Ktot;
@@ -1032,7 +1108,7 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
     p.Ktot = (long long)g.ntaps * d.Cs;
     p.BM = d.Co > 64 ? 128 : 64;
     p.BN = 128;
-    long long tiles = cdiv(d.Co, p.BM) * cdiv(p.Ktot, p.BN);
+    long long tiles = cdiv(d.Co, p.BM) * cdiv(p.Ktot, p.BN) * (d.parity == 2 ? 4 : 1);
     long long nkt = cdiv(P, BK);
     long long want = cdiv(1024, tiles);           // aim for >= 1024 workgroups
     long long maxs = cdiv(nkt, 8);               // >= 8 k-tiles per split
@@ -1048,7 +1124,7 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
     if (!dp) return 0;
     WgradPlan p = wgrad_plan(*dp);
-    return (size_t)p.nsplit * dp->Co * p.Ktot * sizeof(float);
+    return (size_t)p.nsplit * (dp->parity == 2 ? 4 : 1) * dp->Co * p.Ktot * sizeof(float);
 }
 
 extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const float* x, const float* x2,
@@ -1057,17 +1133,19 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     int e = validate(dp, false);
     if (e) return e;
     const dcs_conv_desc& d = *dp;
-    if (d.parity) return fail(DCS_E_INVALID, "conv_wgrad: describe the forward conv (parity=0)");
+    if (d.parity == 1) return fail(DCS_E_INVALID, "conv_wgrad: describe the forward conv (parity 0 or 2)");
     if (!dy || !x || !dw || !ws) return fail(DCS_E_INVALID, "conv_wgrad: null pointer");
     if (d.Co % 4 != 0) return fail(DCS_E_INVALID, "conv_wgrad: Co must be a multiple of 4");
     if (ws_bytes < dcs_conv_wgrad_workspace_size(dp)) return fail(DCS_E_WORKSPACE, "conv_wgrad: workspace too small");
     WgradPlan p = wgrad_plan(d);
     const int gn = (int)cdiv(p.Ktot, p.BN), gm = (int)cdiv(d.Co, p.BM);
-    dim3 grid((unsigned)(gn * gm * p.nsplit));
+    const int ncls = d.parity == 2 ? 4 : 1;
+    dim3 grid((unsigned)(gn * gm * p.nsplit * ncls));
     const bool vec = vec_ok(dp, x);
+    if (d.parity == 2 && !vec) return fail(DCS_E_INVALID, "conv_wgrad: sub-pixel rows need a vectorisable source");
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
-    const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1;
+    const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity;
     if (p.BM == 128) {
         if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
         else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
@@ -1078,6 +1156,12 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     }
     e = check_launch("conv_wgrad");
     if (e) return e;
+    if (d.parity == 2) {
+        const long long tot9 = (long long)d.Co * d.Cs * 9;
+        hipLaunchKernelGGL(wgrad_subpixel_fold_kernel, dim3((unsigned)cdiv(tot9, 256)), dim3(256), 0, s, w, p.nsplit,
+                           d.Co, d.Cs, dw);
+        return check_launch("wgrad_subpixel_fold");
+    }
     long long total = (long long)d.Co * p.Ktot;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, p.nsplit, d.Co,
                        d.Cs, d.KH, d.KW, dw);

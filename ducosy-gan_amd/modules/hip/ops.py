@@ -165,15 +165,27 @@ class ConvGeom:
     def narrow(self):
         return self.cout <= 4
 
+    @property
+    def subpixel(self) -> bool:
+        """Nearest-x2 upsample + 3x3 zero-pad conv (modules/model.py:109-110) run as four
+        sub-pixel phases of a 2x2 conv on the un-upsampled input (2.25x fewer MACs; forward),
+        and its adjoint as one 4x4 stride-2 conv over dy (data gradient)."""
+        return (self.up == 2 and self.k == 3 and self.stride == 1 and self.pad_mode == DCS_PAD_ZERO
+                and self.pads == (1, 1, 1, 1) and self.cout > 4 and self.cin % 16 == 0)
+
     # ---- weight packing ------------------------------------------------------------
     def pack_fwd(self, w: torch.Tensor) -> torch.Tensor:
         """B operand of the forward GEMM: N-major [Np][Kpad] for the MFMA rows pass (ldb =
         Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns)."""
+        if self.subpixel:
+            return self._pack(w, 3, self.cin, 16 * self.cin, self.cout)
         K = self.k * self.k * self.cin
         return self._pack(w, 0, self.cin, K, self.cout)
 
     def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
         ci = self.cin if ci_count is None else ci_count
+        if self.subpixel and ci > 4:
+            return self._pack(w, 4, ci, 16 * self.cout, ci)
         kind = 2 if self.stride == 2 else 1
         K = self.k * self.k * self.cout
         return self._pack(w, kind, ci, K, ci)
@@ -194,7 +206,7 @@ class ConvGeom:
         return wpack.shape[1]  # Kpad (N-major) or columns (K-major): always the inner dim
 
     # ---- descriptors ---------------------------------------------------------------
-    def _desc_fwd(self, s: Src, ldb: int, pro_act: int, epi_act: int) -> lib.ConvDesc:
+    def _desc_fwd(self, s: Src, ldb: int, pro_act: int, epi_act: int, rows: bool = True) -> lib.ConvDesc:
         Ho, Wo = self.out_hw(s.H, s.W)
         d = lib.ConvDesc()
         d.N, d.Hs, d.Ws, d.Cs = s.N, s.H, s.W, s.C
@@ -205,6 +217,8 @@ class ConvGeom:
         d.KH = d.KW = self.k
         d.pt, d.pl = self.pads[0], self.pads[1]
         d.stride, d.parity = self.stride, 0
+        if self.subpixel and rows:
+            d.up, d.parity = 1, 2  # phases over the source grid (the upsample is in the weights)
         d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
         d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
         return d
@@ -246,6 +260,16 @@ class ConvGeom:
         d.Co = ci
         dev = dy.device
         t, l, b, r = self.pads
+        if self.subpixel and not narrow:
+            # adjoint of the sub-pixel forward: a 4x4 stride-2 pad-1 conv over dy (kind-4 pack)
+            d.KH = d.KW = 4
+            d.stride, d.parity, d.pt, d.pl = 2, 0, 1, 1
+            d.Ho, d.Wo = H, W
+            out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
+            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out), _stream())
+            if addend is not None:
+                lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
+            return out
         if self.stride == 2:
             assert self.up == 1 and self.pad_mode == DCS_PAD_ZERO
             d.stride, d.parity, d.pt, d.pl = 2, 1, t, l
@@ -291,7 +315,7 @@ class ConvGeom:
         """dL/dW in torch's OIHW layout."""
         _check_dev(dy, s.t, s.t2)
         pro_act = pro[2] if pro is not None else ACT_NONE
-        d = self._desc_fwd(s, 0, pro_act, ACT_NONE)
+        d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
         assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)
         if out is None:
             out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device,
