@@ -1108,14 +1108,31 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
     p.Ktot = (long long)g.ntaps * d.Cs;
     p.BM = d.Co > 64 ? 128 : 64;
     p.BN = 128;
-    long long tiles = cdiv(d.Co, p.BM) * cdiv(p.Ktot, p.BN) * (d.parity == 2 ? 4 : 1);
-    long long nkt = cdiv(P, BK);
-    long long want = cdiv(1024, tiles);           // aim for >= 1024 workgroups
-    long long maxs = cdiv(nkt, 8);               // >= 8 k-tiles per split
-    long long ns = want < maxs ? want : maxs;
-    if (ns < 1) ns = 1;
-    if (ns > 256) ns = 256;
-    p.kt_per_split = (int)cdiv(nkt, ns);
+    const long long tiles = cdiv(d.Co, p.BM) * cdiv(p.Ktot, p.BN) * (d.parity == 2 ? 4 : 1);
+    const long long nkt = cdiv(P, BK);
+    // Workgroups run in rounds of `slots` (256 CUs x blocks per CU: 3 for the vectorised BM=64
+    // kernel, else 2, by VGPR budget) and every block streams the same number of k-tiles, so a grid of
+    // tiles*nsplit blocks costs ceil(blocks/slots) rounds.  Pick the split count that
+    // fills the rounds best (>= 8 k-tiles per split, <= 256 splits), preferring fewer splits
+    // (less partial-slab traffic) among equally full choices.
+    const bool vec_shape = d.Cs % 16 == 0 && d.s_c == 1 && d.csplit == d.Cs;  // vec_ok minus alignment
+    const long long slots = 256 * (p.BM == 64 && vec_shape ? 3 : 2);
+    long long maxs = cdiv(nkt, 8);
+    if (maxs > 256) maxs = 256;
+    if (maxs < 1) maxs = 1;
+    long long best = 1;
+    double best_score = -1.0;
+    for (long long ns = 1; ns <= maxs; ++ns) {
+        const long long kps = cdiv(nkt, ns);
+        const long long nsr = cdiv(nkt, kps);            // splits actually used
+        const long long blocks = tiles * nsr;
+        const long long rounds = cdiv(blocks, slots);
+        // time ~ rounds * k-tiles per block (+ a small per-block epilogue cost)
+        const double cost = (double)rounds * (double)(kps + 2);
+        const double score = 1.0 / cost;
+        if (score > best_score * 1.0001) { best_score = score; best = ns; }
+    }
+    p.kt_per_split = (int)cdiv(nkt, best);
     p.nsplit = (int)cdiv(nkt, p.kt_per_split);
     return p;
 }
