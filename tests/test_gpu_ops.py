@@ -237,3 +237,23 @@ def test_integration_md_ctypes_example(ops):
     x, w, y = env["x"].cpu(), env["w"].cpu(), env["y"].cpu()
     ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect"), w).permute(0, 2, 3, 1)
     assert float((y - ref).abs().max()) <= 1e-4 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("H", [3, 4, 9, 16])
+def test_reflect_dgrad_direct_and_accumulate(ops, H):
+    """Residual-conv data gradient (padded-grid transposed conv + reflection fold) against
+    autograd through F.pad(reflect) + conv2d, with and without the residual addend, down to
+    the smallest reflectable size."""
+    g, _ = _geom((256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, H))
+    x = rnd((2, 256, H, H), 31, "x").requires_grad_(True)
+    w = rnd((256, 256, 3, 3), 31, "w", -0.05, 0.05)
+    dy = rnd((2, 256, H, H), 31, "dy")
+    torch_conv(x, w, g).backward(dy)
+    wd = g.pack_dgrad(w.cuda())
+    dyn = dy.permute(0, 2, 3, 1).contiguous().cuda()
+    dx = g.dgrad(dyn, wd, H, H)
+    assert rel(dx.permute(0, 3, 1, 2), x.grad) < 1e-4
+    add = rnd((2, H, H, 256), 31, "add").cuda()
+    want = dx + add
+    got = g.dgrad(dyn, wd, H, H, addend=add.clone())
+    assert rel(got, want) < 1e-5
