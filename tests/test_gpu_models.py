@@ -146,3 +146,20 @@ def test_generator_vs_oracle_128():
     for name, p in G.named_parameters():
         if p.dim() == 4:
             assert rel2(p.grad, pr[name].grad) < GTOL, name
+
+
+def test_batched_translation_matches_single_slices():
+    """generate.py path: slices translated in batches give the per-slice outputs (per-sample
+    InstanceNorm; only the statistics' chunking, and so their rounding, depends on the batch)."""
+    import numpy as np
+    from modules.inference import translate_slices
+    from modules.model import Generator
+    torch.manual_seed(0)
+    G = Generator(1, 2).cuda().eval()
+    rng = np.random.default_rng(0)
+    slices = [rng.uniform(-1, 1, size=(40, 40)).astype(np.float32) for _ in range(5)]
+    batched = translate_slices(G, slices, 32, batch=4)
+    single = translate_slices(G, slices, 32, batch=1)
+    for a, b in zip(batched, single):
+        assert a.shape == (40, 40)
+        assert np.abs(a - b).max() <= 1e-5
