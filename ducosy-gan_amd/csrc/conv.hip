@@ -233,6 +233,12 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
                 for (int tx = x0; tx <= x1; ++tx) acc += wp[ty * 3 + tx];
             v = acc;
         }
+    } else if (kind == 5) {  // B[(tap)*ci_count + ci][co], zero for ci >= Cin (padded source)
+        int tap = k / ci_count, ci = k - tap * ci_count;
+        if (tap < taps && col < Cout && ci < Cin) {
+            int ty = tap / KW, tx = tap - ty * KW;
+            v = w[(((long long)col * Cin + ci) * KH + ty) * KW + tx];
+        }
     } else if (kind == 0) {  // B[(tap)*Cin + ci][co]
         int tap = k / Cin, ci = k - tap * Cin;
         if (tap < taps && col < Cout) {
@@ -363,7 +369,9 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
     return d;
 }
 
-template <int BM, int BN, bool VEC, int TAG>
+// VEC: 0 scalar gather (any layout), 1 = 16 consecutive k of one tap per thread (Cs % 16 == 0),
+//      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
+template <int BM, int BN, int VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
@@ -423,7 +431,24 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     float4 rb[BCH];
 
     auto load_a = [&](int kt) {
-        if (VEC) {
+        if (VEC == 2) {  // Cs == 4: taps aj .. aj+3, one float4 each (no prologue)
+            ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rvalid) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = aj + e;
+                    if (j < g.ntaps) {
+                        int ady, adx, bt;
+                        tap_decode(d, g, j, ady, adx, bt);
+                        int sy, sx;
+                        if (map_coord(ri.by + ady, Hv, d.up, d.pad_mode, sy) &&
+                            map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx))
+                            ra[e] = *reinterpret_cast<const float4*>(srow + sy * d.s_h + sx * d.s_w);
+                    }
+                }
+            }
+            aj += BK / 4;
+        } else if (VEC) {
             // (a buffer-descriptor variant of this gather, as in the wgrad pass, measured 3-7 %
             //  slower here: invalid taps would issue loads that the branch now skips)
             ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -560,7 +585,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 // to LDS (8 threads per pixel row, one pixel decode per thread per k-tile).  A lane's MFMA
 // operands are single floats down a column ([2s+h][m]); all 16 k-steps of a tile are read
 // into registers before the tile's MFMAs so LDS latency is paid once per tile.
-template <int BM, int BN, bool VEC, int TAG>
+template <int BM, int BN, int VEC, int TAG>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
     const float* __restrict__ src2, const float* __restrict__ psc, const float* __restrict__ psh,
@@ -606,7 +631,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     const int nb0 = n0 + bc0;
     const bool bcol_ok = nb0 < Ktot;
     int bady = 0, badx = 0, bchan = 0;
-    if (VEC && bcol_ok) {
+    // VEC == 2 (Cs == 4): the thread's 16 columns are 4 taps x 4 channels
+    int q4y[4] = {0, 0, 0, 0}, q4x[4] = {0, 0, 0, 0};
+    bool q4ok[4] = {false, false, false, false};
+    if (VEC == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int j = nb0 / 4 + e;
+            q4ok[e] = nb0 + 4 * e < Ktot;
+            int bt;
+            if (q4ok[e]) tap_decode(d, g, j, q4y[e], q4x[e], bt);
+        }
+    } else if (VEC && bcol_ok) {
         const int j = nb0 / d.Cs;
         bchan = nb0 - j * d.Cs;
         int bt;
@@ -645,7 +681,19 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
         const long long p = kt * BK + kr;
 #pragma unroll
         for (int i = 0; i < BCH; ++i) rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (VEC) {
+        if (VEC == 2) {
+            const int by = pqy * d.stride - d.pt, bx = pqx * d.stride - d.pl;
+            const int rowoff = pn * (int)d.s_n;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                int sy, sx;
+                const bool yok = map_coord_sel(by + q4y[e], Hv, d.up, d.pad_mode, sy);
+                const bool xok = map_coord_sel(bx + q4x[e], Wv, d.up, d.pad_mode, sx);
+                const bool ok = p < P && q4ok[e] && yok && xok;
+                rb[e] = buf_load4(rsrc, ok ? (rowoff + sy * (int)d.s_h + sx * (int)d.s_w) * 4 : OOB_OFF);
+            }
+            advance_pix();
+        } else if (VEC) {
             // the thread's BN/8 columns share one tap (Cs % 16 == 0); bcol_ok covers all of them
             // sub-pixel phases: the tap offsets already include the padding
             const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
@@ -749,7 +797,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
                 const float* b = &Bs[cur][8 * q + lh][bcol[j]];
                 bf[j][q] = make_float4(b[0], b[2 * LDB], b[4 * LDB], b[6 * LDB]);
             }
-        if constexpr (VEC) {
+        if constexpr (VEC != 0) {
             mfma_chain<IM, JN, 0, 2>(af, bf, t);
             if (kt + 1 < kt_end) { load_a(kt + 1); load_b(kt + 1); }
             mfma_chain<IM, JN, 2, 4>(af, bf, t);
@@ -791,7 +839,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
 // their own (co, tap, ci) order so the nsplit reads per output are coalesced; each output is
 // written once (scattered into OIHW).  Fixed split order: deterministic.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int Co, int Cs, int KH,
-                                    int KW, float* __restrict__ dw) {
+                                    int KW, int Cw, float* __restrict__ dw) {
     long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int taps = KH * KW;
     const long long Ktot = (long long)taps * Cs;
@@ -801,8 +849,9 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, in
     const int k = (int)(idx - (long long)co * Ktot);
     const int tap = k / Cs, ci = k - tap * Cs;
     float s = 0.f;
+    if (ci >= Cw) return;  // zero-padded source channel (no weight)
     for (int q = 0; q < nsplit; ++q) s += ws[(long long)q * total + idx];
-    dw[((long long)co * Cs + ci) * taps + tap] = s;
+    dw[((long long)co * Cw + ci) * taps + tap] = s;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -992,6 +1041,7 @@ static int validate(const dcs_conv_desc* d, bool rows) {
     if (d->pad_mode == DCS_PAD_REFLECT && (d->pt >= d->Hs * d->up || d->pl >= d->Ws * d->up))
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
+    if (d->cw < 0 || d->cw > d->Cs) return fail(DCS_E_INVALID, "conv: bad cw (weight channels)");
     if (!d->parity) {
         // output dims must be those of the forward conv over the virtual input
         int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
@@ -999,6 +1049,15 @@ static int validate(const dcs_conv_desc* d, bool rows) {
     }
     (void)rows;
     return DCS_OK;
+}
+
+// 4-channel NHWC source (the packed stem input): float4 per tap, 16-byte aligned pixels
+static bool vec4_ok(const dcs_conv_desc* d, const float* src) {
+    const long long extent = (long long)(d->N - 1) * d->s_n + (long long)(d->Hs - 1) * d->s_h +
+                             (long long)(d->Ws - 1) * d->s_w + d->Cs;
+    return d->Cs == 4 && d->s_c == 1 && d->csplit == 4 && (d->s_w % 4 == 0) && (d->s_h % 4 == 0) &&
+           (d->s_n % 4 == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0) && d->s_n >= 0 && d->s_h >= 0 &&
+           d->s_w >= 0 && extent * 4 < (long long)OOB_OFF - 64;
 }
 
 static bool vec_ok(const dcs_conv_desc* d, const float* src) {
@@ -1028,9 +1087,9 @@ using namespace dcs;
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                 int Kpad, int ncols, int nmajor, float* out, void* stream) {
     if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
-        ci_count > Cin || kind < 0 || kind > 4)
+        (kind != 5 && ci_count > Cin) || (kind == 5 && ci_count < Cin) || kind < 0 || kind > 5)
         return fail(DCS_E_INVALID, "pack_weights: bad arguments");
-    if (kind >= 3 && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
+    if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
     long long total = (long long)Kpad * ncols;
     hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
                        Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
@@ -1059,16 +1118,19 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     const int gx = (int)cdiv(Mmax, 128), gy = (int)cdiv(d.Co, BN);
     dim3 grid((unsigned)(gx * gy * ncls));
     const bool vec = vec_ok(dp, src);
+    const bool v4 = !vec && vec4_ok(dp, src) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
                      d.stride == 1;
     hipStream_t s = as_stream(stream);
     if (BN == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, true, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, false, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
     }
     return check_launch("conv_rows");
 }
@@ -1115,7 +1177,7 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
     // tiles*nsplit blocks costs ceil(blocks/slots) rounds.  Pick the split count that
     // fills the rounds best (>= 8 k-tiles per split, <= 256 splits), preferring fewer splits
     // (less partial-slab traffic) among equally full choices.
-    const bool vec_shape = d.Cs % 16 == 0 && d.s_c == 1 && d.csplit == d.Cs;  // vec_ok minus alignment
+    const bool vec_shape = (d.Cs % 16 == 0 || d.Cs == 4) && d.s_c == 1 && d.csplit == d.Cs;  // minus alignment
     const long long slots = 256 * (p.BM == 64 && vec_shape ? 3 : 2);
     long long maxs = cdiv(nkt, 8);
     if (maxs > 256) maxs = 256;
@@ -1163,13 +1225,16 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
     const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity;
+    const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
     if (p.BM == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
-        else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, false, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (v4) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, false, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (v4) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 2, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 0, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
     }
     e = check_launch("conv_wgrad");
     if (e) return e;
@@ -1181,7 +1246,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     }
     long long total = (long long)d.Co * p.Ktot;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, p.nsplit, d.Co,
-                       d.Cs, d.KH, d.KW, dw);
+                       d.Cs, d.KH, d.KW, d.cw > 0 ? d.cw : d.Cs, dw);
     return check_launch("conv_wgrad_reduce");
 }
 
@@ -1267,7 +1332,7 @@ extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, c
         e = launch_narrow_wgrad_tiled(d, dy, x, psc, psh, w, s);
         if (e) return e;
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(Ktot, 256)), dim3(256), 0, s, w,
-                           narrow_wgrad_tiled_blocks(d), 1, d.Cs, d.KH, d.KW, dw);
+                           narrow_wgrad_tiled_blocks(d), 1, d.Cs, d.KH, d.KW, d.cw > 0 ? d.cw : d.Cs, dw);
         return check_launch("narrow_wgrad_tiled_reduce");
     }
     if (d.Co == 1) hipLaunchKernelGGL((conv_wgrad_narrow_kernel<1, false>), grid, dim3(256), 0, s, d, dy, x, x2, psc, psh, w, pps);
@@ -1278,8 +1343,30 @@ extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, c
     if (e) return e;
     long long total = (long long)d.Co * Ktot;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
-                       d.KH, d.KW, dw);
+                       d.KH, d.KW, d.cw > 0 ? d.cw : d.Cs, dw);
     return check_launch("conv_wgrad_narrow_reduce");
+}
+
+__global__ void pack_nhwc4_kernel(const float* __restrict__ x, int c1, const float* __restrict__ x2, int c2,
+                                  long long HW, long long total, float4* __restrict__ out) {
+    long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel index n*HW + hw
+    if (p >= total) return;
+    const long long n = p / HW, hw = p - n * HW;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < c1; ++c) v[c] = x[(n * c1 + c) * HW + hw];
+    for (int c = 0; c < c2; ++c) v[c1 + c] = x2[(n * c2 + c) * HW + hw];
+    out[p] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+extern "C" int dcs_pack_nhwc4(const float* x, int c1, const float* x2, int c2, int N, int H, int W, float* out,
+                              void* stream) {
+    if (!x || !out || c1 < 1 || c2 < 0 || c1 + c2 > 4 || (c2 > 0 && !x2) || N <= 0 || H <= 0 || W <= 0 ||
+        (reinterpret_cast<uintptr_t>(out) & 15))
+        return fail(DCS_E_INVALID, "pack_nhwc4: bad arguments");
+    const long long HW = (long long)H * W, total = (long long)N * HW;
+    hipLaunchKernelGGL(pack_nhwc4_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), x, c1,
+                       x2, c2, HW, total, reinterpret_cast<float4*>(out));
+    return check_launch("pack_nhwc4");
 }
 
 extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* dx, int N, int H, int W, int C,

@@ -21,7 +21,7 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [
         ("N", c_int32), ("Hs", c_int32), ("Ws", c_int32), ("Cs", c_int32),
         ("s_n", c_int64), ("s_c", c_int64), ("s_h", c_int64), ("s_w", c_int64),
-        ("csplit", c_int32), ("pad0", c_int32),
+        ("csplit", c_int32), ("cw", c_int32),
         ("s2_n", c_int64), ("s2_c", c_int64), ("s2_h", c_int64), ("s2_w", c_int64),
         ("up", c_int32), ("pad_mode", c_int32),
         ("KH", c_int32), ("KW", c_int32), ("pt", c_int32), ("pl", c_int32),
@@ -43,6 +43,7 @@ SIGNATURES = {
     "dcs_conv_wgrad_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
     "dcs_reflect_fold": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "dcs_pack_nhwc4": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
     "dcs_upsample2_grad": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "dcs_in_stats_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "dcs_in_stats": (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P, P, c_size_t, P]),

@@ -119,14 +119,17 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     L = gen_layers(cin, nb)
     W = dict(W)
     W["pk"] = pk = {}
-    for name in ("stem", "down1", "down2", "up1", "up2", "head"):
+    for name in ("down1", "down2", "up1", "up2", "head"):
         pk[f"{name}.w"] = L[name].pack_fwd(W[f"{name}.w"])
+    # stem input: image (+ mask planes) packed once into NHWC x 4 channels, so the 7x7 gather
+    # moves one float4 per tap (the reference's torch.cat of image and masks, fused)
+    stem_src = Src.nhwc(ops.pack_nhwc4(x, x2)) if cin <= 4 else Src.nchw(x, x2)
+    pk["stem.w"] = L["stem"].pack_fwd(W["stem.w"], cin_pad=stem_src.C)
     for b in range(nb):
         pk[f"r{b}.c1.w"] = L["res"].pack_fwd(W[f"r{b}.c1.w"])
         pk[f"r{b}.c2.w"] = L["res"].pack_fwd(W[f"r{b}.c2.w"])
-    xs = Src.nchw(x, x2)
-    N, H, Wd = xs.N, xs.H, xs.W
-    y0 = L["stem"].forward(xs, pk["stem.w"])
+    N, H, Wd = stem_src.N, stem_src.H, stem_src.W
+    y0 = L["stem"].forward(stem_src, pk["stem.w"])
     s0 = ops.in_stats(y0)
     a0 = ops.in_apply(y0, s0, ACT_RELU)
     y1 = L["down1"].forward(Src.nhwc(a0), pk["down1.w"])
@@ -149,7 +152,7 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     out = out.view(N, 1, H, Wd)
     saved = None
     if keep:
-        saved = dict(L=L, W=W, xs=xs, y0=y0, s0=s0, a0=a0, y1=y1, s1=s1, a1=a1, y2=y2, s2=s2, blocks=blocks,
+        saved = dict(L=L, W=W, xs=stem_src, y0=y0, s0=s0, a0=a0, y1=y1, s1=s1, a1=a1, y2=y2, s2=s2, blocks=blocks,
                      h=h, yu1=yu1, su1=su1, au1=au1, yu2=yu2, su2=su2, nb=nb, use_cbam=use_cbam)
     else:
         del a0, a1, au1
@@ -257,10 +260,11 @@ def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: boo
     L = disc_layers(x.shape[1])
     ws = params[0::2]
     bs = params[1::2]
-    pk = [g.pack_fwd(w) for g, w in zip(L, ws)]
+    # layer-0 input packed NHWC x 4 (zero channels) for the vectorised gather
+    xs = Src.nhwc(ops.pack_nhwc4(x)) if x.shape[1] <= 4 else Src.nchw(x)
+    pk = [L[0].pack_fwd(ws[0], cin_pad=xs.C)] + [g.pack_fwd(w) for g, w in zip(L[1:], ws[1:])]
     N = x.shape[0]
     dev = x.device
-    xs = Src.nchw(x)
     # layer 0: conv + bias; its LeakyReLU is the next conv's prologue (scale 1, shift 0)
     y0 = L[0].forward(xs, pk[0], bias=bs[0])
     ones = torch.ones(N, 64, device=dev, dtype=torch.float32)

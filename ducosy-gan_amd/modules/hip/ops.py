@@ -174,9 +174,12 @@ class ConvGeom:
                 and self.pads == (1, 1, 1, 1) and self.cout > 4 and self.cin % 16 == 0)
 
     # ---- weight packing ------------------------------------------------------------
-    def pack_fwd(self, w: torch.Tensor) -> torch.Tensor:
+    def pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
         """B operand of the forward GEMM: N-major [Np][Kpad] for the MFMA rows pass (ldb =
-        Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns)."""
+        Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns).  ``cin_pad``: the
+        source carries that many channels (zero-padded beyond cin; the 4-channel stem)."""
+        if cin_pad is not None and cin_pad != self.cin:
+            return self._pack(w, 5, cin_pad, self.k * self.k * cin_pad, self.cout)
         if self.subpixel:
             return self._pack(w, 3, self.cin, 16 * self.cin, self.cout)
         K = self.k * self.k * self.cin
@@ -227,7 +230,7 @@ class ConvGeom:
     def forward(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
                 epi_act: int = ACT_NONE) -> torch.Tensor:
-        assert s.C == self.cin, (s.C, self.cin)
+        assert s.C == self.cin or (s.C == 4 and self.cin < 4), (s.C, self.cin)
         _check_dev(s.t, s.t2, wpack, bias)
         Ho, Wo = self.out_hw(s.H, s.W)
         pro_act = pro[2] if pro is not None else ACT_NONE
@@ -316,6 +319,8 @@ class ConvGeom:
         _check_dev(dy, s.t, s.t2)
         pro_act = pro[2] if pro is not None else ACT_NONE
         d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
+        if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
+            d.cw = self.cin
         assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)
         if out is None:
             out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device,
@@ -343,6 +348,19 @@ class INStats:
 
     def __init__(self, scale, shift, xmax=None, xargmax=None):
         self.scale, self.shift, self.xmax, self.xargmax = scale, shift, xmax, xargmax
+
+
+def pack_nhwc4(x: torch.Tensor, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NCHW image [N,c1,H,W] (+ NCHW masks [N,c2,H,W]) -> NHWC [N,H,W,4], zero channels after
+    c1+c2: the layout of the vectorised stem gather (the trainer.py:451 concat, fused)."""
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    _check_dev(x, x2)
+    N, c1, H, W = x.shape
+    c2 = x2.shape[1] if x2 is not None else 0
+    out = torch.empty(N, H, W, 4, device=x.device, dtype=torch.float32)
+    lib.call("dcs_pack_nhwc4", _p(x), c1, _p(x2), c2, N, H, W, _p(out), _stream())
+    return out
 
 
 def in_stats(x: torch.Tensor, want_max: bool = False) -> INStats:

@@ -58,7 +58,8 @@ typedef struct dcs_conv_desc {
     int32_t Hs, Ws, Cs;             /* source dims (Cs = reduction channels per tap)      */
     int64_t s_n, s_c, s_h, s_w;     /* source element strides                             */
     int32_t csplit;                 /* channels >= csplit come from src2 (concat fusion)  */
-    int32_t pad0;
+    int32_t cw;                     /* weight input channels if < Cs (zero-padded source  */
+                                    /* channels, e.g. the 3-channel stem packed to 4); 0 = Cs */
     int64_t s2_n, s2_c, s2_h, s2_w; /* src2 strides (channel index relative to csplit)   */
     int32_t up;                     /* nearest-upsample factor of the source (1 or 2)     */
     int32_t pad_mode;               /* DCS_PAD_ZERO / DCS_PAD_REFLECT                     */
@@ -82,6 +83,9 @@ int dcs_version(void);
  * kind 0 forward   : B[(ty*KW+tx)*Cin + ci][co] = W[co][ci][ty][tx]
  * kind 1 dgrad-flip: B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][KH-1-ty][KW-1-tx]  (stride-1 dgrad)
  * kind 2 dgrad     : B[(ty*KW+tx)*Cout + co][ci] = W[co][ci][ty][tx]              (stride-2 dgrad)
+ * kind 3 / 4      : sub-pixel forward / data gradient of nearest-x2 upsample + 3x3 conv
+ * kind 5 fwd-pad  : B[(ty*KW+tx)*ci_count + ci][co] = ci < Cin ? W[co][ci][ty][tx] : 0
+ *                   (forward over a source whose channels are zero-padded to ci_count)
  * ci_count limits the packed input channels (dgrad of a concat input needs only the first). */
 int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                      int Kpad, int ncols, int nmajor, float* out, void* stream);
@@ -97,6 +101,12 @@ size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* d);
 int dcs_conv_wgrad(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
                    const float* pro_scale, const float* pro_shift, float* dw, void* ws,
                    size_t ws_bytes, void* stream);
+
+/* Pack up to 4 NCHW planes (x: [N][c1][H][W], x2: [N][c2][H][W] or NULL) into one NHWC
+ * [N][H][W][4] tensor with zero channels after c1+c2 (c1 + c2 <= 4): the 4-channel layout the
+ * vectorised stem convolution gathers (modules/model.py:94 input, trainer.py:451 concat). */
+int dcs_pack_nhwc4(const float* x, int c1, const float* x2, int c2, int N, int H, int W, float* out,
+                   void* stream);
 
 /* Fold the gradient of a reflection-padded tensor back onto the tensor:
  * dx[n,i,j,c] = addend[n,i,j,c] + sum over padded positions mirroring to (i,j). */

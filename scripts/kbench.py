@@ -44,6 +44,7 @@ LAYERS = [
     ("up1", ConvGeom(256, 128, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 128, False),
     ("up2", ConvGeom(128, 64, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 256, True),
     ("head", ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT), 512, True),
+    ("d0", ConvGeom(1, 64, 4, 2, (1, 1, 1, 1)), 512, False),
     ("d1", ConvGeom(64, 128, 4, 2, (1, 1, 1, 1)), 256, True),
     ("d2", ConvGeom(128, 256, 4, 2, (1, 1, 1, 1)), 128, True),
     ("d3", ConvGeom(256, 512, 4, 2, (1, 1, 1, 1)), 64, True),
@@ -70,7 +71,9 @@ def main():
         p = (st.scale, st.shift, ACT_RELU) if pro else None
         Ho, Wo = g.out_hw(H, H)
         flop = 2.0 * N * Ho * Wo * g.cout * g.cin * g.k * g.k
-        wp = g.pack_fwd(w)
+        if g.cin < 4:  # production layout of the stem / PatchGAN layer 0: NHWC x 4 (zero channels)
+            x = torch.nn.functional.pad(x, (0, 4 - g.cin))
+        wp = g.pack_fwd(w, cin_pad=x.shape[-1])
         t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p), a.reps)
         print(f"{name:8s} {'fwd':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
         dy = torch.randn(N, Ho, Wo, g.cout, device=dev)
