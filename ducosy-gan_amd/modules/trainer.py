@@ -95,18 +95,22 @@ class CycleGANSystem:
         host synchronisation inside)."""
         N = real_A.shape[0]
         G_AB, G_BA, D_A, D_B = self.models
-        m2 = torch.cat([masks, masks]) if masks is not None else None
+        mk = (lambda k: torch.cat([masks] * k)) if masks is not None else (lambda k: None)
 
         # --- Generator step (trainer.py:463-514) ---
+        # Three Generator launches instead of the reference's six calls: G_A2B on
+        # [real_A; real_B] -> [fake_B; id_B]; G_B2A on [real_B; real_A; fake_B] ->
+        # [fake_A; id_A; rec_A]; G_A2B on fake_A -> rec_B.  Same inputs and weights per sample
+        # as trainer.py:466-481 (InstanceNorm is per sample), fewer and fuller launches.
         self.optimizer_G.zero_grad()
-        ab = G_AB(torch.cat([real_A, real_B]), m2)   # [fake_B ; id_B]
-        ba = G_BA(torch.cat([real_B, real_A]), m2)   # [fake_A ; id_A]
+        ab = G_AB(torch.cat([real_A, real_B]), mk(2))              # [fake_B ; id_B]
         fake_B, id_B = ab[:N], ab[N:]
-        fake_A, id_A = ba[:N], ba[N:]
+        ba = G_BA(torch.cat([real_B, real_A, fake_B]), mk(3))      # [fake_A ; id_A ; rec_A]
+        fake_A, id_A, rec_A = ba[:N], ba[N:2 * N], ba[2 * N:]
         loss_id = (self.criterion_identity(id_A, real_A) + self.criterion_identity(id_B, real_B)) / 2
         loss_GAN = (self.criterion_GAN(D_B(fake_B, params_require_grad=False), 1.0)
                     + self.criterion_GAN(D_A(fake_A, params_require_grad=False), 1.0)) / 2
-        rec_A, rec_B = G_BA(fake_B, masks), G_AB(fake_A, masks)
+        rec_B = G_AB(fake_A, masks)
         loss_cycle = (self.criterion_cycle(rec_A, real_A) + self.criterion_cycle(rec_B, real_B)) / 2
         loss_grad_cycle = (self.criterion_gradient(rec_A, real_A) + self.criterion_gradient(rec_B, real_B)) / 2
         loss_grad_id = (self.criterion_gradient(id_A, real_A) + self.criterion_gradient(id_B, real_B)) / 2
