@@ -10,7 +10,7 @@ GPU that is already resident in HBM.  Data parallel: one process per GPU, each w
 shard; one RCCL all-reduce per optimizer (weak scaling).  Rank 0 prints ONE JSON line.
 
 roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (implicit GEMM,
-conv_rows_kernel<128,128,true,1>, forward + data-gradient launches).  Its per-launch duration
+conv_rows_kernel<128,128,1,1>, forward + data-gradient launches).  Its per-launch duration
 is measured live with HIP events on the launch stream over the timed steps; FLOPs are
 algorithmic (2*pixels*256*256*9 per launch).  Peak = 157.3 TFLOP/s (gfx950 f32 MFMA, dense).
 cpu_baseline: the oracle (oracle/ref_torch.py, the CPU restatement of the reference step)
@@ -140,7 +140,7 @@ def main():
                 "residual_blocks": args.blocks, "input_channels": args.cin, "parallelism": f"dp{world}",
             },
             "roofline": {
-                "kernel": "conv_rows_kernel<128,128,true,1> (256-ch 3x3 residual conv, fwd+dgrad)",
+                "kernel": "conv_rows_kernel<128,128,1,1> (256-ch 3x3 residual conv, fwd+dgrad)",
                 "bound": "mfma",
                 "achieved": round(achieved, 3),
                 "peak": F32_MFMA_PEAK_TFLOPS,

@@ -27,17 +27,25 @@ def init_from_env(backend: str = None):
     """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/MASTER_*).
     Returns (rank, world_size, local_rank).  No-op for a single process."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = local_device_index()
     if ws <= 1:
-        return 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
+        return 0, 1, local
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+            backend = os.environ.get("DUCOSY_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend)
-    return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+    return dist.get_rank(), dist.get_world_size(), local
+
+
+def local_device_index() -> int:
+    """GPU of this process: LOCAL_RANK (one process per GPU).  DUCOSY_DEVICE_OVERRIDE pins
+    every rank to one device — for rehearsing the multi-process path on a single GPU with
+    DUCOSY_DIST_BACKEND=gloo (RCCL does not allow two ranks on one device)."""
+    o = os.environ.get("DUCOSY_DEVICE_OVERRIDE")
+    return int(o) if o not in (None, "") else int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def broadcast_(flat: torch.Tensor, src: int = 0):

@@ -14,7 +14,7 @@ import shutil
 import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-KERNEL = "conv_rows_kernel<128, 128, true, 1>"
+KERNEL = "conv_rows_kernel<128, 128, 1, 1>"
 
 
 def _mean_counter(path, counter):
@@ -37,7 +37,7 @@ def main(tag):
     fetch, n = _mean_counter(os.path.join(out, f"prof_{tag}_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
     write, _ = _mean_counter(os.path.join(out, f"prof_{tag}_write", "write_counter_collection.csv"), "WRITE_SIZE")
     res = {
-        "kernel": "conv_rows_kernel<128,128,true,1>",
+        "kernel": "conv_rows_kernel<128,128,1,1>",
         "launches_profiled": n,
         "FETCH_SIZE_kB_mean": fetch,
         "WRITE_SIZE_kB_mean": write,
