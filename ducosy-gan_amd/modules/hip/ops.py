@@ -534,3 +534,74 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step):
     bc2 = 1.0 - beta2 ** step
     lib.call("dcs_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1),
              float(beta2), float(eps), float(bc1), float(bc2), _stream())
+
+
+# ---------------------------------------------------------------------------------------
+# input pipeline: HU transform + anatomical masks (modules/preprocess.py, mask_generator.py)
+# ---------------------------------------------------------------------------------------
+_RAW_DTYPES = {torch.int16: 0, torch.uint16: 1, torch.float32: 2} if hasattr(torch, "uint16") \
+    else {torch.int16: 0, torch.float32: 2}
+MASK_KINDS = ("lung", "mediastinum", "bone", "lung_vessel")
+# mask_generator.py defaults: detect_lung(-1000, -300, min_size 64, border 32),
+# detect_lung_vessels(-300, 600), detect_mediastinum(-300, 450), detect_bone(200, 0.25)
+MASK_DEFAULTS = dict(lung_lower=-1000, lung_upper=-300, min_size=64, border_margin=32,
+                     vessel_lower=-300, vessel_upper=600, mediastinum_lower=-300, mediastinum_upper=450,
+                     bone_threshold=200, spine_margin_ratio=0.25)
+
+
+def hu_transform(raw: torch.Tensor, slope: torch.Tensor, intercept: torch.Tensor, hu_min: float, hu_max: float,
+                 soft: bool = True, sigma: float = 50.0, want_hu: bool = True, want_img: bool = True):
+    """[N,H,W] stored pixels (int16/uint16/float32) -> (hu, img) float32 [N,H,W] on the device
+    (preprocess.py:43-55 with apply_soft_squeezing :6-40).  slope/intercept: float32 [N]."""
+    if not raw.is_cuda or not slope.is_cuda or not intercept.is_cuda:
+        raise RuntimeError("ducosy HIP ops require device tensors (no CPU fallback)")
+    if raw.dtype not in _RAW_DTYPES:
+        raise RuntimeError(f"hu_transform: unsupported pixel dtype {raw.dtype}")
+    if raw.dim() == 2:
+        raw = raw[None]
+    raw = raw.contiguous()
+    N, H, W = raw.shape
+    slope = slope.to(torch.float32).reshape(-1).contiguous()
+    intercept = intercept.to(torch.float32).reshape(-1).contiguous()
+    if slope.numel() != N or intercept.numel() != N:
+        raise ValueError("hu_transform: one slope/intercept per slice")
+    hu = torch.empty(N, H, W, device=raw.device, dtype=torch.float32) if want_hu else None
+    img = torch.empty(N, H, W, device=raw.device, dtype=torch.float32) if want_img else None
+    lib.call("dcs_hu_transform", _p(raw), _RAW_DTYPES[raw.dtype], _p(slope), _p(intercept), N, H, W,
+             float(hu_min), float(hu_max), int(bool(soft)), float(sigma), _p(hu), _p(img), _stream())
+    return hu, img
+
+
+def anatomical_masks(hu: torch.Tensor, mask_types=MASK_KINDS, out: Optional[torch.Tensor] = None, **params):
+    """HU slices [N,H,W] float32 -> float32 masks [N, len(mask_types), H, W] in mask_types order
+    (generate_anatomical_masks per 2-D slice + the channel concat of dataset.py:135-158)."""
+    _check_dev(hu)
+    if hu.dtype != torch.float32:
+        raise RuntimeError("anatomical_masks: HU must be float32")
+    if hu.dim() == 2:
+        hu = hu[None]
+    hu = hu.contiguous()
+    N, H, W = hu.shape
+    kinds = list(mask_types)
+    if not kinds or any(k not in MASK_KINDS for k in kinds) or len(set(kinds)) != len(kinds):
+        raise ValueError(f"anatomical_masks: mask_types must be distinct names from {MASK_KINDS}")
+    p = dict(MASK_DEFAULTS)
+    unknown = set(params) - set(p)
+    if unknown:
+        raise TypeError(f"anatomical_masks: unknown parameters {sorted(unknown)}")
+    p.update(params)
+    nout = len(kinds)
+    if out is None:
+        out = torch.empty(N, nout, H, W, device=hu.device, dtype=torch.float32)
+    elif out.shape != (N, nout, H, W) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError("anatomical_masks: out must be a contiguous float32 [N, nout, H, W] tensor")
+    thr = (ctypes.c_float * 7)(p["lung_lower"], p["lung_upper"], p["vessel_lower"], p["vessel_upper"],
+                               p["mediastinum_lower"], p["mediastinum_upper"], p["bone_threshold"])
+    # spine_start = int(height * (1 - spine_margin_ratio))  (mask_generator.py:212)
+    ip = (ctypes.c_int32 * 3)(int(p["min_size"]), int(p["border_margin"]),
+                              int(H * (1 - p["spine_margin_ratio"])))
+    ch = (ctypes.c_int32 * 4)(*[kinds.index(k) if k in kinds else -1 for k in MASK_KINDS])
+    nb = lib.query("dcs_masks_workspace_size", N, H, W)
+    ws = workspace(nb, hu.device)
+    lib.call("dcs_anatomical_masks", _p(hu), N, H, W, thr, ip, ch, nout, _p(out), _p(ws), ws.numel(), _stream())
+    return out

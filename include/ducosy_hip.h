@@ -193,6 +193,33 @@ int dcs_loss_ssim(const float* X, const float* Y, int N, int H, int W, float dat
 int dcs_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                   float beta2, float eps, float bias_c1, float bias_c2, void* stream);
 
+/* ---- input pipeline (modules/preprocess.py:6-55, modules/mask_generator.py:11-347, as used by
+ *      modules/dataset.py:109-181 for every training slice) ---- */
+
+/* HU transform of N stored-pixel slices [N][H][W]: hu = f32(raw)*slope[n] + intercept[n]
+ * (preprocess.py:45-46); img = [-1,1] image of clip(hu, hu_min, hu_max), soft-squeezed
+ * (apply_soft_squeezing, preprocess.py:6-40, k = 10/sigma, threshold 0.9) when soft != 0, else
+ * linear (preprocess.py:53).  raw_dtype: 0 int16, 1 uint16, 2 float32.  slope/intercept are
+ * device arrays [N].  hu or img may be NULL (not written).  float32 op order as numpy. */
+int dcs_hu_transform(const void* raw, int raw_dtype, const float* slope, const float* intercept, int N,
+                     int H, int W, float hu_min, float hu_max, int soft, float sigma, float* hu,
+                     float* img, void* stream);
+
+/* Anatomical masks of N HU slices [N][H][W] (generate_anatomical_masks, 2-D path per slice):
+ * lung (detect_lung), mediastinum (detect_mediastinum), bone (detect_bone), lung_vessel
+ * (detect_lung_vessels).  Host arrays:
+ *   thresholds[7] = {lung_lower, lung_upper, vessel_lower, vessel_upper, mediastinum_lower,
+ *                    mediastinum_upper, bone_threshold}        (reference defaults -1000, -300,
+ *                    -300, 600, -300, 450, 200)
+ *   iparams[3]    = {min_size, border_margin, spine_start}     (64, 32, int(H*(1-0.25)))
+ *   chan[4]       = output channel of {lung, mediastinum, bone, lung_vessel}, -1 = not wanted
+ * out: float32 [N][nout][H][W] in {0,1} (the channel concat of dataset.py:135-158).
+ * ws: dcs_masks_workspace_size(N, H, W) bytes.  Bit-exact with the reference. */
+size_t dcs_masks_workspace_size(int N, int H, int W);
+int dcs_anatomical_masks(const float* hu, int N, int H, int W, const float* thresholds,
+                         const int32_t* iparams, const int32_t* chan, int nout, float* out, void* ws,
+                         size_t ws_bytes, void* stream);
+
 /* small utilities */
 int dcs_scale_add(float* y, const float* x, float a, int64_t n, void* stream); /* y += a*x */
 /* out = x * (*s) with s a device scalar (loss backward without a host sync) */
