@@ -150,8 +150,9 @@ struct MaskArgs {
 
 // detect_lung thresholds (mask_generator.py:14-29) and the bone candidates (:179-183);
 // per-slice body pixel count (body = hu > -1000).
-__global__ __launch_bounds__(MT) void mask_seed_kernel(const float* __restrict__ hu, MaskArgs a, uint8_t* __restrict__ F,
-                                                       uint8_t* __restrict__ M, SliceInfo* si) {
+__global__ __launch_bounds__(MT) void mask_seed_kernel(const float* __restrict__ hu, const uint8_t* __restrict__ lung_in,
+                                                       MaskArgs a, uint8_t* __restrict__ F, uint8_t* __restrict__ M,
+                                                       SliceInfo* si) {
     const int n = blockIdx.y, HW = a.H * a.W;
     const int p = blockIdx.x * MT + threadIdx.x;
     int body = 0;
@@ -161,7 +162,8 @@ __global__ __launch_bounds__(MT) void mask_seed_kernel(const float* __restrict__
         const float v = hu[i];
         body = v > -1000.f;
         const bool inner = y >= a.border && y < a.H - a.border && x >= a.border && x < a.W - a.border;
-        const bool lc = body && v >= a.lung_lower && v <= a.lung_upper && inner;
+        // a caller-supplied lung mask (detect_mediastinum(hu, lung_mask) etc.) replaces detect_lung
+        const bool lc = lung_in ? lung_in[i] != 0 : body && v >= a.lung_lower && v <= a.lung_upper && inner;
         const bool ab = body && v >= a.bone_thr;
         F[i] = (lc ? F_LUNGC : 0) | (ab ? F_ABONE : 0);
         M[i] = lc;
@@ -455,7 +457,7 @@ extern "C" size_t dcs_masks_workspace_size(int N, int H, int W) {
     return carve(nullptr, N, H, W).bytes;
 }
 
-extern "C" int dcs_anatomical_masks(const float* hu, int N, int H, int W, const float* thresholds,
+extern "C" int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int N, int H, int W, const float* thresholds,
                                     const int32_t* iparams, const int32_t* chan, int nout, float* out, void* ws,
                                     size_t ws_bytes, void* stream) {
     if (!hu || !thresholds || !iparams || !chan || !out || !ws || N <= 0 || H < 1 || W < 1 || nout < 1 || nout > 4)
@@ -473,7 +475,7 @@ extern "C" int dcs_anatomical_masks(const float* hu, int N, int H, int W, const 
     a.vessel_lower = thresholds[2]; a.vessel_upper = thresholds[3];
     a.medi_lower = thresholds[4]; a.medi_upper = thresholds[5];
     a.bone_thr = thresholds[6];
-    a.min_size = iparams[0]; a.border = iparams[1]; a.spine_start = iparams[2];
+    a.min_size = lung_in ? 0 : iparams[0]; a.border = iparams[1]; a.spine_start = iparams[2];
     const int4 ch = make_int4(chan[0], chan[1], chan[2], chan[3]);
     const bool want_medi = ch.y >= 0, want_bone = ch.z >= 0, want_ves = ch.w >= 0;
 
@@ -487,7 +489,7 @@ extern "C" int dcs_anatomical_masks(const float* hu, int N, int H, int W, const 
         return fail(DCS_E_INVALID, "anatomical_masks: memset failed");
     hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)cdiv(N * H, MT)), dim3(MT), 0, s, w.rowmin, W, N * H);
     hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)cdiv(N * H, MT)), dim3(MT), 0, s, w.rowmax, -1, N * H);
-    hipLaunchKernelGGL(mask_seed_kernel, gs, dim3(MT), 0, s, hu, a, w.F, w.M, w.si);
+    hipLaunchKernelGGL(mask_seed_kernel, gs, dim3(MT), 0, s, hu, lung_in, a, w.F, w.M, w.si);
     if ((e = check_launch("masks: seed"))) return e;
     // detect_lung: components of the lung candidates, size filter, gate and hull
     if ((e = run_cc(w, H, W, np, true, s))) return e;

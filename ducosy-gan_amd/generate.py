@@ -8,10 +8,11 @@ Differences from the reference, all deliberate:
     (modules/inference.py) instead of one slice per call;
   * the Generators are built with the input channel count found in the checkpoint
     (generate.py:29-30 hard-codes 1, which cannot load the mask-conditioned cin 3 / cin 2
-    checkpoints that train.py writes); for mask-conditioned checkpoints the mask channels
-    are zero (no mask generator on this path);
+    checkpoints that train.py writes); a mask-conditioned Generator gets the anatomical masks
+    of the NCCT slice in its training order (soft tissue: bone, mediastinum; lung: lung;
+    modules/argmanager.py) from the GPU mask kernel, as the training data pipeline built them;
   * checkpoints are read with torch.load(weights_only=True).
-DICOM reading/writing uses pydicom, imported here only.
+DICOM reading/writing uses modules/dicom.py (pydicom is not installed in this image).
 """
 import argparse
 import glob
@@ -42,27 +43,33 @@ def load_generator(path, device, num_residual_blocks=9):
     return g.to(device).eval()
 
 
-class _MaskPad(torch.nn.Module):
-    """Feeds an image-only batch to a mask-conditioned Generator with zero mask channels."""
+MASK_TYPES = {"soft_tissue": ["bone", "mediastinum"], "lung": ["lung"]}  # argmanager.py:132, 149
 
-    def __init__(self, g):
-        super().__init__()
-        self.g = g
 
-    def forward(self, x):
-        extra = self.g.input_channels - x.shape[1]
-        if extra <= 0:
-            return self.g(x)
-        return self.g(x, torch.zeros(x.shape[0], extra, *x.shape[2:], device=x.device, dtype=x.dtype))
+def _conditioning(g, kind, hu_slices, device):
+    """Per-slice mask channels for a mask-conditioned Generator (None for an image-only one):
+    the training mask types when their count matches the checkpoint, else zero planes."""
+    extra = g.input_channels - 1
+    if extra <= 0:
+        return None
+    types = MASK_TYPES[kind]
+    if len(types) != extra:
+        return [np.zeros((extra,) + h.shape, np.float32) for h in hu_slices]
+    from modules.hip import ops
+    out = []
+    for h in hu_slices:
+        m = ops.anatomical_masks(torch.from_numpy(np.ascontiguousarray(h, np.float32)).to(device), types)
+        out.append(m[0].cpu().numpy())
+    return out
 
 
 def generate(args):
     """generate.py:21-137: per patient, translate every NCCT slice with both models and write
     raw / soft_tissue / lung DICOM copies under working_dir_root."""
-    import pydicom
+    from modules import dicom
     device = torch.device(f"cuda:{args.gpu_id}")
-    soft = _MaskPad(load_generator(args.model_path_soft, device))
-    lung = _MaskPad(load_generator(args.model_path_lung, device))
+    soft = load_generator(args.model_path_soft, device)
+    lung = load_generator(args.model_path_lung, device)
     for dataset_name in args.dataset_names:
         input_dir = os.path.join(args.input_dir_root, dataset_name)
         working_dir = os.path.join(args.working_dir_root, dataset_name)
@@ -75,13 +82,14 @@ def generate(args):
             for d in out_dirs.values():
                 os.makedirs(d, exist_ok=True)
             paths = sorted(glob.glob(os.path.join(ncct, "*.dcm")))
-            dcms = [pydicom.dcmread(p) for p in paths]
+            dcms = [dicom.dcmread(p) for p in paths]
             hu = [hu_from_stored(d.pixel_array, d.RescaleSlope, d.RescaleIntercept) for d in dcms]
             outs = {}
             for name, model, lo, hi in (("soft_tissue", soft, args.soft_hu_min, args.soft_hu_max),
                                         ("lung", lung, args.lung_hu_min, args.lung_hu_max)):
                 outs[name] = (translate_slices(model, [normalise_hu(h, lo, hi) for h in hu], args.img_size,
-                                               args.slice_batch, device), lo, hi)
+                                               args.slice_batch, device, _conditioning(model, name, hu, device)),
+                              lo, hi)
             for i, (p, d) in enumerate(zip(paths, dcms)):
                 try:
                     shutil.copy(p, os.path.join(out_dirs["raw"], os.path.basename(p)))
@@ -90,7 +98,7 @@ def generate(args):
                                                 d.pixel_array.dtype)
                         o = deepcopy(d)
                         o.SeriesDescription = f"Synthetic CECT (from {d.get('SeriesDescription', '')})"
-                        o.file_meta.TransferSyntaxUID = pydicom.uid.ExplicitVRLittleEndian
+                        o.file_meta.TransferSyntaxUID = dicom.EXPLICIT_VR_LE
                         o.SmallestImagePixelValue, o.LargestImagePixelValue = int(px.min()), int(px.max())
                         o.PixelData = px.tobytes()
                         o.save_as(os.path.join(out_dirs[name], os.path.basename(p)))
@@ -103,7 +111,7 @@ def generate(args):
 def synthesis(args):
     """generate.py:140-297: merge the two translations inside their HU ranges over the NCCT,
     z-smooth the volume and write output/{dataset}/{patient}/{idx:04d}.dcm."""
-    import pydicom
+    from modules import dicom
     for dataset_name in args.dataset_names:
         working_dir = os.path.join(args.working_dir_root, dataset_name)
         output_dir = os.path.join(args.output_dir_root, dataset_name)
@@ -114,7 +122,7 @@ def synthesis(args):
                 continue
             merged = []
             for rp, sp, lp in zip(*lists):
-                raw, st, lg = pydicom.dcmread(rp), pydicom.dcmread(sp), pydicom.dcmread(lp)
+                raw, st, lg = dicom.dcmread(rp), dicom.dcmread(sp), dicom.dcmread(lp)
                 raw_hu = hu_from_stored(raw.pixel_array, getattr(raw, "RescaleSlope", 1),
                                         getattr(raw, "RescaleIntercept", 0))
                 merged.append(synthesize(raw.pixel_array, raw_hu, st.pixel_array, lg.pixel_array,
@@ -123,7 +131,7 @@ def synthesis(args):
             out_base = os.path.join(output_dir, os.path.basename(patient_dir))
             os.makedirs(out_base, exist_ok=True)
             for idx, sp in enumerate(lists[1]):
-                o = pydicom.dcmread(sp)
+                o = dicom.dcmread(sp)
                 px = vol[idx]
                 o.PixelData = px.tobytes()
                 vr = "US" if o.PixelRepresentation == 0 else "SS"

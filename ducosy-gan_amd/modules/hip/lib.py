@@ -79,7 +79,7 @@ SIGNATURES = {
     "dcs_hu_transform": (c_int, [P, c_int, P, P, c_int, c_int, c_int, c_float, c_float, c_int, c_float,
                                  P, P, P]),
     "dcs_masks_workspace_size": (c_size_t, [c_int, c_int, c_int]),
-    "dcs_anatomical_masks": (c_int, [P, c_int, c_int, c_int, P, P, P, c_int, P, P, c_size_t, P]),
+    "dcs_anatomical_masks": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_int, P, P, c_size_t, P]),
 }
 
 

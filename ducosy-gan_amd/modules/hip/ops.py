@@ -572,10 +572,13 @@ def hu_transform(raw: torch.Tensor, slope: torch.Tensor, intercept: torch.Tensor
     return hu, img
 
 
-def anatomical_masks(hu: torch.Tensor, mask_types=MASK_KINDS, out: Optional[torch.Tensor] = None, **params):
+def anatomical_masks(hu: torch.Tensor, mask_types=MASK_KINDS, out: Optional[torch.Tensor] = None,
+                     lung_mask: Optional[torch.Tensor] = None, **params):
     """HU slices [N,H,W] float32 -> float32 masks [N, len(mask_types), H, W] in mask_types order
-    (generate_anatomical_masks per 2-D slice + the channel concat of dataset.py:135-158)."""
-    _check_dev(hu)
+    (generate_anatomical_masks per 2-D slice + the channel concat of dataset.py:135-158).
+    lung_mask (optional, binary [N,H,W]) replaces detect_lung, as the lung_mask argument of
+    detect_mediastinum / detect_bone / detect_lung_vessels."""
+    _check_dev(hu, lung_mask)
     if hu.dtype != torch.float32:
         raise RuntimeError("anatomical_masks: HU must be float32")
     if hu.dim() == 2:
@@ -601,7 +604,11 @@ def anatomical_masks(hu: torch.Tensor, mask_types=MASK_KINDS, out: Optional[torc
     ip = (ctypes.c_int32 * 3)(int(p["min_size"]), int(p["border_margin"]),
                               int(H * (1 - p["spine_margin_ratio"])))
     ch = (ctypes.c_int32 * 4)(*[kinds.index(k) if k in kinds else -1 for k in MASK_KINDS])
+    lung_in = None
+    if lung_mask is not None:
+        lung_in = (lung_mask.reshape(N, H, W) != 0).to(torch.uint8).contiguous()
     nb = lib.query("dcs_masks_workspace_size", N, H, W)
     ws = workspace(nb, hu.device)
-    lib.call("dcs_anatomical_masks", _p(hu), N, H, W, thr, ip, ch, nout, _p(out), _p(ws), ws.numel(), _stream())
+    lib.call("dcs_anatomical_masks", _p(hu), _p(lung_in), N, H, W, thr, ip, ch, nout, _p(out), _p(ws), ws.numel(),
+             _stream())
     return out

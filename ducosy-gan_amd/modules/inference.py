@@ -9,7 +9,7 @@ without it.
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Sequence, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -45,16 +45,22 @@ def resize(x: torch.Tensor, size: Tuple[int, int]) -> torch.Tensor:
 
 @torch.no_grad()
 def translate_slices(model, slices: Sequence[np.ndarray], img_size: int, batch: int = 16,
-                     device="cuda") -> List[np.ndarray]:
+                     device="cuda", cond: Optional[Sequence[np.ndarray]] = None) -> List[np.ndarray]:
     """Run the Generator over normalised slices ([H,W] float32 each, any size) in batches of
     `batch` at img_size x img_size, and resize each output back to its slice's size
-    (generate.py:104-116).  Returns [H,W] float32 arrays in [-1, 1]."""
+    (generate.py:104-116).  ``cond``: per-slice mask channels [m,H,W] for a mask-conditioned
+    Generator (resized nearest, concatenated after the image as in trainer.py:451-453).
+    Returns [H,W] float32 arrays in [-1, 1]."""
     out: List[np.ndarray] = []
     for i in range(0, len(slices), batch):
         chunk = slices[i:i + batch]
         x = torch.stack([resize(torch.from_numpy(np.ascontiguousarray(s))[None, None], (img_size, img_size))[0]
                          for s in chunk]).to(device)
-        y = model(x)
+        if cond is not None:
+            m = torch.stack([F.interpolate(torch.as_tensor(np.ascontiguousarray(c))[None].float(),
+                                           size=(img_size, img_size), mode="nearest")[0]
+                             for c in cond[i:i + batch]]).to(device)
+        y = model(x) if cond is None else model(x, m)  # concat fused into the stem gather
         for s, yi in zip(chunk, y):
             out.append(resize(yi[None], tuple(s.shape))[0, 0].float().cpu().numpy())
     return out

@@ -160,8 +160,9 @@ class CycleGANSystem:
 
 
 # -------------------------------------------------------------------------------------------
-# data: DICOM loading/mask generation is outside the hot path; the
-# default source is synthetic slices of the reference's shapes.
+# data: a DICOM tree (modules/dataset.py: decode on the loader workers, HU transform + masks on
+# the GPU) when data_root/dataset_names exists, synthetic slices of the reference's shapes
+# otherwise (or with --synthetic).
 # -------------------------------------------------------------------------------------------
 class SyntheticSlices(torch.utils.data.Dataset):
     """Deterministic synthetic slices: A, B ~ U(-1,1) [1,H,W], masks ~ Bernoulli(0.3)."""
@@ -181,14 +182,18 @@ class SyntheticSlices(torch.utils.data.Dataset):
         return out
 
 
-def _to_dev(batch, device):
+def _to_dev(batch, device, prep=None):
+    """Batch -> (real_A, real_B, masks) on the device; decoded DICOM batches go through the
+    GPU preprocessor (HU transform + masks, modules/dataset.py)."""
+    if prep is not None and (isinstance(batch, list) or "A_raw" in batch):
+        batch = prep(batch)
     real_A = batch["A"].to(device, non_blocking=True)
     real_B = batch["B"].to(device, non_blocking=True)
     masks = batch["masks"].to(device, non_blocking=True) if "masks" in batch else None
     return real_A, real_B, masks
 
 
-def validate_and_save_images(epoch, system, val_loader, args, device, fixed_val_batch):
+def validate_and_save_images(epoch, system, val_loader, args, device, fixed_val_batch, prep=None):
     """trainer.py:187-294: mean validation G loss over the (rank-sharded) validation set and an
     [NCCT | fake CECT | CECT] windowed image grid of a fixed batch (rank 0)."""
     for m in system.models:
@@ -196,7 +201,7 @@ def validate_and_save_images(epoch, system, val_loader, args, device, fixed_val_
     total = torch.zeros((), device=device)
     count = 0
     for batch in val_loader:
-        real_A, real_B, masks = _to_dev(batch, device)
+        real_A, real_B, masks = _to_dev(batch, device, prep)
         total += system.validation_loss(real_A, real_B, masks)
         count += 1
     stats = torch.stack([total, torch.tensor(float(count), device=device)])
@@ -206,7 +211,7 @@ def validate_and_save_images(epoch, system, val_loader, args, device, fixed_val_
     if parallel.rank() == 0 and fixed_val_batch is not None:
         try:
             with torch.no_grad():
-                real_A, real_B, masks = _to_dev(fixed_val_batch, device)
+                real_A, real_B, masks = _to_dev(fixed_val_batch, device, prep)
                 fake_B = system.G_A2B(real_A, masks)
                 grid = torch.cat((apply_windowing(real_A, args), apply_windowing(fake_B, args),
                                   apply_windowing(real_B, args)), -1)
@@ -237,10 +242,7 @@ def _build_datasets(args, n_masks):
     if not getattr(args, "synthetic", False):
         root = os.path.join(args.data_root, args.dataset_names)
         if os.path.isdir(root):
-            try:
-                from .dataset import DicomDataset  # noqa: F401  (DICOM I/O: outside the hot path)
-            except ImportError as e:
-                raise RuntimeError("DICOM input needs modules/dataset.py (pydicom); run with --synthetic") from e
+            from .dataset import DicomDataset
             dirs = sorted(glob.glob(os.path.join(root, "*")))
             random.seed(42)
             random.shuffle(dirs)
@@ -298,11 +300,15 @@ def train_cycle_gan(args, target_range):
     tsampler = torch.utils.data.DistributedSampler(train_ds, world, rank, shuffle=True) if world > 1 else None
     vsampler = torch.utils.data.DistributedSampler(val_ds, world, rank, shuffle=False) if world > 1 else None
     nw = min(int(getattr(args, "num_workers", 0)), 16)
+    prep, collate_fn = None, None
+    if not isinstance(train_ds, SyntheticSlices):
+        from .dataset import SliceBatchPreprocessor, collate
+        prep, collate_fn = SliceBatchPreprocessor(args, device), collate
     dl = torch.utils.data.DataLoader(train_ds, batch_size=per_rank, shuffle=tsampler is None, sampler=tsampler,
                                      num_workers=nw, pin_memory=True, drop_last=True,
-                                     persistent_workers=nw > 0)
+                                     persistent_workers=nw > 0, collate_fn=collate_fn)
     vdl = torch.utils.data.DataLoader(val_ds, batch_size=per_rank * 2, shuffle=False, sampler=vsampler,
-                                      num_workers=nw, pin_memory=True)
+                                      num_workers=nw, pin_memory=True, collate_fn=collate_fn)
     fixed_val_batch = next(iter(vdl))
     if rank == 0:
         print(f"Train/Val split: {len(train_ds)} slices / {len(val_ds)} slices")
@@ -314,7 +320,7 @@ def train_cycle_gan(args, target_range):
         system.train()
         t0 = time.time()
         for i, batch in enumerate(dl):
-            real_A, real_B, masks = _to_dev(batch, device)
+            real_A, real_B, masks = _to_dev(batch, device, prep)
             losses = system.train_step(real_A, real_B, masks)
             if rank == 0 and (i % max(int(getattr(args, "log_every", 10)), 1) == 0):
                 print(f"Epoch {epoch + 1}/{args.epochs} step {i}: G_loss {float(losses['loss_G']):.4f} "
@@ -326,7 +332,7 @@ def train_cycle_gan(args, target_range):
         for s in schedulers:
             s.step()
         torch.cuda.synchronize()
-        val_loss = validate_and_save_images(epoch, system, vdl, args, device, fixed_val_batch)
+        val_loss = validate_and_save_images(epoch, system, vdl, args, device, fixed_val_batch, prep)
         if rank == 0:
             print(f"\nEpoch {epoch + 1} finished in {time.time() - t0:.1f}s. Validation Generator Loss: {val_loss:.4f}")
             _save_epoch(system, schedulers, args, saved_models_dir, epoch, val_loss, best_val_loss, best_epoch)
