@@ -30,6 +30,12 @@ sys.path.insert(0, os.path.join(ROOT, "ducosy-gan_amd"))
 import torch  # noqa: E402
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 16 * F32_MFMA_PEAK_TFLOPS  # v_mfma_f32_32x32x16_bf16: 16x the f32 rate (~2.5 PF dense)
+# peak per mode for the dominant kernel's algorithmic FLOPs: bf16x3 issues 3 bf16 MFMAs per product
+MODE_PEAK = {"f32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+MODE_DTYPE = {"f32": "f32", "bf16": "bf16 (MFMA operands; f32 accumulation and storage)",
+              "bf16x3": "f32 via bf16x3 MFMA (hi/lo split, ~2^-16 per product; f32 accumulation and storage)"}
+MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -83,12 +89,16 @@ def main():
     ap.add_argument("--blocks", type=int, default=9)
     ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mma", default="f32", choices=["f32", "bf16", "bf16x3"],
+                    help="MFMA operand mode of the conv passes: f32 = exact fp32 (the headline), "
+                         "bf16 = BASELINE config 5's half-precision MFMA path, bf16x3 = split hi/lo bf16")
     args = ap.parse_args()
 
     from modules import parallel
     from modules.hip import ops
     from modules.trainer import CycleGANSystem
 
+    ops.set_mma(args.mma)
     rank, world, local = parallel.init_from_env()
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
@@ -131,7 +141,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {
                 "workload": "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
@@ -140,13 +150,13 @@ def main():
                 "residual_blocks": args.blocks, "input_channels": args.cin, "parallelism": f"dp{world}",
             },
             "roofline": {
-                "kernel": "conv_rows_kernel<128,128,1,1> (256-ch 3x3 residual conv, fwd+dgrad)",
+                "kernel": f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)",
                 "bound": "mfma",
                 "achieved": round(achieved, 3),
-                "peak": F32_MFMA_PEAK_TFLOPS,
+                "peak": round(MODE_PEAK[args.mma], 1),
                 "unit": "TFLOP/s",
-                "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": _pmc_traffic(),
+                "frac": round(achieved / MODE_PEAK[args.mma], 4),
+                "traffic": _pmc_traffic() if args.mma == "f32" else None,
                 "launches": n_launch,
                 "ms_per_launch": round(ms_launch, 4),
                 "gflop_per_launch": round(flop_launch / 1e9, 3),

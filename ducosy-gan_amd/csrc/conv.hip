@@ -22,6 +22,42 @@
 namespace dcs {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// MFMA operand modes (dcs_conv_desc.mma): exact f32 (v_mfma_f32_32x32x2_f32), bf16 operands
+// (v_mfma_f32_32x32x16_bf16, f32 accumulation: BASELINE config 5's half-precision MFMA path),
+// and bf16x3 (each f32 operand split into hi + lo bf16, three MFMAs hi*hi + hi*lo + lo*hi:
+// ~2^-16 relative per product instead of 2^-24, at 3/16 of the f32-MFMA cycles per FLOP).
+constexpr int MMA_F32 = 0, MMA_BF16 = 1, MMA_BF16X3 = 3;
+#ifndef DCS_BF16_BUFGATHER
+#define DCS_BF16_BUFGATHER 1  // branch-free buffer-descriptor gather in the bf16 rows pass
+#endif
+
+// bf16 LDS rows of the rows pass: 32 k of hi (+ 32 k of lo for bf16x3) + 8 pad elements;
+// 80-B / 144-B pitches keep the per-lane 16-B fragment reads conflict-free.
+template <int MMA>
+constexpr int lde_bf16() { return MMA == MMA_BF16X3 ? 72 : 40; }
+
+// split 8 floats into hi (round-to-nearest bf16, one v_cvt_pk_bf16_f32 per pair) and, for
+// bf16x3, lo = bf16(v - hi) with hi re-expanded by bit shifts (bf16 -> f32 is exact)
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <int MMA>
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
+    const floatx8 f = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    hi = __builtin_convertvector(f, bf16x8);
+    if constexpr (MMA == MMA_BF16X3) {
+        u32x4v w;
+        __builtin_memcpy(&w, &hi, 16);
+        floatx8 r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            r[2 * q] = f[2 * q] - __uint_as_float(w[q] << 16);
+            r[2 * q + 1] = f[2 * q + 1] - __uint_as_float(w[q] & 0xffff0000u);
+        }
+        lo = __builtin_convertvector(r, bf16x8);
+    }
+}
 
 constexpr int BK = 32;
 constexpr int NT = 256;
@@ -99,6 +135,14 @@ constexpr int OOB_OFF = 0x7fffffff - 64;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const float* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffff00, 0x00020000);
+}
+
+__device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+    float2 f;
+    __builtin_memcpy(&f, &v, 8);
+    return f;
 }
 
 __device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int byte_off) {
@@ -371,7 +415,7 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
 
 // VEC: 0 scalar gather (any layout), 1 = 16 consecutive k of one tap per thread (Cs % 16 == 0),
 //      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
-template <int BM, int BN, int VEC, int TAG>
+template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
 __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
@@ -381,12 +425,23 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     constexpr int WM = BM / 2, WN = BN / 2;        // per-wave tile
     constexpr int IM = WM / 32, JN = WN / 32;      // 32x32 blocks per wave
     constexpr int BTPR = NT / BN;                  // B loader threads per row (2 or 4)
-    constexpr int BKPT = BK / BTPR;                // k per B-loader thread (16 or 8)
+    // bf16: 64-deep k-tiles (twice the MFMA work per round of global loads: the bf16 passes are
+    // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
+    constexpr int BKT = BK;
+    constexpr int AKPT = BKT / 2;                  // k per A-loader thread (2 threads per row)
+    constexpr int ACH = AKPT / 4;                  // float4 per A-loader thread
+    constexpr int BKPT = BKT / BTPR;               // k per B-loader thread
     constexpr int BCH = BKPT / 4;                  // float4 per B-loader thread
     constexpr int KT2 = 4;                         // k-tiles per inner accumulation chain
+    constexpr int LDE = MMA == MMA_BF16X3 ? 72 : BKT + 8;  // bf16 elements per LDS row (bf16 modes)
+    constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK : (BM + BN) * LDE;
 
-    __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
+    // f32: As[2][BM][LDK] | Bs[2][BN][LDK];  bf16 modes: Ah[2][BM][LDE] | Bh[2][BN][LDE]
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    auto As = reinterpret_cast<float (*)[BM][LDK]>(lds);
+    auto Bs = reinterpret_cast<float (*)[BN][LDK]>(lds + 2 * BM * LDK);
+    __bf16* const Ah = reinterpret_cast<__bf16*>(lds);
+    __bf16* const Bh = Ah + 2 * BM * LDE;
     __shared__ long long rowoff[BM];
 
     const int T = gridDim.x;
@@ -405,7 +460,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const int wm = wid >> 1, wn = wid & 1;
 
     // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap)
-    const int arow = tid >> 1, akq = (tid & 1) * 16;
+    const int arow = tid >> 1, akq = (tid & 1) * AKPT;
     const RowInfo ri = row_info(d, g, (int)(m0 + arow));
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     const bool rvalid = ri.out_off >= 0;
@@ -414,20 +469,21 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
     const int K = g.ntaps * d.Cs;
-    const int nkt = (K + BK - 1) / BK;
+    const int nkt = (K + BKT - 1) / BKT;
     const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
     const float* srow = src + ri.n * d.s_n;
     const long long so = (long long)ri.n * d.Cs;
+    const __amdgpu_buffer_rsrc_t arsrc = src_rsrc(src);
 
     // incremental (tap, channel) state of the next k-tile to load, for A and B
     int aj = akq / d.Cs, ac = akq - (akq / d.Cs) * d.Cs;
     int bj = bkq / d.Cs, bc = bkq - (bkq / d.Cs) * d.Cs;
     auto advance = [&](int& j, int& c) {
-        c += BK;
+        c += BKT;
         while (c >= d.Cs) { c -= d.Cs; ++j; }
     };
 
-    float4 ra[4];
+    float4 ra[ACH];
     float4 rb[BCH];
 
     auto load_a = [&](int kt) {
@@ -448,10 +504,28 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
                 }
             }
             aj += BK / 4;
+        } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
+            // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
+            int sy = 0, sx = 0, off = OOB_OFF;
+            if (aj < g.ntaps) {
+                int ady, adx, bt;
+                tap_decode(d, g, aj, ady, adx, bt);
+                const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                if (rvalid && yok && xok) off = (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4;
+            }
+#pragma unroll
+            for (int i = 0; i < ACH; ++i) ra[i] = buf_load4(arsrc, off + 16 * i);
+            if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
+#pragma unroll
+                for (int i = 0; i < ACH; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
+            }
+            advance(aj, ac);
         } else if (VEC) {
             // (a buffer-descriptor variant of this gather, as in the wgrad pass, measured 3-7 %
             //  slower here: invalid taps would issue loads that the branch now skips)
-            ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int i = 0; i < ACH; ++i) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid && aj < g.ntaps) {
                 int ady, adx, bt;
                 tap_decode(d, g, aj, ady, adx, bt);
@@ -460,21 +534,21 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
                     map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx)) {
                     const float* sp = srow + sy * d.s_h + sx * d.s_w + ac;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
+                    for (int i = 0; i < ACH; ++i) ra[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
                     if (d.pro_act != DCS_ACT_NONE) {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
+                        for (int i = 0; i < ACH; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
                     }
                 }
             }
             advance(aj, ac);
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < ACH; ++i) {
                 float e[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    int k = kt * BK + akq + 4 * i + q;
+                    int k = kt * BKT + akq + 4 * i + q;
                     int j = k / d.Cs, c = k - j * d.Cs;
                     e[q] = 0.f;
                     if (rvalid && j < g.ntaps) {
@@ -491,7 +565,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
         long long col;
         bool ok = true;
         if (!d.parity) {
-            col = kt * BK + bkq;
+            col = kt * BKT + bkq;
         } else {  // the BKPT k of this thread share one tap (Cs % 16 == 0)
             ok = bj < g.ntaps;
             int ady, adx, bt = 0;
@@ -504,10 +578,28 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
             rb[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
     auto store_tiles = [&](int buf) {
+        if constexpr (MMA == MMA_F32) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = ra[i];
+            for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
+            for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
+        } else {
+            bf16x8 hi, lo;
+            __bf16* a = Ah + (buf * BM + arow) * LDE;
+#pragma unroll
+            for (int i = 0; i < ACH / 2; ++i) {
+                split8<MMA>(ra[2 * i], ra[2 * i + 1], hi, lo);
+                *reinterpret_cast<bf16x8*>(a + akq + 8 * i) = hi;
+                if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(a + 32 + akq + 8 * i) = lo;
+            }
+            __bf16* b = Bh + (buf * BN + brow) * LDE;
+#pragma unroll
+            for (int i = 0; i < BCH / 2; ++i) {
+                split8<MMA>(rb[2 * i], rb[2 * i + 1], hi, lo);
+                *reinterpret_cast<bf16x8*>(b + bkq + 8 * i) = hi;
+                if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(b + 32 + bkq + 8 * i) = lo;
+            }
+        }
     };
 
     floatx16 acc[IM][JN], t[IM][JN];
@@ -524,6 +616,59 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     __syncthreads();
 
     const int l32 = lane & 31, lk = (lane >> 5) * 16;
+    if constexpr (MMA != MMA_F32) {
+        // k-step s of a k-tile: lane (r, h) supplies A[row r][16s + 8h + 0..7] and
+        // B[16s + 8h + 0..7][col r] (v_mfma_f32_32x32x16_bf16 operand map)
+        constexpr int NST = BKT / 16;
+        const int kh = (lane >> 5) * 8;
+        for (int kt = 0; kt < nkt; ++kt) {
+            const int cur = kt & 1;
+            auto step = [&](int st) {
+                bf16x8 ah[IM], bh[JN], al[IM], bl[JN];
+#pragma unroll
+                for (int i = 0; i < IM; ++i) {
+                    const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
+                    ah[i] = *reinterpret_cast<const bf16x8*>(a);
+                    if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
+                }
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
+                    bh[j] = *reinterpret_cast<const bf16x8*>(b);
+                    if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
+                }
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        if constexpr (MMA == MMA_BF16X3) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                        } else {  // bf16: operand rounding dominates, one accumulation level
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                        }
+                    }
+            };
+#pragma unroll
+            for (int st = 0; st < NST / 2; ++st) step(st);
+            if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
+#pragma unroll
+            for (int st = NST / 2; st < NST; ++st) step(st);
+            if (MMA == MMA_BF16X3 && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        acc[i][j] += t[i][j];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
+            if (kt + 1 < nkt) store_tiles(cur ^ 1);
+            __syncthreads();
+        }
+    } else
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
         float4 af[IM][4], bf[JN][4];
@@ -835,6 +980,197 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// wgrad pass on the bf16 MFMA (dcs_conv_desc.mma = BF16 / BF16X3): regular rows (parity 0),
+// vectorisable sources (Cs % 16 == 0), 128 x 128 tiles.  dW[co][n] = sum_p dy[p][co] x[p][n]
+// with the pixels p as the GEMM reduction.  The bf16 MFMA wants each lane's fragment to be 8
+// consecutive k (here: pixels) of one row, so LDS keeps both operands row-major with the
+// pixels contiguous ([row][32 px (+32 lo) + pad]) and every fragment is one ds_read_b128.
+// Loader: thread (pair q = tid & 63, group g = tid >> 6) reads rows 2q and 2q+1 (one float2)
+// at the 8 consecutive pixels 8g .. 8g+7 of the k-tile and writes them as two bf16x8 rows:
+// no transpose.  The pixel walk is wave-uniform (g is the wave index).
+// ---------------------------------------------------------------------------------------
+template <int MMA, bool UNI>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_mma16_kernel(
+    const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
+    const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws,
+    int kt_per_split, int gn, int gm) {
+    constexpr int BM = 128, BN = 128, WM = 64, WN = 64, IM = 2, JN = 2, KT2 = 4;
+    constexpr int LDE = lde_bf16<MMA>();
+    __shared__ __attribute__((aligned(16))) __bf16 Ah[2][BM][LDE];
+    __shared__ __attribute__((aligned(16))) __bf16 Bh[2][BN][LDE];
+    const dcs_conv_desc d = din;
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = L % gn;
+    const int mtile = (L / gn) % gm;
+    const int split = L / (gn * gm);
+    const int My = d.Ho, Mx = d.Wo, per = My * Mx;
+    const long long P = (long long)per * d.N;
+    const int Ktot = d.KH * d.KW * d.Cs;
+    const int m0 = mtile * BM, n0 = ntile * BN;
+    const long long nkt_all = (P + BK - 1) / BK;
+    const long long kt_beg = (long long)split * kt_per_split;
+    long long kt_end = kt_beg + kt_per_split;
+    if (kt_end > nkt_all) kt_end = nkt_all;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int q = lane;                                          // row pair
+    const int grp = __builtin_amdgcn_readfirstlane(wid);         // pixel group (wave-uniform)
+    const int am = m0 + 2 * q;                                   // dy channels am, am+1
+    const bool a_ok = am < d.Co;                                 // Co % 4 == 0: both or none
+    const int bn = n0 + 2 * q;                                   // columns bn, bn+1 (same tap)
+    const bool b_ok = bn < Ktot;
+    // UNI (Cs % 128 == 0): the tile's 128 columns share one tap, so the tap and the whole
+    // pixel -> source-coordinate walk below are wave-uniform (scalar); the lane only adds its
+    // channel offset.  Otherwise each lane decodes its own tap.
+    int ady = 0, adx = 0, bchan = 0;
+    if (UNI) {
+        const int j = n0 / d.Cs;
+        bchan = n0 - j * d.Cs + 2 * q;
+        ady = j / d.KW;
+        adx = j - ady * d.KW;
+    } else if (b_ok) {
+        const int j = bn / d.Cs;
+        bchan = bn - j * d.Cs;
+        ady = j / d.KW;
+        adx = j - ady * d.KW;
+    }
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+
+    // wave-uniform pixel state of this wave's first pixel in the NEXT k-tile to load
+    int pn = 0, pqy = 0, pqx = 0;
+    {
+        const long long p = kt_beg * BK + 8 * grp;
+        if (p < P) {
+            pn = (int)(p / per);
+            const int rem = (int)(p - (long long)pn * per);
+            pqy = rem / Mx;
+            pqx = rem - pqy * Mx;
+        }
+    }
+    float2 ra[8], rb[8];
+    // branch-free loads through buffer descriptors (OOB offset -> zeros); the host keeps dy and
+    // the source below 2 GiB
+    const __amdgpu_buffer_rsrc_t rdy = src_rsrc(dy), rsrc = src_rsrc(src);
+    auto load = [&](long long kt) {
+        const long long p0 = kt * BK + 8 * grp;
+        int n = pn, qy = pqy, qx = pqx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool pok = p0 + j < P;
+            ra[j] = buf_load2(rdy, (pok && a_ok) ? (int)(((p0 + j) * d.Co + am) * 4) : OOB_OFF);
+            int sy, sx;
+            const bool yok = map_coord_sel(qy * d.stride - d.pt + ady, Hv, d.up, d.pad_mode, sy);
+            const bool xok = map_coord_sel(qx * d.stride - d.pl + adx, Wv, d.up, d.pad_mode, sx);
+            const int base = n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w;
+            const int so = UNI ? __builtin_amdgcn_readfirstlane(base) : base;
+            const bool ok = pok && b_ok && yok && xok;
+            float2 v = buf_load2(rsrc, ok ? (so + bchan) * 4 : OOB_OFF);
+            if (d.pro_act != DCS_ACT_NONE && ok) {
+                const long long o = (long long)n * d.Cs + bchan;
+                v.x = act_apply(fmaf(v.x, psc[o], psh[o]), d.pro_act);
+                v.y = act_apply(fmaf(v.y, psc[o + 1], psh[o + 1]), d.pro_act);
+            }
+            rb[j] = v;
+            if (++qx == Mx) { qx = 0; if (++qy == My) { qy = 0; ++n; } }
+        }
+        // advance the wave's start by one k-tile (32 pixels)
+        pqx += BK;
+        while (pqx >= Mx) { pqx -= Mx; if (++pqy == My) { pqy = 0; ++pn; } }
+    };
+    // two rows (x, y halves of the float2s) of 8 pixels -> bf16 hi (+ lo) rows
+    auto put2 = [&](const float2 (&r)[8], __bf16 (*T)[LDE], int row) {
+        const float4 x0 = make_float4(r[0].x, r[1].x, r[2].x, r[3].x), x1 = make_float4(r[4].x, r[5].x, r[6].x, r[7].x);
+        const float4 y0 = make_float4(r[0].y, r[1].y, r[2].y, r[3].y), y1 = make_float4(r[4].y, r[5].y, r[6].y, r[7].y);
+        bf16x8 h, l;
+        split8<MMA>(x0, x1, h, l);
+        *reinterpret_cast<bf16x8*>(&T[row][8 * grp]) = h;
+        if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(&T[row][32 + 8 * grp]) = l;
+        split8<MMA>(y0, y1, h, l);
+        *reinterpret_cast<bf16x8*>(&T[row + 1][8 * grp]) = h;
+        if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(&T[row + 1][32 + 8 * grp]) = l;
+    };
+    auto store = [&](int buf) {
+        put2(ra, Ah[buf], 2 * q);
+        put2(rb, Bh[buf], 2 * q);
+    };
+
+    floatx16 acc[IM][JN], t[IM][JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
+
+    if (kt_beg < kt_end) {
+        load(kt_beg);
+        store(0);
+    }
+    __syncthreads();
+    const int l32 = lane & 31, kh = (lane >> 5) * 8;
+    for (long long kt = kt_beg; kt < kt_end; ++kt) {
+        const int cur = (int)((kt - kt_beg) & 1);
+        auto step = [&](int st) {
+            bf16x8 ah[IM], bh[JN], al[IM], bl[JN];
+#pragma unroll
+            for (int i = 0; i < IM; ++i) {
+                const __bf16* a = &Ah[cur][wm * WM + i * 32 + l32][16 * st + kh];
+                ah[i] = *reinterpret_cast<const bf16x8*>(a);
+                if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
+            }
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {
+                const __bf16* b = &Bh[cur][wn * WN + j * 32 + l32][16 * st + kh];
+                bh[j] = *reinterpret_cast<const bf16x8*>(b);
+                if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
+            }
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    if constexpr (MMA == MMA_BF16X3) {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                    }
+                    t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                }
+        };
+        step(0);
+        if (kt + 1 < kt_end) load(kt + 1);
+        step(1);
+        const long long rel = kt - kt_beg;
+        if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    acc[i][j] += t[i][j];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                }
+        }
+        if (kt + 1 < kt_end) store(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* slab = ws + (long long)split * d.Co * Ktot;
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + l32;
+        if (col >= Ktot) continue;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (row < d.Co) slab[(long long)row * Ktot + col] = acc[i][j][r];
+            }
+    }
+}
+
 // dw[co][ci][ty][tx] = sum_s ws[s][co][(ty*KW+tx)*Cs + ci].  Threads walk the slabs in
 // their own (co, tap, ci) order so the nsplit reads per output are coalesced; each output is
 // written once (scattered into OIHW).  Fixed split order: deterministic.
@@ -1042,6 +1378,8 @@ static int validate(const dcs_conv_desc* d, bool rows) {
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
     if (d->cw < 0 || d->cw > d->Cs) return fail(DCS_E_INVALID, "conv: bad cw (weight channels)");
+    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3)
+        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16 or DCS_MMA_BF16X3");
     if (!d->parity) {
         // output dims must be those of the forward conv over the virtual input
         int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
@@ -1122,6 +1460,16 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
                      d.stride == 1;
     hipStream_t s = as_stream(stream);
+    const bool mma_ok = vec && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
+    if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
+#define DCS_ROWS_MMA(M)                                                                                              \
+    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy); \
+    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);  \
+    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        if (d.mma == MMA_BF16) { DCS_ROWS_MMA(MMA_BF16) } else { DCS_ROWS_MMA(MMA_BF16X3) }
+#undef DCS_ROWS_MMA
+        return check_launch("conv_rows");
+    }
     if (BN == 128) {
         if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
         else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
@@ -1226,7 +1574,25 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     float* w = reinterpret_cast<float*>(ws);
     const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity;
     const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
-    if (p.BM == 128) {
+    const bool dy_small = (long long)d.N * d.Ho * d.Wo * d.Co * 4 < (long long)OOB_OFF - 64;
+    // The bf16 weight-gradient kernel measured slower than the exact f32 one at every layer
+    // (res 2.1-2.5 ms vs 1.75 ms: its 8-pixel walk per thread is VALU bound), so bf16 modes run
+    // the f32 weight gradient unless DCS_WGRAD_MMA16 is defined (kept for the A/B record).
+#ifdef DCS_WGRAD_MMA16
+    if (d.mma != MMA_F32 && vec && dy_small && p.BM == 128 && p.BN == 128 && !d.parity) {
+#else
+    if (false && dy_small) {
+#endif
+        const bool uni = d.Cs % 128 == 0;
+        if (d.mma == MMA_BF16 && uni)
+            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (d.mma == MMA_BF16)
+            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+        else if (uni)
+            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+        else
+            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+    } else if (p.BM == 128) {
         if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
         else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
         else if (v4) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -17,6 +18,23 @@ from . import lib
 from .lib import ACT_AFFINE, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, DCS_PAD_REFLECT, DCS_PAD_ZERO
 
 IN_EPS = 1e-5
+
+# MFMA operand mode of the MFMA convolution passes (include/ducosy_hip.h DCS_MMA_*): "f32" is
+# exact fp32 (the reference's precision, default); "bf16" rounds the GEMM operands to bf16
+# (BASELINE config 5's half-precision path); "bf16x3" splits each operand into hi + lo bf16.
+_MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3}
+_MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f32")]
+
+
+def set_mma(mode: str) -> None:
+    global _MMA
+    if mode not in _MMA_NAMES:
+        raise ValueError(f"mma mode must be one of {sorted(_MMA_NAMES)}")
+    _MMA = _MMA_NAMES[mode]
+
+
+def get_mma() -> str:
+    return {v: k for k, v in _MMA_NAMES.items()}[_MMA]
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -224,6 +242,7 @@ class ConvGeom:
             d.up, d.parity = 1, 2  # phases over the source grid (the upsample is in the weights)
         d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
         d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
+        d.mma = _MMA
         return d
 
     # ---- forward -------------------------------------------------------------------
@@ -260,6 +279,7 @@ class ConvGeom:
         d.up, d.pad_mode = 1, DCS_PAD_ZERO
         d.KH = d.KW = self.k
         d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
+        d.mma = _MMA
         d.Co = ci
         dev = dy.device
         t, l, b, r = self.pads

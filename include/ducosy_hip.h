@@ -70,7 +70,17 @@ typedef struct dcs_conv_desc {
     int32_t ldb;                    /* packed weights: Kpad (rows pass) / ncols (narrow)  */
     int32_t pro_act;                /* DCS_ACT_* prologue on the source                   */
     int32_t epi_act;                /* DCS_ACT_NONE / DCS_ACT_TANH / DCS_ACT_LRELU        */
+    int32_t mma;                    /* MFMA operands: DCS_MMA_F32 (exact, default),       */
+                                    /* DCS_MMA_BF16 or DCS_MMA_BF16X3 (f32 accumulation)  */
 } dcs_conv_desc;
+
+/* MFMA operand modes of the MFMA convolution passes (dcs_conv_desc.mma).  F32 is exact fp32
+ * (the reference's precision).  BF16 rounds both GEMM operands to bf16 (BASELINE config 5's
+ * half-precision path).  BF16X3 splits each operand into hi + lo bf16 and sums three
+ * products (~2^-16 relative error per product).  Shapes without a bf16 variant run F32. */
+#define DCS_MMA_F32 0
+#define DCS_MMA_BF16 1
+#define DCS_MMA_BF16X3 3
 
 const char* dcs_last_error(void);
 int dcs_version(void);
