@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--mma", default="f32", choices=["f32", "bf16", "bf16x3"],
                     help="MFMA operand mode of the conv passes: f32 = exact fp32 (the headline), "
                          "bf16 = BASELINE config 5's half-precision MFMA path, bf16x3 = split hi/lo bf16")
+    ap.add_argument("--dual", action="store_true",
+                    help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained "
+                         "concurrently, one HIP stream each; value counts the images of both models")
     args = ap.parse_args()
 
     from modules import parallel
@@ -103,11 +106,21 @@ def main():
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
     torch.manual_seed(1234)
-    system = CycleGANSystem(args.cin, args.blocks, True, device=device)
-    batches = [_synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i) for i in range(2)]
+    if args.dual:
+        from modules.trainer import ConcurrentCycleGANs
+        cins = (3, 2)
+        runner = ConcurrentCycleGANs([CycleGANSystem(c, args.blocks, True, device=device) for c in cins], device)
+        batches = [[_synthetic(args.batch, args.img, c - 1, device, 100 * rank + 10 * c + i) for c in cins]
+                   for i in range(2)]
+        step = lambda b: runner.train_step(b)
+    else:
+        system = CycleGANSystem(args.cin, args.blocks, True, device=device)
+        batches = [_synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i) for i in range(2)]
+        step = lambda b: system.train_step(*b)
+    models = 2 if args.dual else 1
 
     for i in range(args.warmup):
-        system.train_step(*batches[i % 2])
+        step(batches[i % 2])
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -115,7 +128,7 @@ def main():
     ops.PROBE.active = True
     t0 = time.perf_counter()
     for i in range(args.steps):
-        system.train_step(*batches[i % 2])
+        step(batches[i % 2])
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -128,7 +141,7 @@ def main():
     n_launch, ms_launch, flop_launch = ops.PROBE.summary()
 
     if rank == 0:
-        value = world * args.batch * args.steps / elapsed
+        value = world * models * args.batch * args.steps / elapsed
         achieved = flop_launch / (ms_launch * 1e-3) / 1e12 if ms_launch > 0 else 0.0
         rec = {
             "metric": "CycleGAN train-step images/sec at 512x512 bs=8/GPU",
@@ -144,10 +157,14 @@ def main():
             "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {
-                "workload": "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
-                            "9 G loss terms + 2 D losses, 3 Adam steps",
+                "workload": ("dual soft-tissue (cin 3) + lung (cin 2) CycleGANs trained concurrently (one HIP "
+                             "stream each), full train step per model; value = images of both models per second"
+                             if args.dual else
+                             "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
+                             "9 G loss terms + 2 D losses, 3 Adam steps"),
                 "img_size": args.img, "per_gpu_batch": args.batch, "global_batch": args.batch * world,
-                "residual_blocks": args.blocks, "input_channels": args.cin, "parallelism": f"dp{world}",
+                "residual_blocks": args.blocks, "input_channels": [3, 2] if args.dual else args.cin,
+                "parallelism": f"dp{world}",
             },
             "roofline": {
                 "kernel": f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)",
@@ -162,7 +179,7 @@ def main():
                 "gflop_per_launch": round(flop_launch / 1e9, 3),
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.dual:
             threads = min(16, os.cpu_count() or 1)
             rec["cpu_baseline"] = cpu_baseline(args.img, args.blocks, args.cin, threads)
         print(json.dumps(rec), flush=True)

@@ -61,9 +61,11 @@ _WS = {}
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:
-    """Scratch buffer reused across calls (stream-ordered reuse is safe on one stream)."""
+    """Scratch buffer reused across calls: one per (device, stream), so stream-ordered reuse is
+    safe and models stepping concurrently on different streams never share scratch."""
     nbytes = max(int(nbytes), 256)
-    key = torch.device(device).index
+    dev = torch.device(device)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         size = max(nbytes, int(buf.numel() * 1.5) if buf is not None else 0)

@@ -159,6 +159,37 @@ class CycleGANSystem:
         return loss_GAN + self.lambda_cyc * loss_cycle + self.lambda_id * loss_id
 
 
+class ConcurrentCycleGANs:
+    """Several CycleGANSystems trained in the same process, each on its own HIP stream
+    (BASELINE config 5: the soft-tissue (cin 3) and lung (cin 2) models concurrently; the
+    reference trains them one after the other, train.py:27-38).  A step enqueues every model's
+    train_step on its stream; the kernels of one model fill the gaps of the other (small
+    normalisation / loss / Adam launches, split-K reductions, launch latency).  Workspaces are
+    per stream (ops.workspace), the kernels are deterministic, so each model's numbers equal a
+    sequential run bit for bit (tests/test_gpu_concurrent.py)."""
+
+    def __init__(self, systems, device):
+        self.systems = list(systems)
+        self.device = torch.device(device)
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.systems]
+
+    def train_step(self, batches):
+        """batches: one (real_A, real_B, masks) per system.  Returns one loss dict per system
+        (device tensors, ready once the streams are synchronised with the caller's)."""
+        cur = torch.cuda.current_stream(self.device)
+        out = []
+        for sysm, st, b in zip(self.systems, self.streams, batches):
+            st.wait_stream(cur)  # inputs produced on the caller's stream
+            with torch.cuda.stream(st):
+                for t in b:
+                    if t is not None:
+                        t.record_stream(st)
+                out.append(sysm.train_step(*b))
+        for st in self.streams:
+            cur.wait_stream(st)
+        return out
+
+
 # -------------------------------------------------------------------------------------------
 # data: a DICOM tree (modules/dataset.py: decode on the loader workers, HU transform + masks on
 # the GPU) when data_root/dataset_names exists, synthetic slices of the reference's shapes

@@ -1,0 +1,39 @@
+"""Concurrent training of two CycleGANs on two HIP streams (BASELINE config 5: soft-tissue cin 3
+and lung cin 2 models; modules/trainer.py ConcurrentCycleGANs) gives each model exactly the
+losses and weights of a sequential run: the kernels are deterministic and every stream has its
+own workspace."""
+import pytest
+import torch
+
+from oracle import prng
+from test_gpu_train import _system
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _batch(seed, i, n, hw, cin):
+    rA = torch.from_numpy(prng.uniform(seed, f"A{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+    rB = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+    mk = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, hw, hw), 0.3)).to(DEV)
+    return rA, rB, mk
+
+
+def test_concurrent_equals_sequential():
+    from modules.trainer import ConcurrentCycleGANs
+    n, hw, nb, steps = 2, 64, 2, 3
+    cfg = [(3, 801), (2, 802)]
+    seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
+    want = [[{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)]
+            for m, (c, s) in zip(seq, cfg)]
+    run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV)
+    got = [[], []]
+    for i in range(steps):
+        outs = run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])
+        torch.cuda.synchronize()
+        for j, o in enumerate(outs):
+            got[j].append({k: float(v) for k, v in o.items()})
+    assert got == want
+    for a, b in zip(seq, run.systems):
+        assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)
+        assert torch.equal(a.optimizer_D_A.flat_p, b.optimizer_D_A.flat_p)
