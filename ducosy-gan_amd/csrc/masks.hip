@@ -6,8 +6,8 @@
 // All of it is integer / byte work bounded by HBM and atomics, never a GEMM:
 //   * threshold passes write one flag byte per pixel (F_* bits below);
 //   * connected components (scipy.ndimage.label, 4-connectivity in 2-D) are a lock-free
-//     union-find over the whole batch (Playne & Hawick 2018): init / merge with the left and
-//     upper neighbour / path compression, with wave-aggregated size counting;
+//     union-find (Playne & Hawick 2018): per 4096-pixel tile in LDS, then across tile
+//     borders in global memory, then path compression with wave-aggregated size counting;
 //   * binary_fill_holes = background components (4-connected) that touch no image edge;
 //   * the lung convex hull (scipy ConvexHull -> matplotlib Path.contains_points) is Andrew's
 //     monotone chain over the per-row extreme lung pixels (the only possible hull vertices),
@@ -68,17 +68,105 @@ __device__ __forceinline__ void uf_union(int* L, int a, int b) {
     } while (!done);
 }
 
-__global__ __launch_bounds__(MT) void uf_init_kernel(const uint8_t* __restrict__ M, int* __restrict__ L, int np) {
-    const int i = blockIdx.x * MT + threadIdx.x;
-    if (i < np) L[i] = M[i] ? i : -1;
+// Tile-local labelling: a workgroup labels the UF_TILE consecutive pixels [t*UF_TILE, ...) of
+// slice n in LDS (edges to the left / upper neighbour that lie inside the tile, LDS atomics) and
+// writes for every foreground pixel the global index of its tile-local root (-1 elsewhere).
+// Only the edges that cross into an earlier tile are then unioned in global memory
+// (uf_border_kernel): W per tile instead of two per pixel.
+constexpr int UF_TILE = 4096;
+
+__device__ __forceinline__ int lds_find(int* lab, int x) {
+    int p = __hip_atomic_load(lab + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(lab + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return x;
 }
 
-__global__ __launch_bounds__(MT) void uf_merge_kernel(const uint8_t* __restrict__ M, int* L, int H, int W, int np) {
+__device__ __forceinline__ void lds_union(int* lab, int a, int b) {
+    bool done;
+    do {
+        a = lds_find(lab, a);
+        b = lds_find(lab, b);
+        if (a < b) {
+            const int old = atomicMin(lab + b, a);
+            done = old == b;
+            b = old;
+        } else if (b < a) {
+            const int old = atomicMin(lab + a, b);
+            done = old == a;
+            a = old;
+        } else {
+            done = true;
+        }
+    } while (!done);
+}
+
+// Up-edge rule: for 4-connectivity the edge (j, j-W) is implied when the left pair is
+// connected on both rows (j-1 ~ j-1-W and j-W ~ j-1-W), so only pixels that start a run in their
+// row or sit under the start of a run in the row above need the union.
+__device__ __forceinline__ bool need_up(bool left_fg, bool upleft_fg) { return !(left_fg && upleft_fg); }
+
+constexpr int UF_SEG = UF_TILE / MT;  // consecutive pixels per thread (16)
+
+__global__ __launch_bounds__(MT) void uf_local_kernel(const uint8_t* __restrict__ M, int* __restrict__ L, int H, int W,
+                                                      int tiles) {
+    __shared__ int lab[UF_TILE];
+    __shared__ uint8_t fgm[UF_TILE];
+    const int HW = H * W;
+    const int n = blockIdx.x / tiles, t = blockIdx.x - n * tiles;
+    const int p0 = t * UF_TILE;
+    const int cnt = min(UF_TILE, HW - p0);
+    const int g0 = n * HW + p0;
+    for (int j = threadIdx.x; j < UF_TILE; j += MT) fgm[j] = j < cnt ? M[g0 + j] : 0;
+    __syncthreads();
+    // runs inside this thread's segment point at their first pixel (no atomics)
+    const int j0 = threadIdx.x * UF_SEG;
+    int x = (p0 + j0) % W;
+    int run = -1;
+#pragma unroll
+    for (int e = 0; e < UF_SEG; ++e) {
+        const int j = j0 + e;
+        if (e > 0 && ++x == W) x = 0;
+        if (!fgm[j]) { lab[j] = -1; run = -1; continue; }
+        if (run < 0 || x == 0) run = j;
+        lab[j] = run;
+    }
+    __syncthreads();
+    // unions: the segment's first pixel with its left neighbour, and the needed up-edges
+    x = (p0 + j0) % W;
+#pragma unroll
+    for (int e = 0; e < UF_SEG; ++e) {
+        const int j = j0 + e;
+        if (e > 0 && ++x == W) x = 0;
+        if (j >= cnt || !fgm[j]) continue;
+        const bool left = x > 0 && j > 0 && fgm[j - 1];
+        if (e == 0 && left) lds_union(lab, j, j - 1);
+        if (j >= W && fgm[j - W] && need_up(left, x > 0 && fgm[j - 1 - W])) lds_union(lab, j, j - W);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < cnt; j += MT) L[g0 + j] = fgm[j] ? g0 + lds_find(lab, j) : -1;
+}
+
+// edges from tile t >= 1 into earlier tiles: its first min(W, UF_TILE) pixels (upper neighbour)
+// and its first pixel (left neighbour, when the tile starts mid-row)
+__global__ __launch_bounds__(MT) void uf_border_kernel(const uint8_t* __restrict__ M, int* L, int H, int W, int tiles,
+                                                       int span, int total) {
     const int i = blockIdx.x * MT + threadIdx.x;
-    if (i >= np || !M[i]) return;
-    const int x = i % W, y = (i / W) % H;
-    if (x > 0 && M[i - 1]) uf_union(L, i, i - 1);
-    if (y > 0 && M[i - W]) uf_union(L, i, i - W);
+    if (i >= total) return;
+    const int per = (tiles - 1) * span;
+    const int n = i / per, r = i - n * per;
+    const int t = 1 + r / span, k = r - (t - 1) * span;
+    const int HW = H * W;
+    const int p = t * UF_TILE + k;
+    if (p >= HW) return;
+    const int g = n * HW + p;
+    if (!M[g]) return;
+    const int x = p % W;
+    const bool left = x > 0 && M[g - 1];
+    if (p >= W && M[g - W] && need_up(left, x > 0 && M[g - 1 - W])) uf_union(L, g, g - W);
+    if (k == 0 && left) uf_union(L, g, g - 1);
 }
 
 // L[i] = root; with count != nullptr also count[root] += 1, aggregated over runs of equal
@@ -154,17 +242,17 @@ __global__ __launch_bounds__(MT) void mask_seed_kernel(const float* __restrict__
                                                        MaskArgs a, uint8_t* __restrict__ F, uint8_t* __restrict__ M,
                                                        SliceInfo* si) {
     const int n = blockIdx.y, HW = a.H * a.W;
-    const int p = blockIdx.x * MT + threadIdx.x;
     int body = 0;
-    if (p < HW) {
+    for (int p = blockIdx.x * MT + threadIdx.x; p < HW; p += gridDim.x * MT) {
         const int i = n * HW + p;
         const int y = p / a.W, x = p - y * a.W;
         const float v = hu[i];
-        body = v > -1000.f;
+        const bool bd = v > -1000.f;
+        body += bd;
         const bool inner = y >= a.border && y < a.H - a.border && x >= a.border && x < a.W - a.border;
         // a caller-supplied lung mask (detect_mediastinum(hu, lung_mask) etc.) replaces detect_lung
-        const bool lc = lung_in ? lung_in[i] != 0 : body && v >= a.lung_lower && v <= a.lung_upper && inner;
-        const bool ab = body && v >= a.bone_thr;
+        const bool lc = lung_in ? lung_in[i] != 0 : bd && v >= a.lung_lower && v <= a.lung_upper && inner;
+        const bool ab = bd && v >= a.bone_thr;
         F[i] = (lc ? F_LUNGC : 0) | (ab ? F_ABONE : 0);
         M[i] = lc;
     }
@@ -179,23 +267,43 @@ __global__ __launch_bounds__(MT) void lung_final_kernel(MaskArgs a, const int* _
                                                         uint8_t* __restrict__ F, SliceInfo* si, int* __restrict__ rowmin,
                                                         int* __restrict__ rowmax) {
     const int n = blockIdx.y, HW = a.H * a.W;
-    const int p = blockIdx.x * MT + threadIdx.x;
-    int lung = 0, root = 0;
-    if (p < HW) {
-        const int i = n * HW + p;
-        const uint8_t f = F[i];
-        if (f & F_LUNGC) {
-            const int r = L[i];
-            if (C[r] >= a.min_size) {
-                lung = 1;
-                root = r == i;
-                F[i] = f | F_LUNG;
-                const int y = p / a.W, x = p - y * a.W;
-                atomicMin(rowmin + n * a.H + y, x);
-                atomicMax(rowmax + n * a.H + y, x);
+    int lung_cnt = 0, root_cnt = 0;
+    // grid-stride with a block-uniform trip count (the wave shuffles below need every lane)
+    for (int p0 = blockIdx.x * MT; p0 < HW; p0 += gridDim.x * MT) {
+        const int p = p0 + threadIdx.x;
+        int lung = 0, y = 0, x = 0;
+        if (p < HW) {
+            const int i = n * HW + p;
+            const uint8_t f = F[i];
+            y = p / a.W;
+            x = p - y * a.W;
+            if (f & F_LUNGC) {
+                const int r = L[i];
+                if (C[r] >= a.min_size) {
+                    lung = 1;
+                    root_cnt += r == i;
+                    F[i] = f | F_LUNG;
+                }
             }
         }
+        lung_cnt += lung;
+        if ((a.W & 63) == 0) {  // the wave's 64 pixels share one row: one atomic pair per wave
+            int mn = lung ? x : 0x7fffffff, mx = lung ? x : -1;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mn = min(mn, __shfl_xor(mn, o, 64));
+                mx = max(mx, __shfl_xor(mx, o, 64));
+            }
+            if ((threadIdx.x & 63) == 0 && mx >= 0) {
+                atomicMin(rowmin + n * a.H + y, mn);
+                atomicMax(rowmax + n * a.H + y, mx);
+            }
+        } else if (lung) {
+            atomicMin(rowmin + n * a.H + y, x);
+            atomicMax(rowmax + n * a.H + y, x);
+        }
     }
+    const int lung = lung_cnt, root = root_cnt;
     __shared__ float red[4];
     const float s = block_sum_256((float)lung, red);
     const float nr = block_sum_256((float)root, red);
@@ -205,8 +313,35 @@ __global__ __launch_bounds__(MT) void lung_final_kernel(MaskArgs a, const int* _
     }
 }
 
-__device__ __forceinline__ long long cross2(int2 o, int2 a, int2 b) {
-    return (long long)(a.x - o.x) * (b.y - o.y) - (long long)(a.y - o.y) * (b.x - o.x);
+// |coordinates| < 1024 (H, W <= 1024): every product below fits in 32 bits
+__device__ __forceinline__ int cross2(int2 o, int2 a, int2 b) {
+    return (a.x - o.x) * (b.y - o.y) - (a.y - o.y) * (b.x - o.x);
+}
+
+// One workgroup per slice: the gate of mask_generator.py:68/116/196 (>= 2 lung regions and
+// lung/body area >= 0.1, in float64 like numpy) and the convex hull of the lung pixels,
+// vertices as (row, col) counter-clockwise, no collinear points (qhull's output).
+// hull_ok = 0 when there are < 3 lung pixels or they are collinear (qhull raises; the
+// reference falls back to the lung mask itself / skips the exclusion).
+// Andrew's monotone chain over pts[0..np) in the given direction (+1 / -1) into out; returns the
+// chain length.  The top two stack entries live in registers (one LDS read per pop).
+__device__ int hull_chain(const int2* pts, int np, int dir, int2* out) {
+    int k = 0;
+    int2 t1 = make_int2(0, 0), t2 = make_int2(0, 0);  // out[k-1], out[k-2]
+    int2 nxt = np > 0 ? pts[dir > 0 ? 0 : np - 1] : make_int2(0, 0);
+    for (int j = 0; j < np; ++j) {
+        const int2 p = nxt;
+        if (j + 1 < np) nxt = pts[dir > 0 ? j + 1 : np - 2 - j];
+        while (k >= 2 && cross2(t2, t1, p) <= 0) {
+            --k;
+            t1 = t2;
+            if (k >= 2) t2 = out[k - 2];
+        }
+        out[k++] = p;
+        t2 = t1;
+        t1 = p;
+    }
+    return k;
 }
 
 // One workgroup per slice: the gate of mask_generator.py:68/116/196 (>= 2 lung regions and
@@ -217,10 +352,12 @@ __device__ __forceinline__ long long cross2(int2 o, int2 a, int2 b) {
 __global__ __launch_bounds__(MT) void lung_hull_kernel(MaskArgs a, SliceInfo* si, const int* __restrict__ rowmin,
                                                        const int* __restrict__ rowmax, int2* __restrict__ hull,
                                                        int maxv) {
-    extern __shared__ int2 sh[];  // pts[maxv], hv[maxv + 1], rows (lo, hi)[H]
+    extern __shared__ int2 sh[];  // pts[maxv], lower[maxv], upper[maxv], rows (lo, hi)[H]
     int2* pts = sh;
-    int2* hv = sh + maxv;
-    int2* rows = sh + 2 * maxv + 1;
+    int2* lo = sh + maxv;
+    int2* up = sh + 2 * maxv;
+    int2* rows = sh + 3 * maxv;
+    __shared__ int npts, nlo, nup;
     const int n = blockIdx.x;
     SliceInfo& s = si[n];
     const int cond = s.nreg >= 2 && s.body > 0 && (double)s.lung_area / (double)s.body >= 0.1;
@@ -228,32 +365,54 @@ __global__ __launch_bounds__(MT) void lung_hull_kernel(MaskArgs a, SliceInfo* si
         if (threadIdx.x == 0) { s.cond = cond; s.hull_ok = 0; s.nv = 0; }
         return;
     }
-    for (int y = threadIdx.x; y < a.H; y += MT) rows[y] = make_int2(rowmin[n * a.H + y], rowmax[n * a.H + y]);
+    // points sorted by (row, col): per row its leftmost then rightmost lung pixel.  Thread t owns
+    // rows 4t .. 4t+3 (H <= 1024); an exclusive scan of the per-thread counts places them.
+    __shared__ int wsum[MT / 64];
+    int cntp[4], tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int y = 4 * threadIdx.x + e;
+        int c = 0;
+        if (y < a.H) {
+            const int2 r = make_int2(rowmin[n * a.H + y], rowmax[n * a.H + y]);
+            rows[y] = r;
+            c = r.y < 0 ? 0 : (r.y != r.x ? 2 : 1);
+        }
+        cntp[e] = c;
+        tot += c;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wv] = inc;
     __syncthreads();
+    int base = inc - tot;
+    for (int w2 = 0; w2 < wv; ++w2) base += wsum[w2];
+    if (threadIdx.x == MT - 1) npts = base + tot;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int y = 4 * threadIdx.x + e;
+        if (cntp[e] == 0) continue;
+        const int2 r = rows[y];
+        pts[base++] = make_int2(y, r.x);
+        if (cntp[e] == 2) pts[base++] = make_int2(y, r.y);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) nlo = hull_chain(pts, npts, +1, lo);
+    if (threadIdx.x == 64) nup = hull_chain(pts, npts, -1, up);  // another wave: runs concurrently
+    __syncthreads();
+    // hull = lower[0 .. nlo-2] ++ upper[0 .. nup-2] (each chain ends where the other starts)
+    const int kl = nlo - 1, k = kl + nup - 1;
+    const int ok = k >= 3;
+    for (int j = threadIdx.x; ok && j < k; j += MT) hull[(long long)n * maxv + j] = j < kl ? lo[j] : up[j - kl];
     if (threadIdx.x == 0) {
-        // points sorted by (row, col): per row its leftmost then rightmost lung pixel
-        int np = 0;
-        for (int y = 0; y < a.H; ++y) {
-            const int2 r = rows[y];
-            if (r.y < 0) continue;
-            pts[np++] = make_int2(y, r.x);
-            if (r.y != r.x) pts[np++] = make_int2(y, r.y);
-        }
-        int k = 0;
-        for (int j = 0; j < np; ++j) {  // lower hull
-            while (k >= 2 && cross2(hv[k - 2], hv[k - 1], pts[j]) <= 0) --k;
-            hv[k++] = pts[j];
-        }
-        for (int j = np - 2, t = k + 1; j >= 0; --j) {  // upper hull
-            while (k >= t && cross2(hv[k - 2], hv[k - 1], pts[j]) <= 0) --k;
-            hv[k++] = pts[j];
-        }
-        --k;  // the last point repeats the first
-        const int ok = k >= 3;
         s.cond = cond;
         s.hull_ok = ok;
         s.nv = ok ? k : 0;
-        for (int j = 0; ok && j < k; ++j) hull[(long long)n * maxv + j] = hv[j];
     }
 }
 
@@ -267,8 +426,8 @@ __device__ __forceinline__ bool point_in_hull(const int2* hv, int nv, int tx, in
         const int2 v1 = hv[j];
         const bool f1 = v1.y >= ty;
         if (f0 != f1) {
-            const long long lhs = (long long)(v1.y - ty) * (v0.x - v1.x);
-            const long long rhs = (long long)(v1.x - tx) * (v0.y - v1.y);
+            const int lhs = (v1.y - ty) * (v0.x - v1.x);
+            const int rhs = (v1.x - tx) * (v0.y - v1.y);
             if ((lhs >= rhs) == f1) inside = !inside;
         }
         v0 = v1;
@@ -415,10 +574,17 @@ static MaskWs carve(void* base, int N, int H, int W) {
     return w;
 }
 
-static int run_cc(MaskWs& w, int H, int W, int np, bool count, hipStream_t s) {
+static int run_cc(MaskWs& w, int N, int H, int W, bool count, hipStream_t s) {
+    const int HW = H * W, np = N * HW;
+    const int tiles = (int)cdiv(HW, UF_TILE);
     const dim3 g((unsigned)cdiv(np, MT));
-    hipLaunchKernelGGL(uf_init_kernel, g, dim3(MT), 0, s, w.M, w.L, np);
-    hipLaunchKernelGGL(uf_merge_kernel, g, dim3(MT), 0, s, w.M, w.L, H, W, np);
+    hipLaunchKernelGGL(uf_local_kernel, dim3((unsigned)(N * tiles)), dim3(MT), 0, s, w.M, w.L, H, W, tiles);
+    if (tiles > 1) {
+        const int span = W < UF_TILE ? W : UF_TILE;
+        const int total = N * (tiles - 1) * span;
+        hipLaunchKernelGGL(uf_border_kernel, dim3((unsigned)cdiv(total, MT)), dim3(MT), 0, s, w.M, w.L, H, W, tiles,
+                           span, total);
+    }
     hipLaunchKernelGGL(fill_int_kernel, g, dim3(MT), 0, s, w.C, 0, np);
     hipLaunchKernelGGL(uf_compress_kernel, g, dim3(MT), 0, s, w.M, w.L, count ? w.C : (int*)nullptr, np);
     return check_launch("masks: connected components");
@@ -462,8 +628,8 @@ extern "C" int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int
                                     size_t ws_bytes, void* stream) {
     if (!hu || !thresholds || !iparams || !chan || !out || !ws || N <= 0 || H < 1 || W < 1 || nout < 1 || nout > 4)
         return fail(DCS_E_INVALID, "anatomical_masks: bad arguments");
-    if ((long long)N * H * W >= (1ll << 31) || H > 4096)
-        return fail(DCS_E_INVALID, "anatomical_masks: batch too large (N*H*W < 2^31, H <= 4096)");
+    if ((long long)N * H * W >= (1ll << 31) || H > 1024 || W > 1024)
+        return fail(DCS_E_INVALID, "anatomical_masks: batch too large (N*H*W < 2^31, H, W <= 1024)");
     for (int c = 0; c < 4; ++c)
         if (chan[c] < -1 || chan[c] >= nout) return fail(DCS_E_INVALID, "anatomical_masks: bad channel map");
     if (ws_bytes < dcs_masks_workspace_size(N, H, W))
@@ -489,18 +655,20 @@ extern "C" int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int
         return fail(DCS_E_INVALID, "anatomical_masks: memset failed");
     hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)cdiv(N * H, MT)), dim3(MT), 0, s, w.rowmin, W, N * H);
     hipLaunchKernelGGL(fill_int_kernel, dim3((unsigned)cdiv(N * H, MT)), dim3(MT), 0, s, w.rowmax, -1, N * H);
-    hipLaunchKernelGGL(mask_seed_kernel, gs, dim3(MT), 0, s, hu, lung_in, a, w.F, w.M, w.si);
+    // the per-slice counters take one atomic per block: at most 64 blocks per slice
+    const dim3 gc((unsigned)(cdiv(HW, MT) < 64 ? cdiv(HW, MT) : 64), (unsigned)N);
+    hipLaunchKernelGGL(mask_seed_kernel, gc, dim3(MT), 0, s, hu, lung_in, a, w.F, w.M, w.si);
     if ((e = check_launch("masks: seed"))) return e;
     // detect_lung: components of the lung candidates, size filter, gate and hull
-    if ((e = run_cc(w, H, W, np, true, s))) return e;
-    hipLaunchKernelGGL(lung_final_kernel, gs, dim3(MT), 0, s, a, w.L, w.C, w.F, w.si, w.rowmin, w.rowmax);
+    if ((e = run_cc(w, N, H, W, true, s))) return e;
+    hipLaunchKernelGGL(lung_final_kernel, gc, dim3(MT), 0, s, a, w.L, w.C, w.F, w.si, w.rowmin, w.rowmax);
     if ((e = check_launch("masks: lung"))) return e;
-    hipLaunchKernelGGL(lung_hull_kernel, dim3((unsigned)N), dim3(MT),
-                       (size_t)(2 * maxv + 1 + H) * sizeof(int2), s, a, w.si, w.rowmin, w.rowmax, w.hull, maxv);
+    hipLaunchKernelGGL(lung_hull_kernel, dim3((unsigned)N), dim3(MT), (size_t)(3 * maxv + H) * sizeof(int2), s, a,
+                       w.si, w.rowmin, w.rowmax, w.hull, maxv);
     if ((e = check_launch("masks: hull"))) return e;
     if (want_ves) {  // holes of the lung mask
         hipLaunchKernelGGL(stage_complement_kernel, gl, dim3(MT), 0, s, w.F, (int)F_LUNG, w.M, np);
-        if ((e = run_cc(w, H, W, np, false, s))) return e;
+        if ((e = run_cc(w, N, H, W, false, s))) return e;
         hipLaunchKernelGGL(mark_edge_kernel, gl, dim3(MT), 0, s, w.M, w.L, H, W, w.C, np);
         hipLaunchKernelGGL(vessel_kernel, gs, dim3(MT), 0, s, hu, a, w.si, w.M, w.L, w.C, w.F);
         if ((e = check_launch("masks: vessels"))) return e;
@@ -511,11 +679,11 @@ extern "C" int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int
         if ((e = check_launch("masks: hull pass"))) return e;
     }
     if (want_bone) {  // region growing over the bone candidates, then the holes of the result
-        if ((e = run_cc(w, H, W, np, false, s))) return e;
+        if ((e = run_cc(w, N, H, W, false, s))) return e;
         hipLaunchKernelGGL(mark_seed_kernel, gl, dim3(MT), 0, s, w.F, w.L, w.C, np);
         hipLaunchKernelGGL(bone_grow_kernel, gl, dim3(MT), 0, s, w.L, w.C, w.F, np);
         hipLaunchKernelGGL(stage_complement_kernel, gl, dim3(MT), 0, s, w.F, (int)F_BONE, w.M, np);
-        if ((e = run_cc(w, H, W, np, false, s))) return e;
+        if ((e = run_cc(w, N, H, W, false, s))) return e;
         hipLaunchKernelGGL(mark_edge_kernel, gl, dim3(MT), 0, s, w.M, w.L, H, W, w.C, np);
         if ((e = check_launch("masks: bone"))) return e;
     }

@@ -227,7 +227,7 @@ int dcs_hu_transform(const void* raw, int raw_dtype, const float* slope, const f
  * lung_in: optional device uint8 [N][H][W] binary lung mask used instead of detect_lung (the
  *   lung_mask argument of detect_mediastinum / detect_bone / detect_lung_vessels); NULL =
  *   computed from hu.
- * ws: dcs_masks_workspace_size(N, H, W) bytes.  Bit-exact with the reference. */
+ * ws: dcs_masks_workspace_size(N, H, W) bytes.  H, W <= 1024.  Bit-exact with the reference. */
 size_t dcs_masks_workspace_size(int N, int H, int W);
 int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int N, int H, int W, const float* thresholds,
                          const int32_t* iparams, const int32_t* chan, int nout, float* out, void* ws,
