@@ -79,6 +79,17 @@ def _pmc_traffic():
         return None
 
 
+def _pmc_mfma_busy(mode):
+    """MFMA-busy fraction of the dominant kernel in this mode from the committed rocprofv3 pass
+    (profiles/mfma_busy.json: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8))."""
+    p = os.path.join(ROOT, "profiles", "mfma_busy.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(mode, {}).get("mfma_busy_fraction")
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,6 +185,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / MODE_PEAK[args.mma], 4),
                 "traffic": _pmc_traffic() if args.mma == "f32" else None,
+                "mfma_busy": _pmc_mfma_busy(args.mma),
                 "launches": n_launch,
                 "ms_per_launch": round(ms_launch, 4),
                 "gflop_per_launch": round(flop_launch / 1e9, 3),

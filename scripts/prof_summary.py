@@ -14,7 +14,7 @@ import shutil
 import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-KERNEL = "conv_rows_kernel<128, 128, 1, 1>"
+KERNEL = "conv_rows_kernel<128, 128, 1, 1, 0>"
 
 
 def _mean_counter(path, counter):
