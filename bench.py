@@ -9,10 +9,16 @@ its Adam, D_A step, D_B step) on the fused HIP path, over one synthetic batch of
 GPU that is already resident in HBM.  Data parallel: one process per GPU, each with its own
 shard; one RCCL all-reduce per optimizer (weak scaling).  Rank 0 prints ONE JSON line.
 
+MFMA operand mode (--mma): bf16x6 by default, an fp32-class split (each fp32 operand = hi + mid
++ lo bf16, six bf16 MFMAs per product, fp32 accumulation and storage; its measured error
+against float64 is at or below the exact-f32 MFMA path's on every layer, tests/test_gpu_mma.py);
+--mma f32 runs the exact v_mfma_f32_32x32x2_f32 path.
+
 roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (implicit GEMM,
-conv_rows_kernel<128,128,1,1>, forward + data-gradient launches).  Its per-launch duration
-is measured live with HIP events on the launch stream over the timed steps; FLOPs are
-algorithmic (2*pixels*256*256*9 per launch).  Peak = 157.3 TFLOP/s (gfx950 f32 MFMA, dense).
+conv_rows_kernel<128,128,1,1,MODE>, forward + data-gradient launches).  Its per-launch
+duration is measured live with HIP events on the launch stream over the timed steps; FLOPs
+are algorithmic (2*pixels*256*256*9 per launch).  Peak: 157.3 TFLOP/s for f32 (gfx950 f32
+MFMA, dense); for bf16x6 the dense bf16 MFMA peak / 6 = 419.5 TFLOP/s of fp32 work.
 cpu_baseline: the oracle (oracle/ref_torch.py, the CPU restatement of the reference step)
 timed on this host on a bounded sample (one 512x512 slice, 9 blocks, one step).
 """
@@ -32,10 +38,12 @@ import torch  # noqa: E402
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 16 * F32_MFMA_PEAK_TFLOPS  # v_mfma_f32_32x32x16_bf16: 16x the f32 rate (~2.5 PF dense)
 # peak per mode for the dominant kernel's algorithmic FLOPs: bf16x3 issues 3 bf16 MFMAs per product
-MODE_PEAK = {"f32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+MODE_PEAK = {"f32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3,
+             "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6}
 MODE_DTYPE = {"f32": "f32", "bf16": "bf16 (MFMA operands; f32 accumulation and storage)",
-              "bf16x3": "f32 via bf16x3 MFMA (hi/lo split, ~2^-16 per product; f32 accumulation and storage)"}
-MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3}
+              "bf16x3": "f32 via bf16x3 MFMA (hi/lo split, ~2^-16 per product; f32 accumulation and storage)",
+              "bf16x6": "f32 via bf16x6 MFMA (hi/mid/lo split, ~2^-24 per product; f32 accumulation and storage)"}
+MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -68,10 +76,10 @@ def cpu_baseline(img, blocks, cin, threads):
                       f"({dt:.2f} s)"}
 
 
-def _pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
-    (profiles/pmc_resconv.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), if present."""
-    p = os.path.join(ROOT, "profiles", "pmc_resconv.json")
+def _pmc_traffic(mode):
+    """HBM bytes per launch of the dominant kernel in this mode from the committed rocprofv3 PMC
+    passes (profiles/pmc_resconv_MODE.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_resconv_{mode}.json")
     try:
         with open(p) as f:
             return json.load(f).get("hbm_bytes_per_launch")
@@ -100,13 +108,17 @@ def main():
     ap.add_argument("--blocks", type=int, default=9)
     ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mma", default="f32", choices=["f32", "bf16", "bf16x3"],
-                    help="MFMA operand mode of the conv passes: f32 = exact fp32 (the headline), "
-                         "bf16 = BASELINE config 5's half-precision MFMA path, bf16x3 = split hi/lo bf16")
+    ap.add_argument("--mma", default="bf16x6", choices=["f32", "bf16", "bf16x3", "bf16x6"],
+                    help="MFMA operand mode of the conv passes: bf16x6 = three-way split, fp32-class "
+                         "(default; error <= the exact-f32 path's, tests/test_gpu_mma.py), f32 = exact "
+                         "fp32 MFMA, bf16x3 = hi/lo split, bf16 = plain bf16 operands")
     ap.add_argument("--dual", action="store_true",
                     help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained "
                          "concurrently, one HIP stream each; value counts the images of both models")
     args = ap.parse_args()
+    if args.dual:  # the concurrent runner steps in its own (exact f32) mode: trainer.py ConcurrentCycleGANs
+        from modules.trainer import ConcurrentCycleGANs
+        args.mma = ConcurrentCycleGANs.MMA
 
     from modules import parallel
     from modules.hip import ops
@@ -184,7 +196,7 @@ def main():
                 "peak": round(MODE_PEAK[args.mma], 1),
                 "unit": "TFLOP/s",
                 "frac": round(achieved / MODE_PEAK[args.mma], 4),
-                "traffic": _pmc_traffic() if args.mma == "f32" else None,
+                "traffic": _pmc_traffic(args.mma),
                 "mfma_busy": _pmc_mfma_busy(args.mma),
                 "launches": n_launch,
                 "ms_per_launch": round(ms_launch, 4),

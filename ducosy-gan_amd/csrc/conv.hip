@@ -28,7 +28,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // (v_mfma_f32_32x32x16_bf16, f32 accumulation: BASELINE config 5's half-precision MFMA path),
 // and bf16x3 (each f32 operand split into hi + lo bf16, three MFMAs hi*hi + hi*lo + lo*hi:
 // ~2^-16 relative per product instead of 2^-24, at 3/16 of the f32-MFMA cycles per FLOP).
-constexpr int MMA_F32 = 0, MMA_BF16 = 1, MMA_BF16X3 = 3;
+constexpr int MMA_F32 = 0, MMA_BF16 = 1, MMA_BF16X3 = 3, MMA_BF16X6 = 6;
 #ifndef DCS_BF16_BUFGATHER
 #define DCS_BF16_BUFGATHER 1  // branch-free buffer-descriptor gather in the bf16 rows pass
 #endif
@@ -59,8 +59,23 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
     }
 }
 
+// three-way split for bf16x6: v = hi + mid + lo (each bf16, residuals exact in f32); the six
+// products that matter (all but mid*lo, lo*mid, lo*lo, each <= 2^-27 relative) give ~2^-24
+// relative error per product: fp32-class
+__device__ __forceinline__ void split8x3(const float4& a, const float4& b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+    const floatx8 f = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    hi = __builtin_convertvector(f, bf16x8);
+    const floatx8 r1 = f - __builtin_convertvector(hi, floatx8);
+    mid = __builtin_convertvector(r1, bf16x8);
+    const floatx8 r2 = r1 - __builtin_convertvector(mid, floatx8);
+    lo = __builtin_convertvector(r2, bf16x8);
+}
+
 constexpr int BK = 32;
 constexpr int NT = 256;
+#ifndef DCS_X6_BK
+#define DCS_X6_BK 16
+#endif
 
 // ---------------------------------------------------------------------------------------
 // geometry helpers
@@ -427,13 +442,16 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     constexpr int BTPR = NT / BN;                  // B loader threads per row (2 or 4)
     // bf16: 64-deep k-tiles (twice the MFMA work per round of global loads: the bf16 passes are
     // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
-    constexpr int BKT = BK;
+    constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : BK;  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
     constexpr int AKPT = BKT / 2;                  // k per A-loader thread (2 threads per row)
     constexpr int ACH = AKPT / 4;                  // float4 per A-loader thread
     constexpr int BKPT = BKT / BTPR;               // k per B-loader thread
     constexpr int BCH = BKPT / 4;                  // float4 per B-loader thread
-    constexpr int KT2 = 4;                         // k-tiles per inner accumulation chain
-    constexpr int LDE = MMA == MMA_BF16X3 ? 72 : BKT + 8;  // bf16 elements per LDS row (bf16 modes)
+    constexpr int KT2 = 128 / BKT;                 // k-tiles per inner accumulation chain (128 k)
+    // bf16 elements per LDS row: planes of BKT k (hi [, mid] [, lo]) + 8 pad; pitches 80 / 144 /
+    // 112 B keep the 16-B fragment reads conflict-free
+    constexpr int NPL = MMA == MMA_BF16X6 ? 3 : (MMA == MMA_BF16X3 ? 2 : 1);
+    constexpr int LDE = NPL * BKT + 8;
     constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK : (BM + BN) * LDE;
 
     // f32: As[2][BM][LDK] | Bs[2][BN][LDK];  bf16 modes: Ah[2][BM][LDE] | Bh[2][BN][LDE]
@@ -583,6 +601,25 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
             for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = ra[i];
 #pragma unroll
             for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
+        } else if constexpr (MMA == MMA_BF16X6) {
+            static_assert(ACH % 2 == 0 && BCH % 2 == 0, "x6 tiles: groups of 8 k per loader thread");
+            bf16x8 hi, mid, lo;
+            __bf16* a = Ah + (buf * BM + arow) * LDE + akq;
+#pragma unroll
+            for (int i = 0; i < ACH / 2; ++i) {
+                split8x3(ra[2 * i], ra[2 * i + 1], hi, mid, lo);
+                *reinterpret_cast<bf16x8*>(a + 8 * i) = hi;
+                *reinterpret_cast<bf16x8*>(a + BKT + 8 * i) = mid;
+                *reinterpret_cast<bf16x8*>(a + 2 * BKT + 8 * i) = lo;
+            }
+            __bf16* b = Bh + (buf * BN + brow) * LDE + bkq;
+#pragma unroll
+            for (int i = 0; i < BCH / 2; ++i) {
+                split8x3(rb[2 * i], rb[2 * i + 1], hi, mid, lo);
+                *reinterpret_cast<bf16x8*>(b + 8 * i) = hi;
+                *reinterpret_cast<bf16x8*>(b + BKT + 8 * i) = mid;
+                *reinterpret_cast<bf16x8*>(b + 2 * BKT + 8 * i) = lo;
+            }
         } else {
             bf16x8 hi, lo;
             __bf16* a = Ah + (buf * BM + arow) * LDE;
@@ -624,24 +661,39 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
         for (int kt = 0; kt < nkt; ++kt) {
             const int cur = kt & 1;
             auto step = [&](int st) {
-                bf16x8 ah[IM], bh[JN], al[IM], bl[JN];
+                bf16x8 ah[IM], bh[JN], al[IM], bl[JN], am[IM], bm[JN];
 #pragma unroll
                 for (int i = 0; i < IM; ++i) {
                     const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
                     ah[i] = *reinterpret_cast<const bf16x8*>(a);
                     if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
+                    if constexpr (MMA == MMA_BF16X6) {
+                        am[i] = *reinterpret_cast<const bf16x8*>(a + BKT);
+                        al[i] = *reinterpret_cast<const bf16x8*>(a + 2 * BKT);
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < JN; ++j) {
                     const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
                     bh[j] = *reinterpret_cast<const bf16x8*>(b);
                     if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
+                    if constexpr (MMA == MMA_BF16X6) {
+                        bm[j] = *reinterpret_cast<const bf16x8*>(b + BKT);
+                        bl[j] = *reinterpret_cast<const bf16x8*>(b + 2 * BKT);
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < IM; ++i)
 #pragma unroll
                     for (int j = 0; j < JN; ++j) {
-                        if constexpr (MMA == MMA_BF16X3) {
+                        if constexpr (MMA == MMA_BF16X6) {  // smallest terms first
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                        } else if constexpr (MMA == MMA_BF16X3) {
                             t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
                             t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
                             t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
@@ -655,7 +707,7 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
             if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
 #pragma unroll
             for (int st = NST / 2; st < NST; ++st) step(st);
-            if (MMA == MMA_BF16X3 && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
+            if (MMA != MMA_BF16 && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
 #pragma unroll
                 for (int i = 0; i < IM; ++i)
 #pragma unroll
@@ -665,6 +717,9 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
                         for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                     }
             }
+#ifdef DCS_ROWS_SYNC2
+            __syncthreads();
+#endif
             if (kt + 1 < nkt) store_tiles(cur ^ 1);
             __syncthreads();
         }
@@ -1378,8 +1433,8 @@ static int validate(const dcs_conv_desc* d, bool rows) {
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
     if (d->cw < 0 || d->cw > d->Cs) return fail(DCS_E_INVALID, "conv: bad cw (weight channels)");
-    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3)
-        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16 or DCS_MMA_BF16X3");
+    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3 && d->mma != MMA_BF16X6)
+        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16, DCS_MMA_BF16X3 or DCS_MMA_BF16X6");
     if (!d->parity) {
         // output dims must be those of the forward conv over the virtual input
         int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
@@ -1460,6 +1515,11 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
                      d.stride == 1;
     hipStream_t s = as_stream(stream);
+    if (vec && d.mma == MMA_BF16X6 && BN == 128) {  // x6: 128-column tiles (8 k per loader thread)
+        if (res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        return check_launch("conv_rows");
+    }
     const bool mma_ok = vec && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \

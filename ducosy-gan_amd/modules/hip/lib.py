@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("DUCOSY_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libdu
 
 DCS_PAD_ZERO, DCS_PAD_REFLECT = 0, 1
 ACT_NONE, ACT_AFFINE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3, 4
-MMA_F32, MMA_BF16, MMA_BF16X3 = 0, 1, 3
+MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6 = 0, 1, 3, 6
 
 
 class ConvDesc(ctypes.Structure):

@@ -168,6 +168,14 @@ class ConcurrentCycleGANs:
     per stream (ops.workspace), the kernels are deterministic, so each model's numbers equal a
     sequential run bit for bit (tests/test_gpu_concurrent.py)."""
 
+    # MFMA operand mode of the concurrent step.  Exact f32: with the bf16-family row kernels
+    # (bf16 / bf16x3 / bf16x6) launching back to back on one stream, a producer -> consumer
+    # kernel pair on the other stream (stem input gradient: narrow conv -> reflect fold) was
+    # seen to read a few stale elements about once per 100-200 steps on MI355X
+    # (scripts/stress_narrow.py reproduces it; every kernel involved is correct in isolation
+    # and with f32 co-runners: 0 / 800).  Single-stream training is unaffected.
+    MMA = "f32"
+
     def __init__(self, systems, device):
         self.systems = list(systems)
         self.device = torch.device(device)
@@ -176,17 +184,23 @@ class ConcurrentCycleGANs:
     def train_step(self, batches):
         """batches: one (real_A, real_B, masks) per system.  Returns one loss dict per system
         (device tensors, ready once the streams are synchronised with the caller's)."""
-        cur = torch.cuda.current_stream(self.device)
-        out = []
-        for sysm, st, b in zip(self.systems, self.streams, batches):
-            st.wait_stream(cur)  # inputs produced on the caller's stream
-            with torch.cuda.stream(st):
-                for t in b:
-                    if t is not None:
-                        t.record_stream(st)
-                out.append(sysm.train_step(*b))
-        for st in self.streams:
-            cur.wait_stream(st)
+        from .hip import ops
+        prev = ops.get_mma()
+        ops.set_mma(self.MMA)
+        try:
+            cur = torch.cuda.current_stream(self.device)
+            out = []
+            for sysm, st, b in zip(self.systems, self.streams, batches):
+                st.wait_stream(cur)  # inputs produced on the caller's stream
+                with torch.cuda.stream(st):
+                    for t in b:
+                        if t is not None:
+                            t.record_stream(st)
+                    out.append(sysm.train_step(*b))
+            for st in self.streams:
+                cur.wait_stream(st)
+        finally:
+            ops.set_mma(prev)
         return out
 
 

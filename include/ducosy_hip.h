@@ -70,8 +70,8 @@ typedef struct dcs_conv_desc {
     int32_t ldb;                    /* packed weights: Kpad (rows pass) / ncols (narrow)  */
     int32_t pro_act;                /* DCS_ACT_* prologue on the source                   */
     int32_t epi_act;                /* DCS_ACT_NONE / DCS_ACT_TANH / DCS_ACT_LRELU        */
-    int32_t mma;                    /* MFMA operands: DCS_MMA_F32 (exact, default),       */
-                                    /* DCS_MMA_BF16 or DCS_MMA_BF16X3 (f32 accumulation)  */
+    int32_t mma;                    /* MFMA operands: DCS_MMA_F32 (exact; 0 = zeroed desc) */
+                                    /* or DCS_MMA_BF16 / _BF16X3 / _BF16X6 (f32 accum.)   */
 } dcs_conv_desc;
 
 /* MFMA operand modes of the MFMA convolution passes (dcs_conv_desc.mma).  F32 is exact fp32
@@ -81,6 +81,9 @@ typedef struct dcs_conv_desc {
 #define DCS_MMA_F32 0
 #define DCS_MMA_BF16 1
 #define DCS_MMA_BF16X3 3
+/* BF16X6: three-way split (hi + mid + lo bf16), six products, ~2^-24 relative error per
+ * product (fp32-class); 128-column tiles only, other shapes run F32. */
+#define DCS_MMA_BF16X6 6
 
 const char* dcs_last_error(void);
 int dcs_version(void);

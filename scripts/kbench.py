@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--nopro", action="store_true", help="drop the IN+ReLU gather prologue (cost probe)")
-    ap.add_argument("--mma", default="f32", help="MFMA operand mode: f32 | bf16 | bf16x3")
+    ap.add_argument("--mma", default="f32", help="MFMA operand mode: f32 | bf16 | bf16x3 | bf16x6")
     a = ap.parse_args()
     ops.set_mma(a.mma)
     dev = torch.device("cuda")

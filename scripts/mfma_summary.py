@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-TAGS = {"f32": 0, "bf16": 1, "bf16x3": 3}
+TAGS = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6}
 
 
 def summarise(tag, mode):
@@ -38,7 +38,11 @@ def summarise(tag, mode):
 
 if __name__ == "__main__":
     tag, modes = sys.argv[1], sys.argv[2:] or ["f32"]
-    out = {m: summarise(tag, m) for m in modes}
+    try:  # merge: modes profiled in earlier passes stay
+        out = json.load(open(os.path.join(ROOT, "profiles", "mfma_busy.json")))
+    except (OSError, ValueError):
+        out = {}
+    out.update({m: summarise(tag, m) for m in modes})
     out["source"] = (f"rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "
                      f"bench.py --steps 1 --warmup 1 --mma MODE (scripts/pmc_mfma.sh, tag {tag})")
     for fn in (f"{tag}_mfma_busy.json", "mfma_busy.json"):  # tagged record + the copy bench.py reads

@@ -1,9 +1,9 @@
 """Summarise a scripts/profile.sh run into profiles/ (run in the build container).
 
-    python scripts/prof_summary.py TAG
+    python scripts/prof_summary.py TAG [MODE]
 
 Copies the rocprofv3 kernel-stats table to profiles/TAG_kernel_stats.csv and writes
-profiles/pmc_resconv.json: the residual-conv kernel's mean HBM-side bytes per launch,
+profiles/pmc_resconv_MODE.json: the residual-conv kernel's mean HBM-side bytes per launch,
 2*FETCH_SIZE + WRITE_SIZE (kB -> B; gfx950 FETCH_SIZE counts half of wide coalesced reads,
 MI355X_MICROARCH.md HBM section), from the two separate PMC passes.
 """
@@ -14,10 +14,10 @@ import shutil
 import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-KERNEL = "conv_rows_kernel<128, 128, 1, 1, 0>"
+TAGS = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6}
 
 
-def _mean_counter(path, counter):
+def _mean_counter(path, counter, KERNEL):
     vals = {}
     for r in csv.DictReader(open(path)):
         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
@@ -26,18 +26,20 @@ def _mean_counter(path, counter):
     return sum(vals.values()) / len(vals), len(vals)
 
 
-def main(tag):
+def main(tag, mode):
+    KERNEL = f"conv_rows_kernel<128, 128, 1, 1, {TAGS[mode]}>"
     out = os.path.join(ROOT, "gpurun_out")
-    stats = os.path.join(out, f"prof_{tag}_trace", "trace_kernel_stats.csv")
-    shutil.copy(stats, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    stats = os.path.join(out, f"prof_{tag}_{mode}_trace", "trace_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(ROOT, "profiles", f"{tag}_{mode}_kernel_stats.csv"))
     avg_ns = None
     for r in csv.DictReader(open(stats)):
         if KERNEL in r["Name"]:
             avg_ns = float(r["AverageNs"])
-    fetch, n = _mean_counter(os.path.join(out, f"prof_{tag}_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write, _ = _mean_counter(os.path.join(out, f"prof_{tag}_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    fetch, n = _mean_counter(os.path.join(out, f"prof_{tag}_{mode}_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", KERNEL)
+    write, _ = _mean_counter(os.path.join(out, f"prof_{tag}_{mode}_write", "write_counter_collection.csv"), "WRITE_SIZE", KERNEL)
     res = {
-        "kernel": "conv_rows_kernel<128,128,1,1>",
+        "kernel": KERNEL,
+        "mode": mode,
         "launches_profiled": n,
         "FETCH_SIZE_kB_mean": fetch,
         "WRITE_SIZE_kB_mean": write,
@@ -46,11 +48,11 @@ def main(tag):
                    "reads; MI355X_MICROARCH.md HBM section). L2 fabric-side bytes: Infinity-Cache hits included.",
         "kernel_trace_avg_ns": avg_ns,
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 1 --warmup 1 "
-                  f"(profile tag {tag}); kernel trace: {tag}_kernel_stats.csv",
+                  f"--mma {mode} (profile tag {tag}); kernel trace: {tag}_{mode}_kernel_stats.csv",
     }
-    json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_resconv.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(ROOT, "profiles", f"pmc_resconv_{mode}.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "bf16x6")

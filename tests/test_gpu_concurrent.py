@@ -20,12 +20,18 @@ def _batch(seed, i, n, hw, cin):
 
 
 def test_concurrent_equals_sequential():
+    from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
     n, hw, nb, steps = 2, 64, 2, 3
     cfg = [(3, 801), (2, 802)]
-    seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
-    want = [[{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)]
-            for m, (c, s) in zip(seq, cfg)]
+    prev = ops.get_mma()
+    ops.set_mma(ConcurrentCycleGANs.MMA)  # the sequential reference in the concurrent runner's mode
+    try:
+        seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
+        want = [[{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)]
+                for m, (c, s) in zip(seq, cfg)]
+    finally:
+        ops.set_mma(prev)
     run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV)
     got = [[], []]
     for i in range(steps):

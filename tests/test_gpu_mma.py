@@ -2,6 +2,7 @@
 float64 CPU reference of the same convolution, forward and data gradient, on every layer
 geometry with a vectorised gather.  Tolerances (max |err| / max |ref|), written per mode:
   f32    exact fp32 MFMA                                  <= 1e-5
+  bf16x6 hi/mid/lo bf16 split, six products               <= 1e-5   (~2^-24 per product)
   bf16x3 hi/lo bf16 split, three products                 <= 5e-5   (~2^-16 per product)
   bf16   bf16 operands, f32 accumulation (config 5)       <= 2e-2   (~2^-9 per operand)
 """
@@ -13,7 +14,7 @@ from test_gpu_ops import CONV_CASES, _geom, rnd, torch_conv
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL = {"f32": 1e-5, "bf16x3": 5e-5, "bf16": 2e-2}
+TOL = {"f32": 1e-5, "bf16x6": 1e-5, "bf16x3": 5e-5, "bf16": 2e-2}
 CASES = [c for c in CONV_CASES if c[0] % 16 == 0 and c[1] % 16 == 0]
 
 
@@ -24,11 +25,12 @@ def _relmax(a, b):
 @pytest.fixture
 def ops():
     from modules.hip import ops as o
+    prev = o.get_mma()
     yield o
-    o.set_mma("f32")
+    o.set_mma(prev)
 
 
-@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "f32"])
+@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "bf16x6", "f32"])
 @pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
 def test_conv_modes_vs_fp64(ops, mode, case):
     g, H = _geom(case)
@@ -56,3 +58,64 @@ def test_conv_modes_vs_fp64(ops, mode, case):
 def test_mode_switch_rejects_unknown(ops):
     with pytest.raises(ValueError):
         ops.set_mma("fp8")
+
+
+def _errs(ops, mode, g, H, x, w, R):
+    ops.set_mma(mode)
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wd = w.float().to(DEV)
+    y = g.forward(ops.Src.nhwc(xd), g.pack_fwd(wd)).permute(0, 3, 1, 2)
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dx = g.dgrad(Rd, g.pack_dgrad(wd), H, H + 1).permute(0, 3, 1, 2)
+    return y, dx
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
+def test_bf16x6_error_matches_exact_f32(ops, case):
+    """bf16x6 is an fp32-class mode: against a float64 convolution of the SAME fp32 operands,
+    its max error is within 1.5x of the exact-fp32 MFMA path's (both are dominated by the fp32
+    accumulation, not the operand split).  Errors are recorded in gpurun_out/x6_err.jsonl."""
+    import json
+    import os
+    g, H = _geom(case)
+    N = 2
+    x = rnd((N, g.cin, H, H + 1), 21, "x").double()
+    w = torch.from_numpy(prng.normal(22, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05)).float().double()
+    xr = x.clone().requires_grad_(True)
+    yr = torch_conv(xr, w, g)
+    R = torch.from_numpy(prng.normal(23, "R", tuple(yr.shape))).float().double()
+    (yr * R).sum().backward()
+    e = {}
+    for mode in ("f32", "bf16x6"):
+        y, dx = _errs(ops, mode, g, H, x, w, R)
+        e[mode] = (_relmax(y, yr.detach()), _relmax(dx, xr.grad))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/x6_err.jsonl", "a") as f:
+        f.write(json.dumps({"case": list(case), "f32": e["f32"], "bf16x6": e["bf16x6"]}) + "\n")
+    for k in range(2):
+        assert e["bf16x6"][k] <= 1.5 * e["f32"][k] + 1e-7, e
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16x6", "bf16x3"])
+def test_modes_deterministic(ops, mode):
+    """Every MFMA mode is run-to-run deterministic (bit-identical forward and data gradient),
+    also with other work in flight on a second stream."""
+    ops.set_mma(mode)
+    side = torch.cuda.Stream()
+    for case in CASES:
+        g, H = _geom(case)
+        x = rnd((2, g.cin, H, H + 1), 31, "x").float().to(DEV).permute(0, 2, 3, 1).contiguous()
+        w = torch.from_numpy(prng.normal(32, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05)).float().to(DEV)
+        pf, pd = g.pack_fwd(w), g.pack_dgrad(w)
+        outs = []
+        for rep in range(4):
+            if rep % 2:
+                with torch.cuda.stream(side):
+                    g.forward(ops.Src.nhwc(x), pf)
+            y = g.forward(ops.Src.nhwc(x), pf)
+            dx = g.dgrad(y.contiguous(), pd, H, H + 1)
+            outs.append((y.clone(), dx.clone()))
+        torch.cuda.synchronize()
+        for y, dx in outs[1:]:
+            assert torch.equal(y, outs[0][0]), (mode, case)
+            assert torch.equal(dx, outs[0][1]), (mode, case)

@@ -113,7 +113,7 @@ def test_optimizer_state_dict_roundtrip():
     assert opt2._t == 2
 
 
-@pytest.mark.parametrize("mode,tol0", [("bf16x3", 1e-3), ("bf16", 3e-2)])
+@pytest.mark.parametrize("mode,tol0", [("bf16x6", 1e-3), ("bf16x3", 1e-3), ("bf16", 3e-2)])
 def test_train_step_mma_modes_vs_reference_golden(mode, tol0):
     """The MFMA operand modes on the reference-generated step fixture: bf16x3 keeps the fp32
     bar (1e-3 rel on step-0 losses); bf16 (BASELINE config 5's half-precision path) is held to
@@ -129,7 +129,7 @@ def test_train_step_mma_modes_vs_reference_golden(mode, tol0):
             rB = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
             mk = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, hw, hw), 0.3)).to(DEV)
             out = {k: float(v) for k, v in s.train_step(rA, rB, mk).items()}
-            tol = tol0 if i == 0 else (1e-2 if mode == "bf16x3" else 3e-2)
+            tol = tol0 if i == 0 else (3e-2 if mode == "bf16" else 1e-2)
             for k, v in out.items():
                 scale = float(z[k][i]) if i == 0 else max(abs(float(z[k][i])), abs(float(z[k][0])))
                 assert abs(v - float(z[k][i])) <= tol * max(scale, 1e-2), (mode, i, k, v, float(z[k][i]))
