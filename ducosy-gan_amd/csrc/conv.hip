@@ -76,6 +76,12 @@ constexpr int NT = 256;
 #ifndef DCS_X6_BK
 #define DCS_X6_BK 16
 #endif
+#ifndef DCS_WGRAD_X6
+#define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
+#endif
+#ifndef DCS_X6_OCC
+#define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
+#endif
 
 // ---------------------------------------------------------------------------------------
 // geometry helpers
@@ -431,7 +437,7 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
 // VEC: 0 scalar gather (any layout), 1 = 16 consecutive k of one tap per thread (Cs % 16 == 0),
 //      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
 template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
-__global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
+__global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy) {
@@ -452,7 +458,11 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     // 112 B keep the 16-B fragment reads conflict-free
     constexpr int NPL = MMA == MMA_BF16X6 ? 3 : (MMA == MMA_BF16X3 ? 2 : 1);
     constexpr int LDE = NPL * BKT + 8;
-    constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK : (BM + BN) * LDE;
+    // x6: three planes [plane][buf][BM+BN rows][16 bf16], the 16-B halves of a row swapped on
+    // odd groups of 8 rows, so both the 8-lane ds_write_b128 groups and the 16-lane
+    // ds_read_b128 groups hit 64 distinct banks (MI355X_MICROARCH.md LDS table)
+    constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK
+                             : MMA == MMA_BF16X6 ? 3 * 2 * (BM + BN) * 16 / 2 : (BM + BN) * LDE;
 
     // f32: As[2][BM][LDK] | Bs[2][BN][LDK];  bf16 modes: Ah[2][BM][LDE] | Bh[2][BN][LDE]
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
@@ -460,6 +470,10 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
     auto Bs = reinterpret_cast<float (*)[BN][LDK]>(lds + 2 * BM * LDK);
     __bf16* const Ah = reinterpret_cast<__bf16*>(lds);
     __bf16* const Bh = Ah + 2 * BM * LDE;
+    // x6 plane offset (bf16 elements) of (plane, buffer, tile row, 8-k half)
+    auto x6o = [](int pl, int buf, int row, int h) {
+        return ((pl * 2 + buf) * (BM + BN) + row) * 16 + 8 * (h ^ ((row >> 3) & 1));
+    };
     __shared__ long long rowoff[BM];
 
     const int T = gridDim.x;
@@ -602,24 +616,16 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
 #pragma unroll
             for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
         } else if constexpr (MMA == MMA_BF16X6) {
-            static_assert(ACH % 2 == 0 && BCH % 2 == 0, "x6 tiles: groups of 8 k per loader thread");
+            static_assert(BKT == 16 && ACH == 2 && BCH == 2, "x6 tiles: 16 k, 8 per loader thread");
             bf16x8 hi, mid, lo;
-            __bf16* a = Ah + (buf * BM + arow) * LDE + akq;
-#pragma unroll
-            for (int i = 0; i < ACH / 2; ++i) {
-                split8x3(ra[2 * i], ra[2 * i + 1], hi, mid, lo);
-                *reinterpret_cast<bf16x8*>(a + 8 * i) = hi;
-                *reinterpret_cast<bf16x8*>(a + BKT + 8 * i) = mid;
-                *reinterpret_cast<bf16x8*>(a + 2 * BKT + 8 * i) = lo;
-            }
-            __bf16* b = Bh + (buf * BN + brow) * LDE + bkq;
-#pragma unroll
-            for (int i = 0; i < BCH / 2; ++i) {
-                split8x3(rb[2 * i], rb[2 * i + 1], hi, mid, lo);
-                *reinterpret_cast<bf16x8*>(b + 8 * i) = hi;
-                *reinterpret_cast<bf16x8*>(b + BKT + 8 * i) = mid;
-                *reinterpret_cast<bf16x8*>(b + 2 * BKT + 8 * i) = lo;
-            }
+            split8x3(ra[0], ra[1], hi, mid, lo);
+            *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, arow, akq >> 3)) = hi;
+            *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, arow, akq >> 3)) = mid;
+            *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, arow, akq >> 3)) = lo;
+            split8x3(rb[0], rb[1], hi, mid, lo);
+            *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
+            *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
+            *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, BM + brow, bkq >> 3)) = lo;
         } else {
             bf16x8 hi, lo;
             __bf16* a = Ah + (buf * BM + arow) * LDE;
@@ -664,22 +670,28 @@ __global__ __launch_bounds__(NT, 2) void conv_rows_kernel(
                 bf16x8 ah[IM], bh[JN], al[IM], bl[JN], am[IM], bm[JN];
 #pragma unroll
                 for (int i = 0; i < IM; ++i) {
-                    const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
-                    ah[i] = *reinterpret_cast<const bf16x8*>(a);
-                    if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
                     if constexpr (MMA == MMA_BF16X6) {
-                        am[i] = *reinterpret_cast<const bf16x8*>(a + BKT);
-                        al[i] = *reinterpret_cast<const bf16x8*>(a + 2 * BKT);
+                        const int row = wm * WM + i * 32 + l32;
+                        ah[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
+                        am[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
+                        al[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
+                    } else {
+                        const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
+                        ah[i] = *reinterpret_cast<const bf16x8*>(a);
+                        if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
                     }
                 }
 #pragma unroll
                 for (int j = 0; j < JN; ++j) {
-                    const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
-                    bh[j] = *reinterpret_cast<const bf16x8*>(b);
-                    if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
                     if constexpr (MMA == MMA_BF16X6) {
-                        bm[j] = *reinterpret_cast<const bf16x8*>(b + BKT);
-                        bl[j] = *reinterpret_cast<const bf16x8*>(b + 2 * BKT);
+                        const int row = BM + wn * WN + j * 32 + l32;
+                        bh[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
+                        bm[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
+                        bl[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
+                    } else {
+                        const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
+                        bh[j] = *reinterpret_cast<const bf16x8*>(b);
+                        if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
                     }
                 }
 #pragma unroll
@@ -1567,6 +1579,199 @@ __global__ void wgrad_subpixel_fold_kernel(const float* __restrict__ ws, int nsp
     dw[idx] = s;
 }
 
+// bf16x6 weight gradient (dcs_conv_desc.mma == DCS_MMA_BF16X6, vectorised sources, parity 0):
+// dW[co][(tap, ci)] = sum_p dy[p][co] * src(p + tap)[ci] with each fp32 operand split into
+// hi + mid + lo bf16 (split8x3) once, when the tile is staged, and the six products of the
+// rows pass on v_mfma_f32_32x32x16_bf16.  Both operands are staged pixel-major
+// ([16 pixels][128 columns] per plane, as they arrive from HBM); the MFMA wants 8 consecutive
+// pixels of one column per lane, which ds_read_b64_tr_b16 delivers from that image (two 4-row
+// transposed reads per fragment, cdna_hip_programming.md T10).  Row pitch 320 B: the 8-lane
+// ds_write_b128 groups and the 32-lane transposed-read halves both cover all banks.  Same
+// pixel walk, split partition (16-pixel tiles, twice the count) and partial slabs as
+// conv_wgrad_kernel.
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
+
+template <int TAG>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
+    const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
+    const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws, int kt_per_split,
+    int gn, int gm) {
+    const dcs_conv_desc d = specialise<TAG>(din);
+    constexpr int BM = 128, BN = 128, BKP = 16;  // output channels x (tap, ci) columns x pixels per k-tile
+    constexpr int WM = BM / 2, WN = BN / 2, IM = WM / 32, JN = WN / 32;
+    constexpr int PITCH = 160;                   // bf16 per LDS row
+    constexpr int KT2 = 8;                       // k-tiles per inner accumulation chain (128 pixels)
+    __shared__ __attribute__((aligned(16))) __bf16 X[2 * 3 * 2 * BKP * PITCH];  // [A|B][plane][buf][pix][col]
+    auto xo = [](int op, int pl, int buf, int pix, int col) {
+        return (((op * 3 + pl) * 2 + buf) * BKP + pix) * PITCH + col;
+    };
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = L % gn;
+    const int mtile = (L / gn) % gm;
+    const int split = L / (gn * gm);
+    const ClassGeom g = class_geom(d, 0);
+    const long long P = (long long)g.My * g.Mx * d.N;
+    const int Ktot = g.ntaps * d.Cs;
+    const int m0 = mtile * BM, n0 = ntile * BN;
+    const long long nkt_all = (P + BKP - 1) / BKP;
+    const long long kt_beg = (long long)split * kt_per_split;
+    long long kt_end = kt_beg + kt_per_split;
+    if (kt_end > nkt_all) kt_end = nkt_all;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int kr = tid >> 4;        // the tile's pixel row this thread stages
+    const int cc = (tid & 15) * 8;  // its 8 columns (of A: output channels; of B: (tap, ci))
+    const int nb0 = n0 + cc;
+    const bool bcol_ok = nb0 < Ktot;
+    int bady = 0, badx = 0, bchan = 0;
+    if (bcol_ok) {  // the 8 columns share one tap (Cs % 16 == 0)
+        const int j = nb0 / d.Cs;
+        bchan = nb0 - j * d.Cs;
+        int bt;
+        tap_decode(d, g, j, bady, badx, bt);
+    }
+    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
+    const __amdgpu_buffer_rsrc_t rsrc = src_rsrc(src);
+    int pn = 0, pqy = 0, pqx = 0;  // pixel of the next k-tile row this thread loads
+    {
+        const long long p = kt_beg * BKP + kr;
+        if (p < P) {
+            const int per = g.My * g.Mx;
+            pn = (int)(p / per);
+            const int rem = (int)(p - (long long)pn * per);
+            pqy = rem / g.Mx;
+            pqx = rem - pqy * g.Mx;
+        }
+    }
+    float4 ra[2], rb[2];
+    auto load = [&](long long kt) {
+        const long long p = kt * BKP + kr;
+        const bool pok = p < P;
+        const int co = m0 + cc;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            ra[i] = (pok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        int sy, sx;
+        const bool yok = map_coord_sel(pqy * d.stride - d.pt + bady, Hv, d.up, d.pad_mode, sy);
+        const bool xok = map_coord_sel(pqx * d.stride - d.pl + badx, Wv, d.up, d.pad_mode, sx);
+        const bool ok = pok && bcol_ok && yok && xok;
+        const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) rb[i] = buf_load4(rsrc, off + 16 * i);
+        if (d.pro_act != DCS_ACT_NONE && ok) {
+            const long long o = (long long)pn * d.Cs + bchan;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) rb[i] = affine_act4(rb[i], psc + o + 4 * i, psh + o + 4 * i, d.pro_act);
+        }
+        pqx += BKP;
+        while (pqx >= g.Mx) {
+            pqx -= g.Mx;
+            if (++pqy == g.My) { pqy = 0; ++pn; }
+        }
+    };
+    auto store = [&](int buf) {
+        bf16x8 hi, mid, lo;
+        split8x3(ra[0], ra[1], hi, mid, lo);
+        *reinterpret_cast<bf16x8*>(X + xo(0, 0, buf, kr, cc)) = hi;
+        *reinterpret_cast<bf16x8*>(X + xo(0, 1, buf, kr, cc)) = mid;
+        *reinterpret_cast<bf16x8*>(X + xo(0, 2, buf, kr, cc)) = lo;
+        split8x3(rb[0], rb[1], hi, mid, lo);
+        *reinterpret_cast<bf16x8*>(X + xo(1, 0, buf, kr, cc)) = hi;
+        *reinterpret_cast<bf16x8*>(X + xo(1, 1, buf, kr, cc)) = mid;
+        *reinterpret_cast<bf16x8*>(X + xo(1, 2, buf, kr, cc)) = lo;
+    };
+    // transposed fragment of columns col0 .. col0+31, all 16 pixels: lane (r, h) receives
+    // pixels 8h .. 8h+7 of column col0 + r.  In a 16-lane group, lane 4q+p addresses pixel
+    // row q (+4 for the second read), columns 4p .. 4p+3.
+    const int g16 = lane >> 4;
+    const int rpix = 8 * (g16 >> 1) + ((lane & 15) >> 2);
+    const int rcol = 16 * (g16 & 1) + 4 * (lane & 3);
+    auto frag = [&](int op, int pl, int buf, int col0) {
+        const __bf16* p0 = X + xo(op, pl, buf, rpix, col0 + rcol);
+        const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(p0));
+        const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(p0 + 4 * PITCH));
+        const shortx8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, c);
+    };
+
+    floatx16 acc[IM][JN], t[IM][JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
+
+    if (kt_beg < kt_end) {
+        load(kt_beg);
+        store(0);
+    }
+    __syncthreads();
+    for (long long kt = kt_beg; kt < kt_end; ++kt) {
+        const int cur = (int)((kt - kt_beg) & 1);
+        bf16x8 ah[IM], am[IM], al[IM], bh[JN], bm[JN], bl[JN];
+#pragma unroll
+        for (int i = 0; i < IM; ++i) {
+            const int c0 = wm * WM + i * 32;
+            ah[i] = frag(0, 0, cur, c0);
+            am[i] = frag(0, 1, cur, c0);
+            al[i] = frag(0, 2, cur, c0);
+        }
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+            const int c0 = wn * WN + j * 32;
+            bh[j] = frag(1, 0, cur, c0);
+            bm[j] = frag(1, 1, cur, c0);
+            bl[j] = frag(1, 2, cur, c0);
+        }
+        if (kt + 1 < kt_end) load(kt + 1);
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {  // smallest terms first, as in the rows pass
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], t[i][j], 0, 0, 0);
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], t[i][j], 0, 0, 0);
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], t[i][j], 0, 0, 0);
+                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+            }
+        const long long rel = kt - kt_beg;
+        if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    acc[i][j] += t[i][j];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                }
+        }
+        if (kt + 1 < kt_end) store(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* slab = ws + (long long)split * d.Co * Ktot;
+    const int l32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + l32;
+        if (col >= Ktot) continue;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (row < d.Co) slab[(long long)row * Ktot + col] = acc[i][j][r];
+            }
+    }
+}
+
 struct WgradPlan {
     int BM, BN, nsplit, kt_per_split;
     long long Ktot;
@@ -1652,6 +1857,10 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+    } else if (d.mma == MMA_BF16X6 && vec && p.BM == 128 && !d.parity && DCS_WGRAD_X6) {
+        // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs
+        if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
     } else if (p.BM == 128) {
         if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
         else if (vec) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);

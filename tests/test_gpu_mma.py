@@ -67,13 +67,14 @@ def _errs(ops, mode, g, H, x, w, R):
     y = g.forward(ops.Src.nhwc(xd), g.pack_fwd(wd)).permute(0, 3, 1, 2)
     Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dx = g.dgrad(Rd, g.pack_dgrad(wd), H, H + 1).permute(0, 3, 1, 2)
-    return y, dx
+    dw = g.wgrad(Rd, ops.Src.nhwc(xd))
+    return y, dx, dw
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
 def test_bf16x6_error_matches_exact_f32(ops, case):
     """bf16x6 is an fp32-class mode: against a float64 convolution of the SAME fp32 operands,
-    its max error is within 1.5x of the exact-fp32 MFMA path's (both are dominated by the fp32
+    its max error (forward, data and weight gradient) is within 1.5x of the exact-fp32 MFMA path's (both are dominated by the fp32
     accumulation, not the operand split).  Errors are recorded in gpurun_out/x6_err.jsonl."""
     import json
     import os
@@ -82,17 +83,18 @@ def test_bf16x6_error_matches_exact_f32(ops, case):
     x = rnd((N, g.cin, H, H + 1), 21, "x").double()
     w = torch.from_numpy(prng.normal(22, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05)).float().double()
     xr = x.clone().requires_grad_(True)
-    yr = torch_conv(xr, w, g)
+    wr = w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, g)
     R = torch.from_numpy(prng.normal(23, "R", tuple(yr.shape))).float().double()
     (yr * R).sum().backward()
     e = {}
     for mode in ("f32", "bf16x6"):
-        y, dx = _errs(ops, mode, g, H, x, w, R)
-        e[mode] = (_relmax(y, yr.detach()), _relmax(dx, xr.grad))
+        y, dx, dw = _errs(ops, mode, g, H, x, w, R)
+        e[mode] = (_relmax(y, yr.detach()), _relmax(dx, xr.grad), _relmax(dw, wr.grad))
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/x6_err.jsonl", "a") as f:
         f.write(json.dumps({"case": list(case), "f32": e["f32"], "bf16x6": e["bf16x6"]}) + "\n")
-    for k in range(2):
+    for k in range(3):  # forward, data gradient, weight gradient
         assert e["bf16x6"][k] <= 1.5 * e["f32"][k] + 1e-7, e
 
 
