@@ -191,13 +191,13 @@ __global__ void box_adjoint_kernel(const float* __restrict__ g, int N, int H, in
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(RB) void cr_loss_kernel(const float* __restrict__ p, const float* __restrict__ t,
                                                      const float* __restrict__ s, int N, int H, int W, float thr,
-                                                     float* __restrict__ gq, double* part) {
+                                                     float* __restrict__ gq, double* part, long long nq_norm) {
     // quantities: 0 region sum, 1 sum p, 2 sum p^2, 3 sum t, 4 sum t^2
     double acc[5] = {0, 0, 0, 0, 0};
     const int Hp = H / 8, Wp = W / 8;
     const long long nq = (long long)N * Hp * Wp;
     const long long n = (long long)N * H * W;
-    const float invq = nq > 0 ? 1.f / (float)nq : 0.f;
+    const float invq = nq_norm > 0 ? 1.f / (float)nq_norm : 1.f;  // nq_norm 0: gq unnormalised
     for (long long e = (long long)blockIdx.x * RB + threadIdx.x; e < n; e += (long long)gridDim.x * RB) {
         float pv = p[e], tv = t[e];
         acc[1] += pv; acc[2] += (double)pv * pv;
@@ -240,6 +240,7 @@ __global__ void cr_loss_final(const double* part, int nb, long long n, long long
     double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
     sc[2] = (float)(0.5 * weight * sg1 / n);
     sc[3] = (float)(sp > 0 ? 0.5 * weight * sg2 / ((n - 1) * sp) : 0.0);
+    sc[5] = 1.f;  // gq already carries 1/nq
 }
 
 __global__ void cr_grad_kernel(const float* __restrict__ p, const float* __restrict__ gq, const float* __restrict__ sc,
@@ -253,7 +254,7 @@ __global__ void cr_grad_kernel(const float* __restrict__ p, const float* __restr
     int nn = (int)(r / H);
     const int Hp = H / 8, Wp = W / 8;
     float g = sc[2] + sc[3] * (p[e] - sc[0]);
-    if (i < Hp * 8 && j < Wp * 8) g += weight * gq[((long long)nn * Hp + i / 8) * Wp + j / 8] / 64.f;
+    if (i < Hp * 8 && j < Wp * 8) g += weight * sc[5] * gq[((long long)nn * Hp + i / 8) * Wp + j / 8] / 64.f;
     grad[e] = g;
 }
 
@@ -419,6 +420,92 @@ __global__ void edge_grad_kernel(const float* __restrict__ gx, const float* __re
             }
         }
     grad[e] = g;
+}
+
+// ---------------------------------------------------------------------------------------
+// Global statistics of the batch-coupled losses over data-parallel ranks (SURVEY.md §8e
+// option ii).  The phases below leave this shard's partial sums in a caller buffer `red`
+// (double) or a 512-bin histogram; the caller sums them over ranks between the phases (one
+// all-reduce each), and the next phase reads the sums back, so every rank finishes with the
+// loss of the WHOLE batch.  The partials are the same quantities the one-call path reduces.
+// ---------------------------------------------------------------------------------------
+// red[r0 + q] = sum of partial q over nb blocks (q < K); optional counts after them
+__global__ void red_sum_kernel(const double* part, int nb, int K, double* red, int r0, double c0, double c1, int nc) {
+    for (int q = 0; q < K; ++q) {
+        const double v = sum_parts(part, nb, q);
+        if (threadIdx.x == 0) red[r0 + q] = v;
+    }
+    if (threadIdx.x == 0) {
+        if (nc > 0) red[r0 + K] = c0;
+        if (nc > 1) red[r0 + K + 1] = c1;
+    }
+}
+
+// region: red = {region sum, sum p, sum p^2, sum t, sum t^2, n, nq} over all ranks
+__global__ void cr_final_red_kernel(const double* red, float weight, float grad_scale, float* sc, float* out) {
+    if (threadIdx.x != 0) return;
+    const double n = red[5], nq = red[6];
+    const double mp = red[1] / n, mt = red[3] / n;
+    const double sp = sqrt(fmax((red[2] - n * mp * mp) / (n - 1), 0.0));
+    const double st = sqrt(fmax((red[4] - n * mt * mt) / (n - 1), 0.0));
+    const double region = nq > 0 ? red[0] / nq : 0.0;
+    out[0] = (float)(weight * (region + 0.5 * (fabs(mp - mt) + fabs(sp - st))));
+    const double sg1 = (mp > mt) ? 1.0 : ((mp < mt) ? -1.0 : 0.0);
+    const double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
+    sc[0] = (float)mp;
+    sc[1] = (float)sp;
+    sc[2] = (float)(grad_scale * 0.5 * weight * sg1 / n);
+    sc[3] = (float)(sp > 0 ? grad_scale * 0.5 * weight * sg2 / ((n - 1) * sp) : 0.0);
+    sc[5] = (float)(nq > 0 ? grad_scale / nq : 0.0);  // gq holds m * sign, unnormalised
+}
+
+// edge: red = {sum ep, sum ep^2, sum et, sum et^2, n, sum ep>tau_p, #ep==tau_p, sum et>tau_t, #et==tau_t}
+__device__ __forceinline__ long long edge_k(double n) { return (long long)(n * 0.1); }  // int(numel * 0.1)
+
+__global__ void edge_radix_init_kernel(unsigned* st_p, unsigned* st_t, const double* red) {
+    if (threadIdx.x == 0) {
+        const unsigned k = (unsigned)edge_k(red[4]);
+        st_p[0] = 0u; st_p[1] = k;
+        st_t[0] = 0u; st_t[1] = k;
+    }
+}
+
+// radix select step from a (summed) histogram, without clearing it (it is the caller's)
+__global__ void radix_select_const_kernel(unsigned* st, int shift, const unsigned* hist) {
+    if (threadIdx.x == 0) {
+        const unsigned k = st[1];
+        unsigned cum = 0u;
+        int b = 255;
+        for (; b > 0; --b) {
+            if (cum + hist[b] >= k) break;
+            cum += hist[b];
+        }
+        st[0] |= ((unsigned)b << shift);
+        st[1] = k - cum;
+    }
+}
+
+__global__ void edge_final_red_kernel(const double* red, const unsigned* st_p, const unsigned* st_t, float grad_scale,
+                                      float* sc, float* out) {
+    if (threadIdx.x != 0) return;
+    const double n = red[4];
+    const double k = (double)edge_k(n);
+    const double mp = red[0] / n, mt = red[2] / n;
+    const double sp = sqrt(fmax((red[1] - n * mp * mp) / (n - 1), 0.0));
+    const double st = sqrt(fmax((red[3] - n * mt * mt) / (n - 1), 0.0));
+    const double taup = (double)__uint_as_float(st_p[0]), taut = (double)__uint_as_float(st_t[0]);
+    const double tkp = (red[5] + (double)st_p[1] * taup) / k;
+    const double tkt = (red[7] + (double)st_t[1] * taut) / k;
+    out[0] = (float)(fabs(mp - mt) + fabs(sp - st) + fabs(tkp - tkt));
+    const double sg1 = (mp > mt) ? 1.0 : ((mp < mt) ? -1.0 : 0.0);
+    const double sg2 = (sp > st) ? 1.0 : ((sp < st) ? -1.0 : 0.0);
+    const double sg3 = (tkp > tkt) ? 1.0 : ((tkp < tkt) ? -1.0 : 0.0);
+    sc[0] = __uint_as_float(st_p[0]);
+    sc[1] = (float)(red[6] > 0 ? (double)st_p[1] / red[6] : 0.0);
+    sc[2] = (float)(grad_scale * sg1 / n);
+    sc[3] = (float)(sp > 0 ? grad_scale * sg2 / ((n - 1) * sp) : 0.0);
+    sc[4] = (float)mp;
+    sc[5] = (float)(grad_scale * sg3 / k);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -644,7 +731,8 @@ extern "C" int dcs_loss_contrast_region(const float* pred, const float* target, 
     long long nq = (long long)N * (H / 8) * (W / 8);
     int nb = red_blocks(n);
     float* gq = w.maps;
-    hipLaunchKernelGGL(cr_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, source, N, H, W, threshold, gq, w.part);
+    hipLaunchKernelGGL(cr_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, source, N, H, W, threshold, gq, w.part,
+                       nq);
     hipLaunchKernelGGL(cr_loss_final, dim3(1), dim3(64), 0, s, w.part, nb, n, nq, weight, w.sc, out);
     if (grad)
         hipLaunchKernelGGL(cr_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, pred, gq, w.sc, N, H, W, weight,
@@ -694,6 +782,118 @@ extern "C" int dcs_loss_contrast_edge(const float* pred, const float* target, in
         hipLaunchKernelGGL(edge_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, gx, gy, N, H, W, grad);
     }
     return check_launch("loss_contrast_edge");
+}
+
+extern "C" int dcs_loss_contrast_region_partial(const float* pred, const float* target, const float* source, int N,
+                                                int H, int W, float threshold, double* red, void* ws, size_t ws_bytes,
+                                                void* stream) {
+    if (!pred || !target || !source || !red || N <= 0 || H <= 0 || W <= 0)
+        return fail(DCS_E_INVALID, "loss_contrast_region_partial: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W, nq = (long long)N * (H / 8) * (W / 8);
+    const int nb = red_blocks(n);
+    // gq = m * sign(p - t), unnormalised: the batch's nq is only known after the reduction
+    hipLaunchKernelGGL(cr_loss_kernel, dim3(nb), dim3(RB), 0, s, pred, target, source, N, H, W, threshold, w.maps,
+                       w.part, 0LL);
+    hipLaunchKernelGGL(red_sum_kernel, dim3(1), dim3(64), 0, s, w.part, nb, 5, red, 0, (double)n, (double)nq, 2);
+    return check_launch("loss_contrast_region_partial");
+}
+
+extern "C" int dcs_loss_contrast_region_finish(const float* pred, int N, int H, int W, float weight, const double* red,
+                                               float grad_scale, float* out, float* grad, void* ws, size_t ws_bytes,
+                                               void* stream) {
+    if (!pred || !red || !out || N <= 0 || H <= 0 || W <= 0)
+        return fail(DCS_E_INVALID, "loss_contrast_region_finish: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W;
+    hipLaunchKernelGGL(cr_final_red_kernel, dim3(1), dim3(64), 0, s, red, weight, grad_scale, w.sc, out);
+    if (grad)
+        hipLaunchKernelGGL(cr_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, pred, w.maps, w.sc, N, H, W,
+                           weight, grad);
+    return check_launch("loss_contrast_region_finish");
+}
+
+extern "C" int dcs_loss_contrast_edge_partial(const float* pred, const float* target, int N, int H, int W, double* red,
+                                              void* ws, size_t ws_bytes, void* stream) {
+    if (!pred || !target || !red || N <= 0 || H <= 0 || W <= 0)
+        return fail(DCS_E_INVALID, "loss_contrast_edge_partial: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W;
+    const int nb = red_blocks(n);
+    float* ep = w.maps;
+    hipLaunchKernelGGL(edge_maps_kernel, dim3(nb), dim3(RB), 0, s, pred, target, N, H, W, ep, ep + n, w.part);
+    hipLaunchKernelGGL(red_sum_kernel, dim3(1), dim3(64), 0, s, w.part, nb, 4, red, 0, (double)n, 0.0, 1);
+    return check_launch("loss_contrast_edge_partial");
+}
+
+extern "C" int dcs_loss_contrast_edge_hist(int N, int H, int W, int pass, const double* red, uint32_t* hist, void* ws,
+                                           size_t ws_bytes, void* stream) {
+    if (!red || !hist || N <= 0 || H <= 0 || W <= 0 || pass < 0 || pass > 3)
+        return fail(DCS_E_INVALID, "loss_contrast_edge_hist: bad arguments (pass 0..3)");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W;
+    const int nb = red_blocks(n);
+    if (pass == 0) hipLaunchKernelGGL(edge_radix_init_kernel, dim3(1), dim3(64), 0, s, w.st, w.st + 4, red);
+    const hipError_t me = hipMemsetAsync(hist, 0, 512 * sizeof(uint32_t), s);
+    if (me != hipSuccess) return fail((int)me, "loss_contrast_edge_hist: memset failed");
+    const int shift = 24 - 8 * pass;
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(nb), dim3(RB), 0, s, w.maps, n, shift, w.st, hist);
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(nb), dim3(RB), 0, s, w.maps + n, n, shift, w.st + 4, hist + 256);
+    return check_launch("loss_contrast_edge_hist");
+}
+
+extern "C" int dcs_loss_contrast_edge_select(int pass, const uint32_t* hist, void* ws, size_t ws_bytes, void* stream) {
+    if (!hist || !ws || ws_bytes < loss_ws_fixed() || pass < 0 || pass > 3)
+        return fail(DCS_E_INVALID, "loss_contrast_edge_select: bad arguments (pass 0..3)");
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const int shift = 24 - 8 * pass;
+    hipLaunchKernelGGL(radix_select_const_kernel, dim3(1), dim3(64), 0, s, w.st, shift, hist);
+    hipLaunchKernelGGL(radix_select_const_kernel, dim3(1), dim3(64), 0, s, w.st + 4, shift, hist + 256);
+    return check_launch("loss_contrast_edge_select");
+}
+
+extern "C" int dcs_loss_contrast_edge_topk(int N, int H, int W, double* red, void* ws, size_t ws_bytes, void* stream) {
+    if (!red || N <= 0 || H <= 0 || W <= 0) return fail(DCS_E_INVALID, "loss_contrast_edge_topk: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W;
+    const int nb = red_blocks(n);
+    hipLaunchKernelGGL(topk_sum_kernel, dim3(nb), dim3(RB), 0, s, w.maps, n, w.st, w.part);
+    hipLaunchKernelGGL(red_sum_kernel, dim3(1), dim3(64), 0, s, w.part, nb, 2, red, 5, 0.0, 0.0, 0);
+    hipLaunchKernelGGL(topk_sum_kernel, dim3(nb), dim3(RB), 0, s, w.maps + n, n, w.st + 4, w.part);
+    hipLaunchKernelGGL(red_sum_kernel, dim3(1), dim3(64), 0, s, w.part, nb, 2, red, 7, 0.0, 0.0, 0);
+    return check_launch("loss_contrast_edge_topk");
+}
+
+extern "C" int dcs_loss_contrast_edge_finish(const float* pred, int N, int H, int W, const double* red,
+                                             float grad_scale, float* out, float* grad, void* ws, size_t ws_bytes,
+                                             void* stream) {
+    if (!pred || !red || !out || N <= 0 || H <= 0 || W <= 0)
+        return fail(DCS_E_INVALID, "loss_contrast_edge_finish: bad arguments");
+    LOSS_CHECK_WS(N, H, W);
+    LossWs w = loss_ws(ws);
+    hipStream_t s = as_stream(stream);
+    const long long n = (long long)N * H * W;
+    float* ep = w.maps;
+    float* gx = ep + 2 * n;
+    float* gy = gx + n;
+    hipLaunchKernelGGL(edge_final_red_kernel, dim3(1), dim3(64), 0, s, red, w.st, w.st + 4, grad_scale, w.sc, out);
+    if (grad) {
+        hipLaunchKernelGGL(edge_grad_maps_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, pred, ep, w.sc, N, H, W,
+                           gx, gy);
+        hipLaunchKernelGGL(edge_grad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, gx, gy, N, H, W, grad);
+    }
+    return check_launch("loss_contrast_edge_finish");
 }
 
 extern "C" int dcs_loss_ssim(const float* X, const float* Y, int N, int H, int W, float data_range, int win,

@@ -22,6 +22,9 @@ def _add_build_train_flags(p: argparse.ArgumentParser):
     g.add_argument("--max_steps_per_epoch", type=int, default=0, help="cap on steps per epoch (0 = full epoch)")
     g.add_argument("--log_every", type=int, default=10, help="print losses every N steps (rank 0)")
     g.add_argument("--seed", type=int, default=0, help="torch seed for weight initialisation")
+    g.add_argument("--global_loss_stats", action="store_true",
+                   help="at N GPUs, compute the batch-coupled losses (ContrastRegion, ContrastEdge) over the "
+                        "whole data-parallel batch (the reference's single-process semantics) instead of per rank")
 
 
 def get_common_infer_args(argv=None):

@@ -68,6 +68,13 @@ SIGNATURES = {
     "dcs_loss_contrast_region": (c_int, [P, P, P, c_int, c_int, c_int, c_float, c_float, P, P, P,
                                          c_size_t, P]),
     "dcs_loss_contrast_edge": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_size_t, P]),
+    "dcs_loss_contrast_region_partial": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, c_size_t, P]),
+    "dcs_loss_contrast_region_finish": (c_int, [P, c_int, c_int, c_int, c_float, P, c_float, P, P, P, c_size_t, P]),
+    "dcs_loss_contrast_edge_partial": (c_int, [P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
+    "dcs_loss_contrast_edge_hist": (c_int, [c_int, c_int, c_int, c_int, P, P, P, c_size_t, P]),
+    "dcs_loss_contrast_edge_select": (c_int, [c_int, P, P, c_size_t, P]),
+    "dcs_loss_contrast_edge_topk": (c_int, [c_int, c_int, c_int, P, P, c_size_t, P]),
+    "dcs_loss_contrast_edge_finish": (c_int, [P, c_int, c_int, c_int, P, c_float, P, P, P, c_size_t, P]),
     "dcs_loss_ssim": (c_int, [P, P, c_int, c_int, c_int, c_float, c_int, c_float, c_float, c_float,
                               P, P, P, c_size_t, P]),
     "dcs_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_float,

@@ -546,6 +546,53 @@ def loss_contrast_edge(pred, target, want_grad=True):
                       want_grad)
 
 
+def loss_contrast_region_global(pred, target, source, threshold, weight, allreduce, grad_scale, want_grad=True):
+    """ContrastRegionLoss of the WHOLE data-parallel batch (SURVEY.md §8e option ii): this
+    shard's partial sums, ``allreduce`` (in-place sum over ranks), then the whole-batch value
+    and this shard's gradient times ``grad_scale``.  With an identity ``allreduce`` and
+    grad_scale 1 it equals loss_contrast_region."""
+    p, t, s = pred.contiguous(), target.contiguous(), source.contiguous()
+    _check_dev(p, t, s)
+    N, H, W = _plane_dims(p)
+    dev = p.device
+    ws = workspace(lib.query("dcs_loss_workspace_size", N, H, W), dev)  # one buffer for both phases
+    red = torch.zeros(8, device=dev, dtype=torch.float64)
+    lib.call("dcs_loss_contrast_region_partial", _p(p), _p(t), _p(s), N, H, W, float(threshold), _p(red), _p(ws),
+             ws.numel(), _stream())
+    allreduce(red)
+    out = torch.empty(1, device=dev, dtype=torch.float32)
+    grad = torch.empty_like(p) if want_grad else None
+    lib.call("dcs_loss_contrast_region_finish", _p(p), N, H, W, float(weight), _p(red), float(grad_scale), _p(out),
+             _p(grad), _p(ws), ws.numel(), _stream())
+    return out.view(()), grad
+
+
+def loss_contrast_edge_global(pred, target, allreduce, grad_scale, want_grad=True):
+    """ContrastEdgeLoss of the WHOLE data-parallel batch: Sobel-magnitude mean/std and the exact
+    top-10 % mean by a radix select whose four 256-bin histograms are summed over ranks.  Six
+    small all-reduces per evaluation; no host synchronisation."""
+    p, t = pred.contiguous(), target.contiguous()
+    _check_dev(p, t)
+    N, H, W = _plane_dims(p)
+    dev = p.device
+    ws = workspace(lib.query("dcs_loss_workspace_size", N, H, W), dev)
+    red = torch.zeros(9, device=dev, dtype=torch.float64)
+    hist = torch.empty(512, device=dev, dtype=torch.int32)
+    lib.call("dcs_loss_contrast_edge_partial", _p(p), _p(t), N, H, W, _p(red), _p(ws), ws.numel(), _stream())
+    allreduce(red[:5])
+    for ps in range(4):
+        lib.call("dcs_loss_contrast_edge_hist", N, H, W, ps, _p(red), _p(hist), _p(ws), ws.numel(), _stream())
+        allreduce(hist)
+        lib.call("dcs_loss_contrast_edge_select", ps, _p(hist), _p(ws), ws.numel(), _stream())
+    lib.call("dcs_loss_contrast_edge_topk", N, H, W, _p(red), _p(ws), ws.numel(), _stream())
+    allreduce(red[5:9])
+    out = torch.empty(1, device=dev, dtype=torch.float32)
+    grad = torch.empty_like(p) if want_grad else None
+    lib.call("dcs_loss_contrast_edge_finish", _p(p), N, H, W, _p(red), float(grad_scale), _p(out), _p(grad), _p(ws),
+             ws.numel(), _stream())
+    return out.view(()), grad
+
+
 def loss_ssim(X, Y, data_range=1.0, win=11, sigma=1.5, K=(0.01, 0.03), want_grad=True):
     x, y = X.contiguous(), Y.contiguous()
     return _loss_call("dcs_loss_ssim", x,

@@ -8,7 +8,18 @@ rescales the saved gradient by the incoming scalar on the device (no host sync).
 import torch
 import torch.nn as nn
 
+from . import parallel
 from .hip import ops
+
+# the batch-coupled losses (ContrastRegion mean/std, ContrastEdge mean/std/top-10 %)
+# use per-rank statistics by default (option i: DDP semantics, exact vs the reference at one
+# GPU).  GLOBAL_STATS = True (train.py --global_loss_stats) computes them over the whole
+# data-parallel batch instead (option ii: the reference's single-process semantics at N GPUs).
+GLOBAL_STATS = False
+
+
+def _global(flag):
+    return (GLOBAL_STATS if flag is None else flag) and parallel.world() > 1
 
 
 class _FusedLoss(torch.autograd.Function):
@@ -74,12 +85,17 @@ class ContrastAttentionLoss(nn.Module):
 class ContrastRegionLoss(nn.Module):
     """trainer.py:89-130 (statistics over the whole batch tensor, unbiased std)."""
 
-    def __init__(self, threshold=0.3, weight=2.0):
+    def __init__(self, threshold=0.3, weight=2.0, global_stats=None):
         super().__init__()
         self.threshold, self.weight = threshold, weight
+        self.global_stats = global_stats  # None: module default GLOBAL_STATS
         self.pool = nn.AvgPool2d(kernel_size=8, stride=8)
 
     def forward(self, pred, target, source):
+        if _global(self.global_stats):
+            return _apply(lambda p, t, s, want_grad: ops.loss_contrast_region_global(
+                p, t, s, self.threshold, self.weight, parallel.allreduce_sum_, parallel.world(), want_grad),
+                pred, target, source)
         return _apply(lambda p, t, s, want_grad: ops.loss_contrast_region(
             p, t, s, self.threshold, self.weight, want_grad), pred, target, source)
 
@@ -87,14 +103,18 @@ class ContrastRegionLoss(nn.Module):
 class ContrastEdgeLoss(nn.Module):
     """trainer.py:133-184 (exact top-10 % by radix select)."""
 
-    def __init__(self):
+    def __init__(self, global_stats=None):
         super().__init__()
+        self.global_stats = global_stats
         self.register_buffer("sobel_x", torch.tensor([[-1, 0, 1], [-2, 0, 2], [-1, 0, 1]],
                                                      dtype=torch.float32).view(1, 1, 3, 3))
         self.register_buffer("sobel_y", torch.tensor([[-1, -2, -1], [0, 0, 0], [1, 2, 1]],
                                                      dtype=torch.float32).view(1, 1, 3, 3))
 
     def forward(self, pred, target, source=None):
+        if _global(self.global_stats):
+            return _apply(lambda p, t, want_grad: ops.loss_contrast_edge_global(
+                p, t, parallel.allreduce_sum_, parallel.world(), want_grad), pred, target)
         return _apply(lambda p, t, want_grad: ops.loss_contrast_edge(p, t, want_grad), pred, target)
 
 

@@ -68,6 +68,13 @@ def allreduce_mean_(flat: torch.Tensor):
     return flat
 
 
+def allreduce_sum_(t: torch.Tensor):
+    """In-place sum over ranks (the small partial-sum buffers of the global-statistics losses)."""
+    if world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
 def shard(n_total: int, r: int = None, w: int = None):
     """[start, stop) of rank r's share of n_total samples (equal shards; reference batch_size
     is the GLOBAL batch, modules/argmanager.py:95)."""

@@ -327,6 +327,8 @@ def train_cycle_gan(args, target_range):
     use_cbam = getattr(args, "use_cbam", True)
     nb = int(getattr(args, "num_residual_blocks", 9))
     torch.manual_seed(int(getattr(args, "seed", 0)))
+    from . import losses as _losses
+    _losses.GLOBAL_STATS = bool(getattr(args, "global_loss_stats", False))
     system = CycleGANSystem(input_channels, nb, use_cbam, lr=args.lr, lambda_cyc=args.lambda_cyc,
                             lambda_id=args.lambda_id, device=device)
     lr_lambda = lambda epoch: 1.0 - max(0, epoch + 1 - args.decay_epoch) / (args.epochs - args.decay_epoch)

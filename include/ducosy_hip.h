@@ -177,6 +177,32 @@ int dcs_cbam_backward(const float* dout, const float* y, const float* scale, con
                       const float* sa, int N, int H, int W, int C, int Cr, int ksa, float* dy,
                       float* dw1, float* dw2, float* dwsa, void* ws, size_t ws_bytes, void* stream);
 
+/* Global statistics of the batch-coupled losses over data-parallel ranks (SURVEY.md §8e
+ * option ii; replaces the whole-batch reductions of modules/trainer.py:126-128 and :170-180
+ * when the batch is sharded).  Phase functions: each leaves this shard's partial sums in a
+ * caller buffer (red: double, histograms: uint32[512]) that the caller sums over ranks (one
+ * all-reduce) before the next phase reads it.  All ranks then finish with the loss of the whole
+ * batch; d loss / d pred of the local shard is multiplied by grad_scale (the world size, so
+ * that the all-reduce-MEAN of parameter gradients equals the whole-batch gradient).  With one
+ * rank and no reduction the result equals dcs_loss_contrast_region / _edge.  ws: the same
+ * dcs_loss_workspace_size(N, H, W) buffer for every phase of one loss evaluation.
+ *   region: partial -> sum red[0..6] -> finish
+ *   edge:   partial -> sum red[0..4] -> for pass 0..3 { hist -> sum hist[0..511] -> select }
+ *           -> topk -> sum red[5..8] -> finish                                           */
+int dcs_loss_contrast_region_partial(const float* pred, const float* target, const float* source, int N, int H,
+                                     int W, float threshold, double* red, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_region_finish(const float* pred, int N, int H, int W, float weight, const double* red,
+                                    float grad_scale, float* out, float* grad, void* ws, size_t ws_bytes,
+                                    void* stream);
+int dcs_loss_contrast_edge_partial(const float* pred, const float* target, int N, int H, int W, double* red,
+                                   void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_edge_hist(int N, int H, int W, int pass, const double* red, uint32_t* hist, void* ws,
+                                size_t ws_bytes, void* stream);
+int dcs_loss_contrast_edge_select(int pass, const uint32_t* hist, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_edge_topk(int N, int H, int W, double* red, void* ws, size_t ws_bytes, void* stream);
+int dcs_loss_contrast_edge_finish(const float* pred, int N, int H, int W, const double* red, float grad_scale,
+                                  float* out, float* grad, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- losses (modules/trainer.py:22-184, 347-351; pytorch_msssim.SSIM) ----
  * All take single-channel planes [N,1,H,W]; each writes the loss value to out[0] and the
  * gradient d(loss)/d(pred) (unscaled) to grad (may be NULL for value only). */
