@@ -618,11 +618,25 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
         } else if constexpr (MMA == MMA_BF16X6) {
             static_assert(BKT == 16 && ACH == 2 && BCH == 2, "x6 tiles: 16 k, 8 per loader thread");
             bf16x8 hi, mid, lo;
+#ifdef DCS_X6_FAKEA
+            {
+                const floatx8 f = {ra[0].x, ra[0].y, ra[0].z, ra[0].w, ra[1].x, ra[1].y, ra[1].z, ra[1].w};
+                hi = mid = lo = __builtin_convertvector(f, bf16x8);
+            }
+#else
             split8x3(ra[0], ra[1], hi, mid, lo);
+#endif
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, arow, akq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, arow, akq >> 3)) = mid;
             *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, arow, akq >> 3)) = lo;
+#ifdef DCS_X6_FAKEB  // timing experiment only: B conversion without the split arithmetic
+            {
+                const floatx8 f = {rb[0].x, rb[0].y, rb[0].z, rb[0].w, rb[1].x, rb[1].y, rb[1].z, rb[1].w};
+                hi = mid = lo = __builtin_convertvector(f, bf16x8);
+            }
+#else
             split8x3(rb[0], rb[1], hi, mid, lo);
+#endif
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
             *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, BM + brow, bkq >> 3)) = lo;

@@ -46,7 +46,9 @@ out_ref = fold(dpad_ref).clone()
 torch.cuda.synchronize()
 s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
 rec = {"pack": [], "narrow": [], "fold": []}
-for it in range(300):
+CHAIN = len(sys.argv) > 2 and sys.argv[2] == "chain"  # pack -> narrow -> clone(dpad) -> fold, one stream
+chain = []
+for it in range(int(sys.argv[3]) if len(sys.argv) > 3 else 300):
     s0.wait_stream(torch.cuda.current_stream())
     s1.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s1):
@@ -54,6 +56,11 @@ for it in range(300):
             res.forward(ops.Src.nhwc(xr), pr)
     with torch.cuda.stream(s0):
         k = it % 3
+        if CHAIN:
+            wp = stem.pack_dgrad(w, 1)
+            dp = narrow(wp)
+            chain.append((wp.clone(), dp.clone(), fold(dp)))
+            continue
         if k == 0:
             rec["pack"].append(stem.pack_dgrad(w, 1))
         elif k == 1:
@@ -61,6 +68,12 @@ for it in range(300):
         else:
             rec["fold"].append(fold(dpad_ref))
 torch.cuda.synchronize()
+if CHAIN:
+    bad = [(i, torch.equal(a, wp_ref), torch.equal(b, dpad_ref), torch.equal(c, out_ref))
+           for i, (a, b, c) in enumerate(chain)
+           if not (torch.equal(a, wp_ref) and torch.equal(b, dpad_ref) and torch.equal(c, out_ref))]
+    print(sys.argv[1], "chain", len(chain), "mismatching chains (i, pack ok, dpad clone ok, fold ok):", bad[:12])
+    sys.exit(0)
 refs = {"pack": wp_ref, "narrow": dpad_ref, "fold": out_ref}
 for k, v in rec.items():
     bad = [i for i, o in enumerate(v) if not torch.equal(o, refs[k])]
