@@ -79,6 +79,9 @@ constexpr int NT = 256;
 #ifndef DCS_WGRAD_X6
 #define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
 #endif
+#ifndef DCS_X6_PIPE
+#define DCS_X6_PIPE 1  // bf16x6 rows: global loads two k-tiles ahead (two register sets)
+#endif
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
@@ -518,9 +521,9 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
     float4 ra[ACH];
     float4 rb[BCH];
 
-    auto load_a = [&](int kt) {
+    auto load_a = [&](int kt, auto& dst) {
         if (VEC == 2) {  // Cs == 4: taps aj .. aj+3, one float4 each (no prologue)
-            ra[0] = ra[1] = ra[2] = ra[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[0] = dst[1] = dst[2] = dst[3] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -531,7 +534,7 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                         int sy, sx;
                         if (map_coord(ri.by + ady, Hv, d.up, d.pad_mode, sy) &&
                             map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx))
-                            ra[e] = *reinterpret_cast<const float4*>(srow + sy * d.s_h + sx * d.s_w);
+                            dst[e] = *reinterpret_cast<const float4*>(srow + sy * d.s_h + sx * d.s_w);
                     }
                 }
             }
@@ -547,17 +550,17 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                 if (rvalid && yok && xok) off = (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4;
             }
 #pragma unroll
-            for (int i = 0; i < ACH; ++i) ra[i] = buf_load4(arsrc, off + 16 * i);
+            for (int i = 0; i < ACH; ++i) dst[i] = buf_load4(arsrc, off + 16 * i);
             if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
 #pragma unroll
-                for (int i = 0; i < ACH; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
+                for (int i = 0; i < ACH; ++i) dst[i] = affine_act4(dst[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
             }
             advance(aj, ac);
         } else if (VEC) {
             // (a buffer-descriptor variant of this gather, as in the wgrad pass, measured 3-7 %
             //  slower here: invalid taps would issue loads that the branch now skips)
 #pragma unroll
-            for (int i = 0; i < ACH; ++i) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int i = 0; i < ACH; ++i) dst[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid && aj < g.ntaps) {
                 int ady, adx, bt;
                 tap_decode(d, g, aj, ady, adx, bt);
@@ -566,10 +569,10 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                     map_coord(ri.bx + adx, Wv, d.up, d.pad_mode, sx)) {
                     const float* sp = srow + sy * d.s_h + sx * d.s_w + ac;
 #pragma unroll
-                    for (int i = 0; i < ACH; ++i) ra[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
+                    for (int i = 0; i < ACH; ++i) dst[i] = *reinterpret_cast<const float4*>(sp + 4 * i);
                     if (d.pro_act != DCS_ACT_NONE) {
 #pragma unroll
-                        for (int i = 0; i < ACH; ++i) ra[i] = affine_act4(ra[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
+                        for (int i = 0; i < ACH; ++i) dst[i] = affine_act4(dst[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
                     }
                 }
             }
@@ -589,11 +592,11 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                         e[q] = gather1(d, src, src2, psc, psh, ri.n, ri.by + ady, ri.bx + adx, c);
                     }
                 }
-                ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+                dst[i] = make_float4(e[0], e[1], e[2], e[3]);
             }
         }
     };
-    auto load_b = [&](int kt) {
+    auto load_b = [&](int kt, auto& dst) {
         long long col;
         bool ok = true;
         if (!d.parity) {
@@ -607,35 +610,35 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i)
-            rb[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
-    auto store_tiles = [&](int buf) {
+    auto store_tiles = [&](int buf, const auto& sa, const auto& sb) {
         if constexpr (MMA == MMA_F32) {
 #pragma unroll
-            for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = ra[i];
+            for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = sa[i];
 #pragma unroll
-            for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = rb[i];
+            for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = sb[i];
         } else if constexpr (MMA == MMA_BF16X6) {
             static_assert(BKT == 16 && ACH == 2 && BCH == 2, "x6 tiles: 16 k, 8 per loader thread");
             bf16x8 hi, mid, lo;
 #ifdef DCS_X6_FAKEA
             {
-                const floatx8 f = {ra[0].x, ra[0].y, ra[0].z, ra[0].w, ra[1].x, ra[1].y, ra[1].z, ra[1].w};
+                const floatx8 f = {sa[0].x, sa[0].y, sa[0].z, sa[0].w, sa[1].x, sa[1].y, sa[1].z, sa[1].w};
                 hi = mid = lo = __builtin_convertvector(f, bf16x8);
             }
 #else
-            split8x3(ra[0], ra[1], hi, mid, lo);
+            split8x3(sa[0], sa[1], hi, mid, lo);
 #endif
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, arow, akq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, arow, akq >> 3)) = mid;
             *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, arow, akq >> 3)) = lo;
 #ifdef DCS_X6_FAKEB  // timing experiment only: B conversion without the split arithmetic
             {
-                const floatx8 f = {rb[0].x, rb[0].y, rb[0].z, rb[0].w, rb[1].x, rb[1].y, rb[1].z, rb[1].w};
+                const floatx8 f = {sb[0].x, sb[0].y, sb[0].z, sb[0].w, sb[1].x, sb[1].y, sb[1].z, sb[1].w};
                 hi = mid = lo = __builtin_convertvector(f, bf16x8);
             }
 #else
-            split8x3(rb[0], rb[1], hi, mid, lo);
+            split8x3(sb[0], sb[1], hi, mid, lo);
 #endif
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
@@ -645,14 +648,14 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
             __bf16* a = Ah + (buf * BM + arow) * LDE;
 #pragma unroll
             for (int i = 0; i < ACH / 2; ++i) {
-                split8<MMA>(ra[2 * i], ra[2 * i + 1], hi, lo);
+                split8<MMA>(sa[2 * i], sa[2 * i + 1], hi, lo);
                 *reinterpret_cast<bf16x8*>(a + akq + 8 * i) = hi;
                 if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(a + 32 + akq + 8 * i) = lo;
             }
             __bf16* b = Bh + (buf * BN + brow) * LDE;
 #pragma unroll
             for (int i = 0; i < BCH / 2; ++i) {
-                split8<MMA>(rb[2 * i], rb[2 * i + 1], hi, lo);
+                split8<MMA>(sb[2 * i], sb[2 * i + 1], hi, lo);
                 *reinterpret_cast<bf16x8*>(b + bkq + 8 * i) = hi;
                 if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(b + 32 + bkq + 8 * i) = lo;
             }
@@ -667,9 +670,9 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    load_a(0);
-    load_b(0);
-    store_tiles(0);
+    load_a(0, ra);
+    load_b(0, rb);
+    store_tiles(0, ra, rb);
     __syncthreads();
 
     const int l32 = lane & 31, lk = (lane >> 5) * 16;
@@ -678,61 +681,55 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
         // B[16s + 8h + 0..7][col r] (v_mfma_f32_32x32x16_bf16 operand map)
         constexpr int NST = BKT / 16;
         const int kh = (lane >> 5) * 8;
-        for (int kt = 0; kt < nkt; ++kt) {
-            const int cur = kt & 1;
-            auto step = [&](int st) {
-                bf16x8 ah[IM], bh[JN], al[IM], bl[JN], am[IM], bm[JN];
+        auto step = [&](int cur, int st) {
+            bf16x8 ah[IM], bh[JN], al[IM], bl[JN], am[IM], bm[JN];
 #pragma unroll
-                for (int i = 0; i < IM; ++i) {
-                    if constexpr (MMA == MMA_BF16X6) {
-                        const int row = wm * WM + i * 32 + l32;
-                        ah[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
-                        am[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
-                        al[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
-                    } else {
-                        const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
-                        ah[i] = *reinterpret_cast<const bf16x8*>(a);
-                        if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
-                    }
+            for (int i = 0; i < IM; ++i) {
+                if constexpr (MMA == MMA_BF16X6) {
+                    const int row = wm * WM + i * 32 + l32;
+                    ah[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
+                    am[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
+                    al[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
+                } else {
+                    const __bf16* a = Ah + (cur * BM + wm * WM + i * 32 + l32) * LDE + 16 * st + kh;
+                    ah[i] = *reinterpret_cast<const bf16x8*>(a);
+                    if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
                 }
+            }
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {
+                if constexpr (MMA == MMA_BF16X6) {
+                    const int row = BM + wn * WN + j * 32 + l32;
+                    bh[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
+                    bm[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
+                    bl[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
+                } else {
+                    const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
+                    bh[j] = *reinterpret_cast<const bf16x8*>(b);
+                    if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < IM; ++i)
 #pragma unroll
                 for (int j = 0; j < JN; ++j) {
-                    if constexpr (MMA == MMA_BF16X6) {
-                        const int row = BM + wn * WN + j * 32 + l32;
-                        bh[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(0, cur, row, kh >> 3));
-                        bm[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(1, cur, row, kh >> 3));
-                        bl[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(2, cur, row, kh >> 3));
-                    } else {
-                        const __bf16* b = Bh + (cur * BN + wn * WN + j * 32 + l32) * LDE + 16 * st + kh;
-                        bh[j] = *reinterpret_cast<const bf16x8*>(b);
-                        if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
+                    if constexpr (MMA == MMA_BF16X6) {  // smallest terms first
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    } else if constexpr (MMA == MMA_BF16X3) {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    } else {  // bf16: operand rounding dominates, one accumulation level
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
                     }
                 }
-#pragma unroll
-                for (int i = 0; i < IM; ++i)
-#pragma unroll
-                    for (int j = 0; j < JN; ++j) {
-                        if constexpr (MMA == MMA_BF16X6) {  // smallest terms first
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
-                        } else if constexpr (MMA == MMA_BF16X3) {
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
-                        } else {  // bf16: operand rounding dominates, one accumulation level
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                        }
-                    }
-            };
-#pragma unroll
-            for (int st = 0; st < NST / 2; ++st) step(st);
-            if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
-#pragma unroll
-            for (int st = NST / 2; st < NST; ++st) step(st);
+        };
+        auto fold_t = [&](int kt) {  // close the inner accumulation chain every KT2 k-tiles
             if (MMA != MMA_BF16 && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
 #pragma unroll
                 for (int i = 0; i < IM; ++i)
@@ -743,11 +740,37 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                         for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                     }
             }
-#ifdef DCS_ROWS_SYNC2
-            __syncthreads();
-#endif
-            if (kt + 1 < nkt) store_tiles(cur ^ 1);
-            __syncthreads();
+        };
+        if constexpr (MMA == MMA_BF16X6 && DCS_X6_PIPE) {
+            // two register sets: tile kt+2's gather is in flight while tile kt computes, so
+            // staging tile kt+1 waits only for loads issued a whole k-tile earlier
+            float4 ra2[ACH], rb2[BCH];
+            if (1 < nkt) { load_a(1, ra); load_b(1, rb); }
+            for (int kt = 0; kt < nkt; kt += 2) {
+                if (kt + 2 < nkt) { load_a(kt + 2, ra2); load_b(kt + 2, rb2); }
+                step(0, 0);
+                fold_t(kt);
+                if (kt + 1 < nkt) store_tiles(1, ra, rb);
+                __syncthreads();
+                if (kt + 1 >= nkt) break;
+                if (kt + 3 < nkt) { load_a(kt + 3, ra); load_b(kt + 3, rb); }
+                step(1, 0);
+                fold_t(kt + 1);
+                if (kt + 2 < nkt) store_tiles(0, ra2, rb2);
+                __syncthreads();
+            }
+        } else {
+            for (int kt = 0; kt < nkt; ++kt) {
+                const int cur = kt & 1;
+#pragma unroll
+                for (int st = 0; st < NST / 2; ++st) step(cur, st);
+                if (kt + 1 < nkt) { load_a(kt + 1, ra); load_b(kt + 1, rb); }
+#pragma unroll
+                for (int st = NST / 2; st < NST; ++st) step(cur, st);
+                fold_t(kt);
+                if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb);
+                __syncthreads();
+            }
         }
     } else
     for (int kt = 0; kt < nkt; ++kt) {
@@ -766,7 +789,7 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
         // MFMAs of the tile in two halves with the next tile's gather in between; the inner
         // chain t spans KT2 k-tiles (two-level summation, see mfma_ktile)
         mfma_chain<IM, JN, 0, 2>(af, bf, t);
-        if (kt + 1 < nkt) { load_a(kt + 1); load_b(kt + 1); }
+        if (kt + 1 < nkt) { load_a(kt + 1, ra); load_b(kt + 1, rb); }
         mfma_chain<IM, JN, 2, 4>(af, bf, t);
         if ((kt % KT2) == KT2 - 1 || kt + 1 == nkt) {
 #pragma unroll
@@ -778,7 +801,7 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
                     for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                 }
         }
-        if (kt + 1 < nkt) store_tiles(cur ^ 1);
+        if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb);
         __syncthreads();
     }
 
