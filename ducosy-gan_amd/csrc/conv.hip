@@ -71,6 +71,17 @@ __device__ __forceinline__ void split8x3(const float4& a, const float4& b, bf16x
     lo = __builtin_convertvector(r2, bf16x8);
 }
 
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split4x3(const float4& a, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+    const f32x4v f = {a.x, a.y, a.z, a.w};
+    hi = __builtin_convertvector(f, bf16x4);
+    const f32x4v r1 = f - __builtin_convertvector(hi, f32x4v);
+    mid = __builtin_convertvector(r1, bf16x4);
+    const f32x4v r2 = r1 - __builtin_convertvector(mid, f32x4v);
+    lo = __builtin_convertvector(r2, bf16x4);
+}
+
 constexpr int BK = 32;
 constexpr int NT = 256;
 #ifndef DCS_X6_BK
@@ -78,6 +89,9 @@ constexpr int NT = 256;
 #endif
 #ifndef DCS_WGRAD_X6
 #define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
+#endif
+#ifndef DCS_X6_BN64
+#define DCS_X6_BN64 1  // bf16x6 rows also for 64-column tiles
 #endif
 #ifndef DCS_X6_PIPE
 #define DCS_X6_PIPE 1  // bf16x6 rows: global loads two k-tiles ahead (two register sets)
@@ -619,7 +633,7 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
 #pragma unroll
             for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = sb[i];
         } else if constexpr (MMA == MMA_BF16X6) {
-            static_assert(BKT == 16 && ACH == 2 && BCH == 2, "x6 tiles: 16 k, 8 per loader thread");
+            static_assert(BKT == 16 && ACH == 2 && (BCH == 2 || BCH == 1), "x6 tiles: 16 k, 8 / 4 per loader thread");
             bf16x8 hi, mid, lo;
 #ifdef DCS_X6_FAKEA
             {
@@ -632,17 +646,24 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, arow, akq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, arow, akq >> 3)) = mid;
             *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, arow, akq >> 3)) = lo;
+            if constexpr (BCH == 2) {
 #ifdef DCS_X6_FAKEB  // timing experiment only: B conversion without the split arithmetic
-            {
                 const floatx8 f = {sb[0].x, sb[0].y, sb[0].z, sb[0].w, sb[1].x, sb[1].y, sb[1].z, sb[1].w};
                 hi = mid = lo = __builtin_convertvector(f, bf16x8);
-            }
 #else
-            split8x3(sb[0], sb[1], hi, mid, lo);
+                split8x3(sb[0], sb[1], hi, mid, lo);
 #endif
-            *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
-            *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
-            *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, BM + brow, bkq >> 3)) = lo;
+                *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
+                *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
+                *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, BM + brow, bkq >> 3)) = lo;
+            } else {  // 64-column tiles: 4 k per thread, the 8-byte half of a 16-byte chunk
+                bf16x4 h4, m4, l4;
+                split4x3(sb[0], h4, m4, l4);
+                const int sub = 4 * ((bkq >> 2) & 1);
+                *reinterpret_cast<bf16x4*>(Ah + x6o(0, buf, BM + brow, bkq >> 3) + sub) = h4;
+                *reinterpret_cast<bf16x4*>(Ah + x6o(1, buf, BM + brow, bkq >> 3) + sub) = m4;
+                *reinterpret_cast<bf16x4*>(Ah + x6o(2, buf, BM + brow, bkq >> 3) + sub) = l4;
+            }
         } else {
             bf16x8 hi, lo;
             __bf16* a = Ah + (buf * BM + arow) * LDE;
@@ -1564,9 +1585,10 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
                      d.stride == 1;
     hipStream_t s = as_stream(stream);
-    if (vec && d.mma == MMA_BF16X6 && BN == 128) {  // x6: 128-column tiles (8 k per loader thread)
-        if (res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+    if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64)) {  // x6: 128- or 64-column tiles
+        if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
         return check_launch("conv_rows");
     }
     const bool mma_ok = vec && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
