@@ -113,10 +113,13 @@ def main():
                          "(default; error <= the exact-f32 path's, tests/test_gpu_mma.py), f32 = exact "
                          "fp32 MFMA, bf16x3 = hi/lo split, bf16 = plain bf16 operands")
     ap.add_argument("--dual", action="store_true",
-                    help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained "
-                         "concurrently, one HIP stream each; value counts the images of both models")
+                    help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one "
+                         "process; value counts the images of both models")
+    ap.add_argument("--dual-schedule", default="serial", choices=["serial", "concurrent"],
+                    help="--dual: both models on one stream in the --mma mode (serial), or one HIP stream "
+                         "each in exact f32 (concurrent; trainer.py ConcurrentCycleGANs)")
     args = ap.parse_args()
-    if args.dual:  # the concurrent runner steps in its own (exact f32) mode: trainer.py ConcurrentCycleGANs
+    if args.dual and args.dual_schedule == "concurrent":  # the two-stream runner's own (exact f32) mode
         from modules.trainer import ConcurrentCycleGANs
         args.mma = ConcurrentCycleGANs.MMA
 
@@ -132,7 +135,8 @@ def main():
     if args.dual:
         from modules.trainer import ConcurrentCycleGANs
         cins = (3, 2)
-        runner = ConcurrentCycleGANs([CycleGANSystem(c, args.blocks, True, device=device) for c in cins], device)
+        runner = ConcurrentCycleGANs([CycleGANSystem(c, args.blocks, True, device=device) for c in cins], device,
+                                     schedule=args.dual_schedule)
         batches = [[_synthetic(args.batch, args.img, c - 1, device, 100 * rank + 10 * c + i) for c in cins]
                    for i in range(2)]
         step = lambda b: runner.train_step(b)
@@ -180,8 +184,9 @@ def main():
             "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {
-                "workload": ("dual soft-tissue (cin 3) + lung (cin 2) CycleGANs trained concurrently (one HIP "
-                             "stream each), full train step per model; value = images of both models per second"
+                "workload": (f"dual soft-tissue (cin 3) + lung (cin 2) CycleGANs in one process "
+                             f"({'one HIP stream each' if args.dual_schedule == 'concurrent' else 'one after the other on one stream'}), "
+                             "full train step per model; value = images of both models per second"
                              if args.dual else
                              "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
                              "9 G loss terms + 2 D losses, 3 Adam steps"),

@@ -176,14 +176,23 @@ class ConcurrentCycleGANs:
     # and with f32 co-runners: 0 / 800).  Single-stream training is unaffected.
     MMA = "f32"
 
-    def __init__(self, systems, device):
+    def __init__(self, systems, device, schedule="concurrent"):
+        """schedule "concurrent": one HIP stream per system, exact-f32 operands (above);
+        "serial": the systems step one after the other on the caller's stream in the current
+        operand mode (bf16x6 by default), which on MI355X is the faster way to train both."""
+        if schedule not in ("concurrent", "serial"):
+            raise ValueError("schedule must be 'concurrent' or 'serial'")
         self.systems = list(systems)
         self.device = torch.device(device)
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.systems]
+        self.schedule = schedule
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.systems] \
+            if schedule == "concurrent" else []
 
     def train_step(self, batches):
         """batches: one (real_A, real_B, masks) per system.  Returns one loss dict per system
         (device tensors, ready once the streams are synchronised with the caller's)."""
+        if self.schedule == "serial":
+            return [sysm.train_step(*b) for sysm, b in zip(self.systems, batches)]
         from .hip import ops
         prev = ops.get_mma()
         ops.set_mma(self.MMA)

@@ -43,3 +43,21 @@ def test_concurrent_equals_sequential():
     for a, b in zip(seq, run.systems):
         assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)
         assert torch.equal(a.optimizer_D_A.flat_p, b.optimizer_D_A.flat_p)
+
+
+def test_serial_schedule_equals_independent_runs():
+    """The serial schedule (both models on the caller's stream, default operand mode) gives each
+    model exactly the numbers of its own run."""
+    from modules.trainer import ConcurrentCycleGANs
+    n, hw, nb, steps = 2, 64, 2, 2
+    cfg = [(3, 811), (2, 812)]
+    want = []
+    for c, s in cfg:
+        m = _system(c, nb, prng.step_model_seeds(s))
+        want.append([{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)])
+    run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV, schedule="serial")
+    got = [[], []]
+    for i in range(steps):
+        for j, o in enumerate(run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])):
+            got[j].append({k: float(v) for k, v in o.items()})
+    assert got == want
