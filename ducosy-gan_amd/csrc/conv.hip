@@ -1667,11 +1667,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         return (((op * 3 + pl) * 2 + buf) * BKP + pix) * PITCH + col;
     };
 
+    // sub-pixel descriptors (parity 2) run one GEMM per phase z, as in conv_wgrad_kernel
+    const int ncls = d.parity == 2 ? 4 : 1;
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int ntile = L % gn;
     const int mtile = (L / gn) % gm;
-    const int split = L / (gn * gm);
-    const ClassGeom g = class_geom(d, 0);
+    const int z = (L / (gn * gm)) % ncls;
+    const int split = L / (gn * gm * ncls);
+    const ClassGeom g = class_geom(d, z);
     const long long P = (long long)g.My * g.Mx * d.N;
     const int Ktot = g.ntaps * d.Cs;
     const int m0 = mtile * BM, n0 = ntile * BN;
@@ -1708,16 +1711,20 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     }
     float4 ra[2], rb[2];
     auto load = [&](long long kt) {
-        const long long p = kt * BKP + kr;
+        long long p = kt * BKP + kr;
         const bool pok = p < P;
         const int co = m0 + cc;
+        if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             ra[i] = (pok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        // sub-pixel phases: the tap offsets already include the padding
+        const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
+        const int vx = d.parity == 2 ? pqx + badx : pqx * d.stride - d.pl + badx;
         int sy, sx;
-        const bool yok = map_coord_sel(pqy * d.stride - d.pt + bady, Hv, d.up, d.pad_mode, sy);
-        const bool xok = map_coord_sel(pqx * d.stride - d.pl + badx, Wv, d.up, d.pad_mode, sx);
+        const bool yok = map_coord_sel(vy, Hv, d.up, d.pad_mode, sy);
+        const bool xok = map_coord_sel(vx, Wv, d.up, d.pad_mode, sx);
         const bool ok = pok && bcol_ok && yok && xok;
         const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
 #pragma unroll
@@ -1815,7 +1822,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         __syncthreads();
     }
 
-    float* slab = ws + (long long)split * d.Co * Ktot;
+    float* slab = ws + ((long long)split * ncls + z) * d.Co * Ktot;
     const int l32 = lane & 31;
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
@@ -1916,7 +1923,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (d.mma == MMA_BF16X6 && vec && p.BM == 128 && !d.parity && DCS_WGRAD_X6) {
+    } else if (d.mma == MMA_BF16X6 && vec && p.BM == 128 && d.parity != 1 && DCS_WGRAD_X6) {
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs
         if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
