@@ -443,9 +443,10 @@ __device__ __forceinline__ void mfma_ktile(const float4 (&af)[IM][4], const floa
 template <int TAG>
 __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
 #ifndef DCS_NO_SPECIALISE
-    if constexpr (TAG == 1) {
+    if constexpr (TAG == 1) {  // the residual-block convs: no prologue / epilogue activation
         d.KH = 3; d.KW = 3; d.stride = 1; d.up = 1; d.parity = 0;
         d.Cs = 256; d.csplit = 256; d.s_c = 1;
+        d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
     }
 #endif
     return d;
@@ -1583,7 +1584,7 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     const bool vec = vec_ok(dp, src);
     const bool v4 = !vec && vec4_ok(dp, src) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
-                     d.stride == 1;
+                     d.stride == 1 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
     hipStream_t s = as_stream(stream);
     if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64)) {  // x6: 128- or 64-column tiles
         if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
@@ -1903,7 +1904,8 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     if (d.parity == 2 && !vec) return fail(DCS_E_INVALID, "conv_wgrad: sub-pixel rows need a vectorisable source");
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
-    const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity;
+    const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity &&
+                     d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
     const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool dy_small = (long long)d.N * d.Ho * d.Wo * d.Co * 4 < (long long)OOB_OFF - 64;
     // The bf16 weight-gradient kernel measured slower than the exact f32 one at every layer
