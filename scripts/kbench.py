@@ -36,13 +36,15 @@ def timeit(fn, reps):
 
 
 LAYERS = [
-    # name, geom, input H, pro
+    # name, geom, input H, pro (as in training, modules/hip/networks.py: the Generator's MFMA
+    # convs read materialised IN outputs; the head and PatchGAN layers 1-4 apply IN + act in
+    # their gather)
     ("stem", ConvGeom(3, 64, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT), 512, False),
-    ("down1", ConvGeom(64, 128, 3, 2, (1, 1, 1, 1)), 512, True),
-    ("down2", ConvGeom(128, 256, 3, 2, (1, 1, 1, 1)), 256, True),
-    ("res", ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT), 128, True),
+    ("down1", ConvGeom(64, 128, 3, 2, (1, 1, 1, 1)), 512, False),
+    ("down2", ConvGeom(128, 256, 3, 2, (1, 1, 1, 1)), 256, False),
+    ("res", ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT), 128, False),
     ("up1", ConvGeom(256, 128, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 128, False),
-    ("up2", ConvGeom(128, 64, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 256, True),
+    ("up2", ConvGeom(128, 64, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2), 256, False),
     ("head", ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT), 512, True),
     ("d0", ConvGeom(1, 64, 4, 2, (1, 1, 1, 1)), 512, False),
     ("d1", ConvGeom(64, 128, 4, 2, (1, 1, 1, 1)), 256, True),
