@@ -115,13 +115,14 @@ def main():
     ap.add_argument("--dual", action="store_true",
                     help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one "
                          "process; value counts the images of both models")
-    ap.add_argument("--dual-schedule", default="serial", choices=["serial", "concurrent"],
-                    help="--dual: both models on one stream in the --mma mode (serial), or one HIP stream "
-                         "each in exact f32 (concurrent; trainer.py ConcurrentCycleGANs)")
+    ap.add_argument("--dual-schedule", default="serial", choices=["serial", "concurrent", "groups"],
+                    help="--dual: both models on one stream (serial), one HIP stream each (concurrent; "
+                         "trainer.py ConcurrentCycleGANs), or split GPU groups (groups: soft tissue on the first "
+                         "half of the ranks, lung on the second, each with its own all-reduce)")
+    ap.add_argument("--workload", default="step", choices=["step", "g_a2b"],
+                    help="step: the full training step (BASELINE config 3/4); g_a2b: Generator_A2B forward + "
+                         "backward only (BASELINE config 2, conv + CBAM kernels)")
     args = ap.parse_args()
-    if args.dual and args.dual_schedule == "concurrent":  # the two-stream runner's own (exact f32) mode
-        from modules.trainer import ConcurrentCycleGANs
-        args.mma = ConcurrentCycleGANs.MMA
 
     from modules import parallel
     from modules.hip import ops
@@ -132,7 +133,32 @@ def main():
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
     torch.manual_seed(1234)
-    if args.dual:
+    groups = args.dual and args.dual_schedule == "groups"
+    if groups:
+        if world < 2 or world % 2:
+            raise SystemExit("--dual-schedule groups needs an even number of processes (one model per half)")
+        gi, _ = parallel.split_groups(2)
+        cin = (3, 2)[gi]  # soft tissue on ranks 0..w/2-1, lung on w/2..w-1
+        system = CycleGANSystem(cin, args.blocks, True, device=device)
+        batches = [_synthetic(args.batch, args.img, cin - 1, device, 100 * rank + i) for i in range(2)]
+        step = lambda b: system.train_step(*b)
+    elif args.workload == "g_a2b":
+        from modules.model import Generator, weights_init_normal
+        G = Generator(input_channels=args.cin, num_residual_blocks=args.blocks, use_cbam=True)
+        G.apply(weights_init_normal)
+        G.to(device)
+        for p_ in G.parameters():
+            p_.grad = torch.zeros_like(p_)
+        batches = []
+        for i in range(2):
+            a, _, m = _synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i)
+            dout = torch.randn(args.batch, 1, args.img, args.img, device=device)
+            batches.append((a, m, dout))
+
+        def step(b):
+            out = G(b[0], b[1])
+            out.backward(b[2])
+    elif args.dual:
         from modules.trainer import ConcurrentCycleGANs
         cins = (3, 2)
         runner = ConcurrentCycleGANs([CycleGANSystem(c, args.blocks, True, device=device) for c in cins], device,
@@ -144,7 +170,7 @@ def main():
         system = CycleGANSystem(args.cin, args.blocks, True, device=device)
         batches = [_synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i) for i in range(2)]
         step = lambda b: system.train_step(*b)
-    models = 2 if args.dual else 1
+    models = 2 if args.dual and not groups else 1
 
     for i in range(args.warmup):
         step(batches[i % 2])
@@ -170,8 +196,22 @@ def main():
     if rank == 0:
         value = world * models * args.batch * args.steps / elapsed
         achieved = flop_launch / (ms_launch * 1e-3) / 1e12 if ms_launch > 0 else 0.0
+        if args.workload == "g_a2b":
+            workload = ("Generator_A2B (ResNet-9 + CBAM) forward + backward (weight and input gradients), "
+                        "BASELINE config 2")
+        elif groups:
+            workload = ("dual soft-tissue (cin 3) + lung (cin 2) CycleGANs as split GPU groups (ranks 0..w/2-1 "
+                        "soft tissue, w/2..w-1 lung, one all-reduce group each), full train step per rank")
+        elif args.dual:
+            workload = (f"dual soft-tissue (cin 3) + lung (cin 2) CycleGANs in one process "
+                        f"({'one HIP stream each' if args.dual_schedule == 'concurrent' else 'one after the other on one stream'}), "
+                        "full train step per model; value = images of both models per second")
+        else:
+            workload = ("full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
+                        "9 G loss terms + 2 D losses, 3 Adam steps")
         rec = {
-            "metric": "CycleGAN train-step images/sec at 512x512 bs=8/GPU",
+            "metric": ("Generator_A2B fwd+bwd images/sec at 512x512 bs=8/GPU" if args.workload == "g_a2b"
+                       else "CycleGAN train-step images/sec at 512x512 bs=8/GPU"),
             "value": round(value, 4),
             "unit": "img/s",
             "n_gpus": world,
@@ -184,15 +224,10 @@ def main():
             "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {
-                "workload": (f"dual soft-tissue (cin 3) + lung (cin 2) CycleGANs in one process "
-                             f"({'one HIP stream each' if args.dual_schedule == 'concurrent' else 'one after the other on one stream'}), "
-                             "full train step per model; value = images of both models per second"
-                             if args.dual else
-                             "full soft-tissue CycleGAN train step: 2x Generator (ResNet-9 + CBAM) + 2x PatchGAN, "
-                             "9 G loss terms + 2 D losses, 3 Adam steps"),
+                "workload": workload,
                 "img_size": args.img, "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                 "residual_blocks": args.blocks, "input_channels": [3, 2] if args.dual else args.cin,
-                "parallelism": f"dp{world}",
+                "parallelism": f"2 groups x dp{world // 2}" if groups else f"dp{world}",
             },
             "roofline": {
                 "kernel": f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)",
@@ -208,7 +243,7 @@ def main():
                 "gflop_per_launch": round(flop_launch / 1e9, 3),
             },
         }
-        if world == 1 and not args.no_cpu_baseline and not args.dual:
+        if world == 1 and not args.no_cpu_baseline and not args.dual and args.workload == "step":
             threads = min(16, os.cpu_count() or 1)
             rec["cpu_baseline"] = cpu_baseline(args.img, args.blocks, args.cin, threads)
         print(json.dumps(rec), flush=True)

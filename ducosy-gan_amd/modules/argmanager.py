@@ -24,7 +24,10 @@ def _add_build_train_flags(p: argparse.ArgumentParser):
     g.add_argument("--seed", type=int, default=0, help="torch seed for weight initialisation")
     g.add_argument("--global_loss_stats", action="store_true",
                    help="at N GPUs, compute the batch-coupled losses (ContrastRegion, ContrastEdge) over the "
-                        "whole data-parallel batch (the reference's single-process semantics) instead of per rank")
+                        "whole data-parallel batch, the reference's semantics (the default; kept for scripts)")
+    g.add_argument("--per_rank_loss_stats", action="store_true",
+                   help="at N GPUs, compute the batch-coupled losses on each rank's shard (DDP semantics; no "
+                        "collectives inside the losses) instead of over the whole batch")
 
 
 def get_common_infer_args(argv=None):

@@ -28,6 +28,11 @@ _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
 
 
+# bf16x6 residual convs on pre-split operands staged by LDS-DMA (csrc/conv_x6p.hip); 0 = the
+# split-in-the-gather rows kernel of conv.hip (A/B switch)
+_X6P = os.environ.get("DUCOSY_X6P", "0") == "1"
+
+
 def set_mma(mode: str) -> None:
     global _MMA
     if mode not in _MMA_NAMES:
@@ -77,6 +82,21 @@ def workspace(nbytes: int, device) -> torch.Tensor:
     if _WS_POISON:  # debug: every request sees NaN bytes (finds reads of unwritten scratch)
         buf.fill_(0xFF)
     return buf
+
+
+def split_x6(t: torch.Tensor) -> torch.Tensor:
+    """fp32 tensor (contiguous, numel % 8 == 0) -> its bf16x6 operand planes: groups of 8
+    consecutive elements as [hi[8], mid[8], lo[8]] bf16 (held in an int16 tensor, 3 x numel)."""
+    if not t.is_contiguous() or t.numel() % 8:
+        raise ValueError("split_x6: contiguous tensor with numel % 8 == 0 expected")
+    _check_dev(t)
+    out = torch.empty(t.numel() * 3, dtype=torch.int16, device=t.device)
+    lib.call("dcs_split_x6", _p(t), t.numel(), _p(out), _stream())
+    return out
+
+
+def _x6p(d: lib.ConvDesc) -> bool:
+    return _X6P and d.mma == lib.MMA_BF16X6 and bool(lib.query("dcs_conv_rows_x6p_ok", ctypes.byref(d)))
 
 
 def _round_up(x, m):
@@ -263,9 +283,16 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
+        x6p = (not self.narrow and bias is None and s.t2 is None and s.t.is_contiguous()
+               and s.strides == (s.H * s.W * s.C, 1, s.W * s.C, s.C) and _x6p(d))
+        if x6p:  # operands split once, k-tiles staged by LDS-DMA (conv_x6p.hip)
+            sp, wpp = split_x6(s.t), split_x6(wpack)
         e0 = PROBE.begin() if _is_res_geom(self) else None
-        lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
-                 _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
+        if x6p:
+            lib.call("dcs_conv_rows_x6p", ctypes.byref(d), _p(sp), _p(wpp), _p(out), _stream())
+        else:
+            lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
+                     _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
         PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
         return out
 
@@ -318,9 +345,15 @@ class ConvGeom:
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
             dpad = torch.empty(N, d.Ho, d.Wo, ci, device=dev, dtype=torch.float32)
+            x6p = not narrow and dy.is_contiguous() and _x6p(d)
+            if x6p:
+                sp, wpp = split_x6(dy), split_x6(wpack_d)
             e0 = PROBE.begin() if _is_res_geom(self) else None
-            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad),
-                     _stream())
+            if x6p:
+                lib.call("dcs_conv_rows_x6p", ctypes.byref(d), _p(sp), _p(wpp), _p(dpad), _stream())
+            else:
+                lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad),
+                         _stream())
             PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
             lib.call("dcs_reflect_fold", _p(dpad), _p(addend), _p(out), N, H, W, ci, p, _stream())

@@ -11,15 +11,25 @@ import torch.nn as nn
 from . import parallel
 from .hip import ops
 
-# the batch-coupled losses (ContrastRegion mean/std, ContrastEdge mean/std/top-10 %)
-# use per-rank statistics by default (option i: DDP semantics, exact vs the reference at one
-# GPU).  GLOBAL_STATS = True (train.py --global_loss_stats) computes them over the whole
-# data-parallel batch instead (option ii: the reference's single-process semantics at N GPUs).
-GLOBAL_STATS = False
+# the batch-coupled losses (ContrastRegion mean/std, ContrastEdge mean/std/top-10 %).
+# The reference's nn.DataParallel (trainer.py:333-338) evaluates them on the whole batch gathered
+# on cuda:0, so with more than one replica they are computed over the whole data-parallel batch
+# by default (option ii, a few small all-reduces per evaluation).  GLOBAL_STATS = False
+# (train.py --per_rank_loss_stats) uses each rank's shard instead (option i: DDP semantics).
+# None = the default (whole batch); a module's own ``global_stats`` argument overrides it.
+GLOBAL_STATS = None
 
 
 def _global(flag):
-    return (GLOBAL_STATS if flag is None else flag) and parallel.world() > 1
+    mode = GLOBAL_STATS if flag is None else flag
+    return (True if mode is None else bool(mode)) and parallel.world() > 1
+
+
+def stats_mode() -> str:
+    """Which statistics the batch-coupled losses use in this process (printed at start-up)."""
+    if parallel.world() == 1:
+        return "single replica (whole batch)"
+    return "whole data-parallel batch" if _global(None) else "per rank (--per_rank_loss_stats)"
 
 
 class _FusedLoss(torch.autograd.Function):

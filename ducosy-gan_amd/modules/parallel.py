@@ -3,9 +3,14 @@
 Replaces the reference's single-process nn.DataParallel (modules/trainer.py:333-338), which
 scatters every G/D call over 8 GPUs, re-broadcasts all parameters per call and reduces
 gradients to cuda:0.  Here each rank owns full replicas of G_A2B, G_B2A, D_A, D_B and its own
-batch shard; per optimizer step there is exactly ONE all-reduce of that optimizer's flat
-gradient buffer (FusedAdam.flat_g: 91.6 MB for the G pair, 11.05 MB per D at cin 3), averaged
-over ranks.  Initial weights are broadcast from rank 0 once.
+batch shard; per optimizer step the optimizer's flat gradient buffer (FusedAdam.flat_g: 91.6 MB
+for the G pair, 11.05 MB per D at cin 3) is averaged over the replicas.  The G buffer goes out
+in buckets while the G backward is still running (``GradBuckets``); initial weights are
+broadcast from the group's first rank once.
+
+Replica group: by default every rank of the job.  ``set_group`` narrows it to a sub-group, for
+BASELINE config 5 on one node as split GPU groups (soft-tissue model on ranks 0..w/2-1, lung
+model on ranks w/2..w-1, each group with its own collectives; ``split_groups``).
 """
 from __future__ import annotations
 
@@ -14,13 +19,29 @@ import os
 import torch
 import torch.distributed as dist
 
+_GROUP = None  # process group of this rank's replicas (None: the default group)
+
+
+def _on():
+    return dist.is_available() and dist.is_initialized()
+
+
+def set_group(group) -> None:
+    """Collectives, world() and rank() refer to ``group`` from now on (None: every rank)."""
+    global _GROUP
+    _GROUP = group
+
+
+def group():
+    return _GROUP
+
 
 def world():
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    return dist.get_world_size(_GROUP) if _on() else 1
 
 
 def rank():
-    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+    return dist.get_rank(_GROUP) if _on() else 0
 
 
 def init_from_env(backend: str = None):
@@ -40,6 +61,22 @@ def init_from_env(backend: str = None):
     return dist.get_rank(), dist.get_world_size(), local
 
 
+def split_groups(n_groups: int):
+    """Cut the job into ``n_groups`` equal contiguous rank groups (every rank must call this).
+    Returns (index of this rank's group, its process group) and makes it the replica group."""
+    w, r = dist.get_world_size(), dist.get_rank()
+    if w % n_groups:
+        raise ValueError(f"world size {w} is not a multiple of {n_groups} groups")
+    per = w // n_groups
+    mine = None
+    for gi in range(n_groups):
+        pg = dist.new_group(list(range(gi * per, (gi + 1) * per)))
+        if gi == r // per:
+            mine = pg
+    set_group(mine)
+    return r // per, mine
+
+
 def local_device_index() -> int:
     """GPU of this process: LOCAL_RANK (one process per GPU).  DUCOSY_DEVICE_OVERRIDE pins
     every rank to one device — for rehearsing the multi-process path on a single GPU with
@@ -49,29 +86,35 @@ def local_device_index() -> int:
 
 
 def broadcast_(flat: torch.Tensor, src: int = 0):
+    """Broadcast from the replica group's rank ``src``."""
     if world() > 1:
-        dist.broadcast(flat, src)
+        gsrc = dist.get_global_rank(_GROUP, src) if _GROUP is not None else src
+        dist.broadcast(flat, gsrc, group=_GROUP)
     return flat
 
 
+def _scale_(flat: torch.Tensor, s: float):
+    if flat.is_cuda:
+        from .hip import ops
+        ops.scale_add_(flat, flat, s - 1.0)  # flat *= s on the device kernel
+    else:
+        flat.mul_(s)
+
+
 def allreduce_mean_(flat: torch.Tensor):
-    """In-place mean over ranks of a flat gradient buffer (one collective)."""
+    """In-place mean over the replicas of a flat gradient buffer (one collective)."""
     w = world()
     if w == 1:
         return flat
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-    if flat.is_cuda:
-        from .hip import ops
-        ops.scale_add_(flat, flat, 1.0 / w - 1.0)  # flat *= 1/w on the device kernel
-    else:
-        flat.mul_(1.0 / w)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=_GROUP)
+    _scale_(flat, 1.0 / w)
     return flat
 
 
 def allreduce_sum_(t: torch.Tensor):
-    """In-place sum over ranks (the small partial-sum buffers of the global-statistics losses)."""
+    """In-place sum over the replicas (the small partial-sum buffers of the whole-batch losses)."""
     if world() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_GROUP)
     return t
 
 
@@ -82,3 +125,70 @@ def shard(n_total: int, r: int = None, w: int = None):
     w = world() if w is None else w
     per = n_total // w
     return r * per, (r + 1) * per
+
+
+class GradBuckets:
+    """All-reduce-mean of one flat gradient buffer in buckets, each launched (async) as soon
+    as the backward has finished accumulating every parameter of the bucket, so the exchange
+    of the early buckets overlaps the rest of the backward.
+
+    buckets: list of lists of parameters whose ``.grad`` are views of ``flat`` (FusedAdam
+    layout); each bucket must be one contiguous span of ``flat``.  Autograd accumulates a leaf
+    once per backward however many graph branches reach it (the branches are summed first), so
+    a bucket is complete after one post-accumulate hook per member.  ``arm()`` before the
+    backward, ``finish()`` after it (waits for every bucket and applies 1/world); ``early``
+    counts the buckets launched from inside the backward.  With one replica both are no-ops."""
+
+    def __init__(self, flat: torch.Tensor, buckets):
+        self.flat = flat
+        self.spans, self.members = [], []
+        base = flat.data_ptr()
+        esz = flat.element_size()
+        for b in buckets:
+            offs = [((p.grad.data_ptr() - base) // esz, p.numel()) for p in b]
+            lo = min(o for o, _ in offs)
+            hi = max(o + n for o, n in offs)
+            if sum(n for _, n in offs) != hi - lo:
+                raise ValueError("GradBuckets: a bucket must be one contiguous span of the flat buffer")
+            self.spans.append((lo, hi))
+            self.members.append(b)
+        self._handles = []
+        self._works = []
+        self._left = None
+        self.early = 0
+
+    def arm(self):
+        if world() == 1:
+            return
+        self._works = [None] * len(self.spans)
+        self._left = [len(b) for b in self.members]
+        self._handles = []
+        self.early = 0
+        for bi, b in enumerate(self.members):
+            for p in b:
+                self._handles.append(p.register_post_accumulate_grad_hook(self._hook(bi)))
+
+    def _hook(self, bi):
+        def fn(_p):
+            self._left[bi] -= 1
+            if self._left[bi] == 0:
+                lo, hi = self.spans[bi]
+                self._works[bi] = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_GROUP,
+                                                  async_op=True)
+                self.early += 1
+        return fn
+
+    def finish(self):
+        w = world()
+        if w == 1:
+            return
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+        for bi, wk in enumerate(self._works):
+            lo, hi = self.spans[bi]
+            if wk is None:  # a member received no gradient this step: reduce the bucket now
+                dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_GROUP)
+            else:
+                wk.wait()
+        _scale_(self.flat, 1.0 / w)

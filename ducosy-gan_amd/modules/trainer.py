@@ -77,6 +77,11 @@ class CycleGANSystem:
         # identical initial replicas on every rank
         for opt in self.optimizers:
             parallel.broadcast_(opt.flat_p, 0)
+        # G gradient exchange in two buckets: G_B2A's half is final once its one backward call has
+        # run, and goes out while the G_A2B backward of the batched [real_A; real_B] call (the
+        # last of the step, ~40 % of the G backward) is still computing.
+        self._g_sync = parallel.GradBuckets(self.optimizer_G.flat_g,
+                                            [list(self.G_A2B.parameters()), list(self.G_B2A.parameters())])
 
     @property
     def models(self):
@@ -121,8 +126,9 @@ class CycleGANSystem:
         loss_G = (loss_GAN + self.lambda_cyc * loss_cycle + self.lambda_id * loss_id
                   + LAMBDA_GRAD * loss_grad_cycle + LAMBDA_GRAD_ID * loss_grad_id + LAMBDA_SSIM * loss_ssim
                   + LAMBDA_CA * loss_ca + LAMBDA_CR * loss_cr + LAMBDA_CE * loss_ce)
+        self._g_sync.arm()
         loss_G.backward()
-        parallel.allreduce_mean_(self.optimizer_G.flat_g)
+        self._g_sync.finish()  # replica mean of the G gradient
         self.optimizer_G.step()
 
         # --- Discriminator steps (trainer.py:517-525), real and fake batched ---
@@ -160,26 +166,20 @@ class CycleGANSystem:
 
 
 class ConcurrentCycleGANs:
-    """Several CycleGANSystems trained in the same process, each on its own HIP stream
-    (BASELINE config 5: the soft-tissue (cin 3) and lung (cin 2) models concurrently; the
-    reference trains them one after the other, train.py:27-38).  A step enqueues every model's
-    train_step on its stream; the kernels of one model fill the gaps of the other (small
-    normalisation / loss / Adam launches, split-K reductions, launch latency).  Workspaces are
-    per stream (ops.workspace), the kernels are deterministic, so each model's numbers equal a
-    sequential run bit for bit (tests/test_gpu_concurrent.py)."""
+    """Several CycleGANSystems trained in the same process (BASELINE config 5: the soft-tissue
+    (cin 3) and lung (cin 2) models; the reference trains them one after the other,
+    train.py:27-38).
 
-    # MFMA operand mode of the concurrent step.  Exact f32: with the bf16-family row kernels
-    # (bf16 / bf16x3 / bf16x6) launching back to back on one stream, a producer -> consumer
-    # kernel pair on the other stream (stem input gradient: narrow conv -> reflect fold) was
-    # seen to read a few stale elements about once per 100-200 steps on MI355X
-    # (scripts/stress_narrow.py reproduces it; every kernel involved is correct in isolation
-    # and with f32 co-runners: 0 / 800).  Single-stream training is unaffected.
-    MMA = "f32"
+    schedule "serial" (default): the systems step one after the other on the caller's stream.
+    schedule "concurrent": one HIP stream per system; the kernels of one model fill the gaps of
+    the other (small normalisation / loss / Adam launches, split-K reductions, launch latency).
+    Workspaces are per stream (ops.workspace) and the kernels are deterministic, so each
+    model's numbers equal its own sequential run bit for bit in every MFMA operand mode
+    (tests/test_gpu_concurrent.py; guard bands around every output and workspace,
+    tests/test_gpu_guard.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
+    --dual-schedule groups, modules/parallel.py): each model on its own half of the ranks."""
 
-    def __init__(self, systems, device, schedule="concurrent"):
-        """schedule "concurrent": one HIP stream per system, exact-f32 operands (above);
-        "serial": the systems step one after the other on the caller's stream in the current
-        operand mode (bf16x6 by default), which on MI355X is the faster way to train both."""
+    def __init__(self, systems, device, schedule="serial"):
         if schedule not in ("concurrent", "serial"):
             raise ValueError("schedule must be 'concurrent' or 'serial'")
         self.systems = list(systems)
@@ -193,23 +193,17 @@ class ConcurrentCycleGANs:
         (device tensors, ready once the streams are synchronised with the caller's)."""
         if self.schedule == "serial":
             return [sysm.train_step(*b) for sysm, b in zip(self.systems, batches)]
-        from .hip import ops
-        prev = ops.get_mma()
-        ops.set_mma(self.MMA)
-        try:
-            cur = torch.cuda.current_stream(self.device)
-            out = []
-            for sysm, st, b in zip(self.systems, self.streams, batches):
-                st.wait_stream(cur)  # inputs produced on the caller's stream
-                with torch.cuda.stream(st):
-                    for t in b:
-                        if t is not None:
-                            t.record_stream(st)
-                    out.append(sysm.train_step(*b))
-            for st in self.streams:
-                cur.wait_stream(st)
-        finally:
-            ops.set_mma(prev)
+        cur = torch.cuda.current_stream(self.device)
+        out = []
+        for sysm, st, b in zip(self.systems, self.streams, batches):
+            st.wait_stream(cur)  # inputs produced on the caller's stream
+            with torch.cuda.stream(st):
+                for t in b:
+                    if t is not None:
+                        t.record_stream(st)
+                out.append(sysm.train_step(*b))
+        for st in self.streams:
+            cur.wait_stream(st)
         return out
 
 
@@ -337,7 +331,9 @@ def train_cycle_gan(args, target_range):
     nb = int(getattr(args, "num_residual_blocks", 9))
     torch.manual_seed(int(getattr(args, "seed", 0)))
     from . import losses as _losses
-    _losses.GLOBAL_STATS = bool(getattr(args, "global_loss_stats", False))
+    _losses.GLOBAL_STATS = False if getattr(args, "per_rank_loss_stats", False) else None
+    if rank == 0:
+        print(f"Batch-coupled loss statistics (ContrastRegion/ContrastEdge): {_losses.stats_mode()}")
     system = CycleGANSystem(input_channels, nb, use_cbam, lr=args.lr, lambda_cyc=args.lambda_cyc,
                             lambda_id=args.lambda_id, device=device)
     lr_lambda = lambda epoch: 1.0 - max(0, epoch + 1 - args.decay_epoch) / (args.epochs - args.decay_epoch)
@@ -352,7 +348,10 @@ def train_cycle_gan(args, target_range):
         print(f"=> No checkpoint found at '{ckpt_path}'")
 
     train_ds, val_ds = _build_datasets(args, n_masks)
-    per_rank = max(args.batch_size // world, 1)
+    if args.batch_size % world:
+        raise ValueError(f"--batch_size {args.batch_size} (the global batch, as in the reference) must be a "
+                         f"multiple of the {world} processes")
+    per_rank = args.batch_size // world
     tsampler = torch.utils.data.DistributedSampler(train_ds, world, rank, shuffle=True) if world > 1 else None
     vsampler = torch.utils.data.DistributedSampler(val_ds, world, rank, shuffle=False) if world > 1 else None
     nw = min(int(getattr(args, "num_workers", 0)), 16)
@@ -361,10 +360,12 @@ def train_cycle_gan(args, target_range):
         from .dataset import SliceBatchPreprocessor, collate
         prep, collate_fn = SliceBatchPreprocessor(args, device), collate
     dl = torch.utils.data.DataLoader(train_ds, batch_size=per_rank, shuffle=tsampler is None, sampler=tsampler,
-                                     num_workers=nw, pin_memory=True, drop_last=True,
+                                     num_workers=nw, pin_memory=True, drop_last=world > 1,
                                      persistent_workers=nw > 0, collate_fn=collate_fn)
     vdl = torch.utils.data.DataLoader(val_ds, batch_size=per_rank * 2, shuffle=False, sampler=vsampler,
                                       num_workers=nw, pin_memory=True, collate_fn=collate_fn)
+    if len(dl) == 0:
+        raise ValueError(f"no training batches: {len(train_ds)} slices for {world} processes x batch {per_rank}")
     fixed_val_batch = next(iter(vdl))
     if rank == 0:
         print(f"Train/Val split: {len(train_ds)} slices / {len(val_ds)} slices")

@@ -228,10 +228,32 @@ def gen_steps(rm, rt, n, hw, nb, cin, steps, seed, fname):
     np.savez_compressed(os.path.join(OUT, fname), **out)
 
 
+def gen_curve(rm, rt, n, hw, nb, cin, steps, seed, threads, fname):
+    """Loss curves of the reference step loop (modules/trainer.py:447-525) over `steps` steps
+    at BASELINE config 1, run once per torch thread count: the spread between the runs is the
+    reference's own run-to-run envelope (summation order), against which the HIP path's curve
+    is judged (tests/test_gpu_curve.py).  Only the loss history is stored."""
+    out = {"meta": np.array([n, hw, nb, cin, steps, seed]), "threads": np.array(threads)}
+    for th in threads:
+        torch.set_num_threads(th)
+        tmp = os.path.join(OUT, f".curve_tmp_{th}.npz")
+        gen_steps(rm, rt, n, hw, nb, cin, steps, seed, tmp)
+        z = np.load(tmp)
+        for k in z.files:
+            if k.startswith("loss_"):
+                out[f"t{th}:{k}"] = z[k]
+        os.remove(tmp)
+        print(f"curve: {th} threads done", flush=True)
+    np.savez_compressed(os.path.join(OUT, fname), **out)
+
+
 def main():
     torch.set_num_threads(8)
     torch.manual_seed(0)
     rm, rt = _load_reference()
+    if "--curve" in sys.argv:  # only the loss-curve fixture (minutes of CPU)
+        gen_curve(rm, rt, 2, 128, 1, 3, 50, 601, [1, 2, 4, 8], "curve_128.npz")
+        return
     gen_generator(rm, 3, 1, True, 2, 32, 101, "gen_cin3_nb1_32.npz")
     gen_generator(rm, 1, 9, True, 1, 32, 102, "gen_cin1_nb9_32.npz")
     gen_generator(rm, 2, 2, False, 2, 32, 103, "gen_cin2_nb2_nocbam_32.npz")
@@ -242,6 +264,7 @@ def main():
     gen_losses(rt, 2, 64, 401, "losses_64.npz")
     gen_losses(rt, 1, 48, 402, "losses_48.npz")
     gen_steps(rm, rt, 2, 64, 1, 3, 3, 501, "steps_64.npz")
+    gen_curve(rm, rt, 2, 128, 1, 3, 50, 601, [1, 2, 4, 8], "curve_128.npz")
     print("golden vectors written to", OUT)
 
 

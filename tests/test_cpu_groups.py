@@ -1,0 +1,131 @@
+"""Replica groups and the bucketed gradient exchange on the gloo backend (CPU, several processes).
+
+* world 4 cut into two groups (BASELINE config 5 as split GPU groups: soft-tissue model on ranks
+  0-1, lung model on ranks 2-3): inside each group the all-reduce-mean of the shard gradients
+  equals that model's full-batch gradient (oracle Generator, per-sample losses), and the
+  rank-0 broadcast gives each group its own first rank's weights;
+* world 2: GradBuckets (trainer.py's G exchange, launched from post-accumulate hooks while the
+  backward runs) equals one all-reduce-mean of the whole flat buffer, with a parameter reached
+  by two graph branches (as G_A2B's weights are) and one reached once, and both buckets go out
+  from inside the backward.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _setup(rank, world, port):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    from conftest import ROOT
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "ducosy-gan_amd")]
+    torch.set_num_threads(1)
+
+
+def _groups_worker(rank, world, port, q):
+    _setup(rank, world, port)
+    from modules import parallel
+    from oracle import prng
+    from oracle import ref_torch as orc
+    try:
+        parallel.init_from_env("gloo")
+        gi, _ = parallel.split_groups(2)
+        assert gi == rank // 2 and parallel.world() == 2 and parallel.rank() == rank % 2
+        cin = (3, 2)[gi]  # soft tissue / lung
+        shapes = orc.generator_param_shapes(cin, 1, True)
+        sd = prng.init_state_dict(shapes, 300 + rank)  # every rank starts different
+        flat = torch.cat([torch.from_numpy(v).reshape(-1) for v in sd.values()])
+        parallel.broadcast_(flat, 0)
+        first = torch.cat([torch.from_numpy(v).reshape(-1)
+                           for v in prng.init_state_dict(shapes, 300 + 2 * gi).values()])
+        assert torch.equal(flat, first)  # the group's own first rank, not global rank 0
+        p, off = {}, 0
+        for k, shp in shapes.items():
+            n = int(torch.Size(shp).numel())
+            p[k] = flat[off:off + n].view(shp).clone().requires_grad_(True)
+            off += n
+        x = torch.from_numpy(prng.uniform(40 + gi, "x", (4, cin, 16, 16), -1, 1))
+        t = torch.from_numpy(prng.uniform(40 + gi, "t", (4, 1, 16, 16), -1, 1))
+        lo, hi = parallel.shard(4)
+        orc.l1(orc.generator_forward(p, x[lo:hi], 1, True), t[lo:hi]).backward()
+        g = torch.cat([v.grad.reshape(-1) for v in p.values()])
+        parallel.allreduce_mean_(g)
+        if parallel.rank() == 0:
+            for v in p.values():
+                v.grad = None
+            orc.l1(orc.generator_forward(p, x, 1, True), t).backward()
+            full = torch.cat([v.grad.reshape(-1) for v in p.values()])
+            q.put((gi, float((g - full).norm() / full.norm())))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:
+        q.put((-1, repr(e)))
+        raise
+
+
+def _buckets_worker(rank, world, port, q):
+    _setup(rank, world, port)
+    from modules import parallel
+    try:
+        parallel.init_from_env("gloo")
+        flat = torch.zeros(10)
+        a = torch.nn.Parameter(torch.arange(4.0))
+        b = torch.nn.Parameter(torch.arange(6.0) - 2)
+        a.grad, b.grad = flat[:4].view(4), flat[4:].view(6)
+        sync = parallel.GradBuckets(flat, [[a], [b]])
+        x = torch.tensor(float(rank + 1))
+        sync.arm()
+        # a is used by two graph branches that reach it separately (two accumulations)
+        la = (a * x).sum()
+        lb = (a * a * x).sum() + (b.square() * x).sum()
+        torch.autograd.backward([la, lb])
+        early = sync.early
+        sync.finish()
+        sums = [sum(r + 1.0 for r in range(world))]
+        xm = sums[0] / world
+        want = torch.cat([xm * (1 + 2 * torch.arange(4.0)), xm * 2 * (torch.arange(6.0) - 2)])
+        q.put((rank, float((flat - want).abs().max()), early))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:
+        q.put((-1, repr(e), 0))
+        raise
+
+
+def _run(target, world, n_results):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=280) for _ in range(n_results)]
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(pr.exitcode == 0 for pr in procs), ([pr.exitcode for pr in procs], res)
+    return res
+
+
+@pytest.mark.timeout(300)
+def test_split_groups_world4():
+    res = _run(_groups_worker, 4, 2)
+    assert sorted(r[0] for r in res) == [0, 1], res
+    assert all(isinstance(r[1], float) and r[1] < 1e-5 for r in res), res
+
+
+@pytest.mark.timeout(300)
+def test_grad_buckets_world2():
+    res = _run(_buckets_worker, 2, 2)
+    for r in res:
+        assert r[0] >= 0, r
+        assert r[1] < 1e-6 and r[2] == 2, r  # both buckets launched from inside the backward

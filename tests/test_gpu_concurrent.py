@@ -19,26 +19,28 @@ def _batch(seed, i, n, hw, cin):
     return rA, rB, mk
 
 
-def test_concurrent_equals_sequential():
+@pytest.mark.parametrize("mode", ["bf16x6", "f32"])
+def test_concurrent_equals_sequential(mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
     n, hw, nb, steps = 2, 64, 2, 3
     cfg = [(3, 801), (2, 802)]
     prev = ops.get_mma()
-    ops.set_mma(ConcurrentCycleGANs.MMA)  # the sequential reference in the concurrent runner's mode
+    ops.set_mma(mode)
     try:
         seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
         want = [[{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)]
                 for m, (c, s) in zip(seq, cfg)]
+        run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV,
+                                  schedule="concurrent")
+        got = [[], []]
+        for i in range(steps):
+            outs = run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])
+            torch.cuda.synchronize()
+            for j, o in enumerate(outs):
+                got[j].append({k: float(v) for k, v in o.items()})
     finally:
         ops.set_mma(prev)
-    run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV)
-    got = [[], []]
-    for i in range(steps):
-        outs = run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])
-        torch.cuda.synchronize()
-        for j, o in enumerate(outs):
-            got[j].append({k: float(v) for k, v in o.items()})
     assert got == want
     for a, b in zip(seq, run.systems):
         assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)

@@ -43,7 +43,9 @@ def test_fullsize_steps_match_oracle():
         a, b, m = _inputs(seed, i, 1)
         want = oracle.step(a, b, m)
         got = {k: float(v) for k, v in gpu.train_step(a.to(DEV), b.to(DEV), m.to(DEV)).items()}
-        tol = 1e-3 if i == 0 else 1e-2
+        # step 1 follows one Adam update (measured 2.9e-4; the CPU reference itself moves ~2e-4 on the
+        # D losses across thread counts after one step)
+        tol = 1e-3 if i == 0 else 2e-3
         for k, ref in want.items():
             e = _rel(got[k], float(ref))
             worst[(i, k)] = e

@@ -121,6 +121,7 @@ def test_train_step_mma_modes_vs_reference_golden(mode, tol0):
     from modules.hip import ops
     z = np.load(os.path.join(GOLDEN, "steps_64.npz"))
     n, hw, nb, cin, steps, seed = [int(v) for v in z["meta"]]
+    prev = ops.get_mma()
     ops.set_mma(mode)
     try:
         s = _system(cin, nb, prng.step_model_seeds(seed))
@@ -134,4 +135,4 @@ def test_train_step_mma_modes_vs_reference_golden(mode, tol0):
                 scale = float(z[k][i]) if i == 0 else max(abs(float(z[k][i])), abs(float(z[k][0])))
                 assert abs(v - float(z[k][i])) <= tol * max(scale, 1e-2), (mode, i, k, v, float(z[k][i]))
     finally:
-        ops.set_mma("f32")
+        ops.set_mma(prev)
