@@ -63,13 +63,28 @@ def _conditioning(g, kind, hu_slices, device):
     return out
 
 
-def generate(args):
-    """generate.py:21-137: per patient, translate every NCCT slice with both models and write
-    raw / soft_tissue / lung DICOM copies under working_dir_root."""
+def _model_args(args, soft_tissue_args, lung_args):
+    """The reference passes the per-model settings as two extra namespaces (model_path, hu_min,
+    hu_max; modules/argmanager.py:52-82); this build's single parser carries them as
+    --model_path_soft / --soft_hu_min / ... on ``args``.  Either form is accepted."""
+    if soft_tissue_args is None:
+        soft_tissue_args = argparse.Namespace(model_path=args.model_path_soft, hu_min=args.soft_hu_min,
+                                              hu_max=args.soft_hu_max)
+    if lung_args is None:
+        lung_args = argparse.Namespace(model_path=args.model_path_lung, hu_min=args.lung_hu_min,
+                                       hu_max=args.lung_hu_max)
+    return soft_tissue_args, lung_args
+
+
+def generate(args, soft_tissue_args=None, lung_args=None):
+    """generate.py:21-137 (same signature): per patient, translate every NCCT slice with both
+    models and write raw / soft_tissue / lung DICOM copies under working_dir_root."""
     from modules import dicom
+    sa, la = _model_args(args, soft_tissue_args, lung_args)
     device = torch.device(f"cuda:{args.gpu_id}")
-    soft = load_generator(args.model_path_soft, device)
-    lung = load_generator(args.model_path_lung, device)
+    soft = load_generator(sa.model_path, device)
+    lung = load_generator(la.model_path, device)
+    batch = int(getattr(args, "slice_batch", 16))
     for dataset_name in args.dataset_names:
         input_dir = os.path.join(args.input_dir_root, dataset_name)
         working_dir = os.path.join(args.working_dir_root, dataset_name)
@@ -85,10 +100,10 @@ def generate(args):
             dcms = [dicom.dcmread(p) for p in paths]
             hu = [hu_from_stored(d.pixel_array, d.RescaleSlope, d.RescaleIntercept) for d in dcms]
             outs = {}
-            for name, model, lo, hi in (("soft_tissue", soft, args.soft_hu_min, args.soft_hu_max),
-                                        ("lung", lung, args.lung_hu_min, args.lung_hu_max)):
+            for name, model, lo, hi in (("soft_tissue", soft, sa.hu_min, sa.hu_max),
+                                        ("lung", lung, la.hu_min, la.hu_max)):
                 outs[name] = (translate_slices(model, [normalise_hu(h, lo, hi) for h in hu], args.img_size,
-                                               args.slice_batch, device, _conditioning(model, name, hu, device)),
+                                               batch, device, _conditioning(model, name, hu, device)),
                               lo, hi)
             for i, (p, d) in enumerate(zip(paths, dcms)):
                 try:
@@ -108,10 +123,12 @@ def generate(args):
     print("\nGeneration complete.")
 
 
-def synthesis(args):
-    """generate.py:140-297: merge the two translations inside their HU ranges over the NCCT,
-    z-smooth the volume and write output/{dataset}/{patient}/{idx:04d}.dcm."""
+def synthesis(args, soft_tissue_args=None, lung_args=None):
+    """generate.py:137-297 (same signature): merge the two translations inside their HU ranges
+    over the NCCT, z-smooth the volume (modules/postprocess.py) and write
+    output/{dataset}/{patient}/{idx:04d}.dcm."""
     from modules import dicom
+    sa, la = _model_args(args, soft_tissue_args, lung_args)
     for dataset_name in args.dataset_names:
         working_dir = os.path.join(args.working_dir_root, dataset_name)
         output_dir = os.path.join(args.output_dir_root, dataset_name)
@@ -126,7 +143,7 @@ def synthesis(args):
                 raw_hu = hu_from_stored(raw.pixel_array, getattr(raw, "RescaleSlope", 1),
                                         getattr(raw, "RescaleIntercept", 0))
                 merged.append(synthesize(raw.pixel_array, raw_hu, st.pixel_array, lg.pixel_array,
-                                         (args.soft_hu_min, args.soft_hu_max), (args.lung_hu_min, args.lung_hu_max)))
+                                         (sa.hu_min, sa.hu_max), (la.hu_min, la.hu_max)))
             vol = smooth_volume(merged)
             out_base = os.path.join(output_dir, os.path.basename(patient_dir))
             os.makedirs(out_base, exist_ok=True)
@@ -167,6 +184,7 @@ def get_args(argv=None):
 
 if __name__ == "__main__":
     a = get_args()
+    soft_a, lung_a = _model_args(a, None, None)
     if not a.skip_convert:
-        generate(a)
-    synthesis(a)
+        generate(a, soft_a, lung_a)
+    synthesis(a, soft_a, lung_a)

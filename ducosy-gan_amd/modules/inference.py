@@ -80,19 +80,11 @@ def synthesize(raw_stored: np.ndarray, raw_hu: np.ndarray, soft_stored: np.ndarr
 
 
 def smooth_volume(volume: Iterable[np.ndarray]) -> np.ndarray:
-    """generate.py:246-254 + modules/postprocess.py:6-117 ('gaussian3d', sharpen 1.7 / 1.2,
-    bone voxels >= 750 restored): z-smoothing of the merged stored-value volume, int16 out."""
-    from scipy.ndimage import gaussian_filter, gaussian_filter1d
-    vol = np.asarray(volume, dtype=np.float32)
-    vol = gaussian_filter1d(vol, sigma=0.8, axis=0)
-    original = vol.copy()
-    high = vol >= 750
-    smoothed = gaussian_filter(vol, sigma=(0.7, 0.05, 0.05))
-    amount, radius = 1.7, 1.2
-    sm = smoothed.astype(np.float64)
-    og = original.astype(np.float64)
-    hf = sm - gaussian_filter(sm, sigma=(0, radius, radius))
-    ohf = og - gaussian_filter(og, sigma=(0, radius, radius))
-    sharp = np.clip(sm + ((1 - amount) * hf + amount * ohf) * amount, og.min(), og.max())
-    sharp[high] = og[high]
-    return sharp.astype(np.int16)
+    """generate.py:246-254: z Gaussian (sigma 0.8) of the merged stored-value volume, then
+    modules/postprocess.py's 'gaussian3d' (sigma_z 0.7, sigma_xy 0.05) with sharpening (1.7 /
+    1.2); voxels >= 750 keep their value; int16 out."""
+    from scipy.ndimage import gaussian_filter1d
+    from .postprocess import postprocess_ct_volume
+    vol = gaussian_filter1d(np.asarray(volume, dtype=np.float32), sigma=0.8, axis=0)
+    return postprocess_ct_volume(vol, method="gaussian3d", sigma_z=0.7, sigma_xy=0.05, enhance_sharpness=True,
+                                 sharpen_amount=1.7, sharpen_radius=1.2)

@@ -1,0 +1,75 @@
+"""The pre-split LDS-DMA bf16x6 residual conv (csrc/conv_x6p.hip) against the split-in-the-gather
+bf16x6 rows kernel of conv.hip and against float64.
+
+Both kernels issue the same six bf16 products per operand pair in the same order into the same
+two-level fp32 chains (inner chains of 128 k), from the same hi/mid/lo split: their outputs
+must be bit-identical.  Cases: the forward (reflection padding 1) and the stride-1 data
+gradient (zero padding 2 onto the padded grid), a pixel count that is not a multiple of the
+128-row tile, and more than one image.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _res():
+    from modules.hip.lib import DCS_PAD_REFLECT
+    from modules.hip.ops import ConvGeom
+    return ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT)
+
+
+def _run(x6p, fn):
+    from modules.hip import ops
+    prev_mode, prev = ops.get_mma(), ops._X6P
+    ops.set_mma("bf16x6")
+    ops._X6P = x6p
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    finally:
+        ops._X6P = prev
+        ops.set_mma(prev_mode)
+
+
+@pytest.mark.parametrize("n,h", [(2, 16), (3, 13), (1, 32)])
+def test_x6p_forward_and_dgrad_bit_exact(n, h):
+    from modules.hip import ops
+    g = _res()
+    x = torch.from_numpy(prng.normal(61, f"x{n}{h}", (n, h, h, 256))).float().to(DEV)
+    w = torch.from_numpy(prng.normal(62, "w", (256, 256, 3, 3), 0, 0.02)).float().to(DEV)
+    dy = torch.from_numpy(prng.normal(63, f"dy{n}{h}", (n, h, h, 256))).float().to(DEV)
+    wp, wd = g.pack_fwd(w), g.pack_dgrad(w)
+    d = g._desc_fwd(ops.Src.nhwc(x), wp.shape[1], 0, 0)
+    d.mma = 6
+    from modules.hip import lib
+    import ctypes
+    assert lib.query("dcs_conv_rows_x6p_ok", ctypes.byref(d)) == 1
+    f_new = _run(True, lambda: g.forward(ops.Src.nhwc(x), wp))
+    f_old = _run(False, lambda: g.forward(ops.Src.nhwc(x), wp))
+    assert torch.equal(f_new, f_old), float((f_new - f_old).abs().max())
+    b_new = _run(True, lambda: g.dgrad(dy, wd, h, h))
+    b_old = _run(False, lambda: g.dgrad(dy, wd, h, h))
+    assert torch.equal(b_new, b_old), float((b_new - b_old).abs().max())
+    # and against float64 (reflect pad + conv), at the fp32-class bar of tests/test_gpu_mma.py
+    xd = x.double().permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xd, (1, 1, 1, 1), mode="reflect"), w.double())
+    err = float((f_new.double().permute(0, 3, 1, 2) - ref).abs().max() / ref.abs().max())
+    assert err < 2e-6, err
+
+
+def test_split_x6_planes():
+    """dcs_split_x6: v = hi + mid + lo exactly representable pieces, interleaved per 8 elements."""
+    from modules.hip import ops
+    x = torch.from_numpy(prng.normal(64, "s", (4096,))).float().to(DEV) * 3.7
+    sp = ops.split_x6(x).view(-1, 3, 8).view(torch.bfloat16).float()  # [groups][plane][8]
+    rec = (sp[:, 0] + sp[:, 1] + sp[:, 2]).reshape(-1)
+    err = (rec - x).abs() / x.abs().clamp_min(1e-30)
+    assert float(err.max()) < 2 ** -22
+    hi = x.view(-1, 8).to(torch.bfloat16).float()
+    assert torch.equal(sp[:, 0], hi)
