@@ -100,6 +100,7 @@ constexpr int NT = 256;
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
 
+
 // ---------------------------------------------------------------------------------------
 // geometry helpers
 // ---------------------------------------------------------------------------------------
@@ -280,6 +281,18 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
     if (nmajor) { col = (int)(idx / Kpad); k = (int)(idx - (long long)col * Kpad); }
     else { k = (int)(idx / ncols); col = (int)(idx - (long long)k * ncols); }
     int taps = KH * KW;
+    if (kind & DCS_PACK_KSLICE) {  // K rows in slice-major order: k' = (c/16)*taps*16 + tap*16 + c%16
+        kind &= 7;
+        const int C = kind == 0 ? Cin : Cout;  // reduction channels per tap
+        const int per = taps * 16;
+        if (k < taps * C) {
+            const int slice = k / per, rem = k - slice * per;
+            const int tap = rem >> 4, cs = rem & 15;
+            k = tap * C + slice * 16 + cs;
+        } else {
+            k = 1 << 30;  // K padding: zero
+        }
+    }
     float v = 0.f;
     if (kind == 3 || kind == 4) {
         // nearest-x2 upsample + 3x3 conv (zero pad 1) split into sub-pixel phases; each
@@ -512,8 +525,8 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
     // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap)
     const int arow = tid >> 1, akq = (tid & 1) * AKPT;
     const RowInfo ri = row_info(d, g, (int)(m0 + arow));
-    if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     const bool rvalid = ri.out_off >= 0;
+    if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     // B loader: one output channel row, BKPT consecutive k
     const int brow = tid / BTPR, bkq = (tid % BTPR) * BKPT;
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
@@ -525,12 +538,29 @@ __global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_r
     const long long so = (long long)ri.n * d.Cs;
     const __amdgpu_buffer_rsrc_t arsrc = src_rsrc(src);
 
-    // incremental (tap, channel) state of the next k-tile to load, for A and B
-    int aj = akq / d.Cs, ac = akq - (akq / d.Cs) * d.Cs;
+    // incremental (tap, channel) state of the next k-tile to load, for A and B.  TAG 1 (the
+    // residual convs) runs the DCS_KORDER_SLICE K order: all taps of a 16-channel slice, then
+    // the next slice, so the source rows a slice gathers are re-read by its next taps from
+    // L1/L2 instead of after a sweep over all channels (the dispatch requires d.korder == SLICE)
+    constexpr bool KS = TAG == 1;
+    int aj, ac;
+    if constexpr (KS) {
+        const int p0 = akq >> 4;
+        aj = p0 % g.ntaps;
+        ac = (p0 / g.ntaps) * 16 + (akq & 15);
+    } else {
+        aj = akq / d.Cs;
+        ac = akq - (akq / d.Cs) * d.Cs;
+    }
     int bj = bkq / d.Cs, bc = bkq - (bkq / d.Cs) * d.Cs;
     auto advance = [&](int& j, int& c) {
-        c += BKT;
-        while (c >= d.Cs) { c -= d.Cs; ++j; }
+        if constexpr (KS) {
+            j += BKT / 16;
+            while (j >= g.ntaps) { j -= g.ntaps; c += 16; }
+        } else {
+            c += BKT;
+            while (c >= d.Cs) { c -= d.Cs; ++j; }
+        }
     };
 
     float4 ra[ACH];
@@ -1551,7 +1581,10 @@ using namespace dcs;
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                 int Kpad, int ncols, int nmajor, float* out, void* stream) {
     if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
-        (kind != 5 && ci_count > Cin) || (kind == 5 && ci_count < Cin) || kind < 0 || kind > 5)
+        (kind != 5 && ci_count > Cin) || (kind == 5 && ci_count < Cin) || kind < 0 ||
+        (kind & 7) > 5 || (kind & ~(7 | DCS_PACK_KSLICE)) ||
+        ((kind & DCS_PACK_KSLICE) && (((kind & 7) != 0 && (kind & 7) != 1) ||
+                                      ((kind & 7) == 0 ? Cin : Cout) % 16 != 0)))
         return fail(DCS_E_INVALID, "pack_weights: bad arguments");
     if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
     long long total = (long long)Kpad * ncols;
@@ -1583,8 +1616,15 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     dim3 grid((unsigned)(gx * gy * ncls));
     const bool vec = vec_ok(dp, src);
     const bool v4 = !vec && vec4_ok(dp, src) && d.pro_act == DCS_ACT_NONE && !d.parity;
-    const bool res = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
-                     d.stride == 1 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
+    const bool res_geom = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
+                          d.stride == 1 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
+    // the residual-geometry kernels (TAG 1) run the slice-major K order, every other kernel the
+    // tap-major one: the weights must have been packed to match
+    const bool res = res_geom && d.korder == DCS_KORDER_SLICE;
+    if (d.korder == DCS_KORDER_SLICE && !(res_geom && vec_ok(dp, src)))
+        return fail(DCS_E_INVALID, "conv_rows: DCS_KORDER_SLICE is implemented for the 256-channel 3x3 stride-1 "
+                                   "residual geometry with a vectorisable source");
+    if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
     if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64)) {  // x6: 128- or 64-column tiles
         if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);

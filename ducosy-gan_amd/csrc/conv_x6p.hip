@@ -564,7 +564,8 @@ extern "C" int dcs_conv_rows_x6p_ok(const dcs_conv_desc* dp) {
     const dcs_conv_desc& d = *dp;
     const long long src_bytes = (long long)d.N * d.Hs * d.Ws * d.Cs * 6;
     const long long w_bytes = (long long)cdiv(d.Co, XP_BN) * XP_BN * d.ldb * 6;
-    return d.parity == 0 && d.stride == 1 && d.up == 1 && d.Cs % XP_BK == 0 && d.Co % XP_BN == 0 &&
+    return d.korder == DCS_KORDER_TAP && d.parity == 0 && d.stride == 1 && d.up == 1 && d.Cs % XP_BK == 0 &&
+           d.Co % XP_BN == 0 &&
            d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE &&
            d.ldb >= d.KH * d.KW * d.Cs && d.ldb % 32 == 0 && d.KH * d.KW <= 64 &&
            (d.pad_mode == DCS_PAD_ZERO || d.pad_mode == DCS_PAD_REFLECT) &&

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("DUCOSY_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libdu
 DCS_PAD_ZERO, DCS_PAD_REFLECT = 0, 1
 ACT_NONE, ACT_AFFINE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3, 4
 MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6 = 0, 1, 3, 6
+KORDER_TAP, KORDER_SLICE, PACK_KSLICE = 0, 1, 8
 
 
 class ConvDesc(ctypes.Structure):
@@ -29,6 +30,7 @@ class ConvDesc(ctypes.Structure):
         ("stride", c_int32), ("parity", c_int32),
         ("Ho", c_int32), ("Wo", c_int32), ("Co", c_int32),
         ("ldb", c_int32), ("pro_act", c_int32), ("epi_act", c_int32), ("mma", c_int32),
+        ("korder", c_int32),
     ]
 
 

@@ -31,6 +31,8 @@ _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
 # bf16x6 residual convs on pre-split operands staged by LDS-DMA (csrc/conv_x6p.hip); 0 = the
 # split-in-the-gather rows kernel of conv.hip (A/B switch)
 _X6P = os.environ.get("DUCOSY_X6P", "0") == "1"
+# residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
+_KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
 
 
 def set_mma(mode: str) -> None:
@@ -201,6 +203,15 @@ class ConvGeom:
     pad_mode: int = DCS_PAD_ZERO
     up: int = 1  # nearest upsampling of the input before the conv
 
+    @property
+    def kslice(self) -> bool:
+        """The residual convs run the slice-major K order (include/ducosy_hip.h
+        DCS_KORDER_SLICE: 3.7x fewer L2 misses on the gathered rows, 4 % faster in bf16x6) in the
+        bf16 operand modes; their packed weights follow it.  The exact-f32 kernel keeps the
+        tap-major order (its gather decodes the tap once per 8 k-tiles there), as does the
+        pre-split x6p path (conv_x6p.hip)."""
+        return _is_res_geom(self) and _KSLICE and not _X6P and _MMA != lib.MMA_F32
+
     def out_hw(self, H, W):
         Hv, Wv = H * self.up, W * self.up
         t, l, b, r = self.pads
@@ -239,6 +250,8 @@ class ConvGeom:
         return self._pack(w, kind, ci, K, ci)
 
     def _pack(self, w, kind, ci_count, K, ncols):
+        if kind in (0, 1) and ncols > 4 and self.kslice:
+            kind |= lib.PACK_KSLICE
         if ncols <= 4:
             Kpad, cols, nmajor = K, (1 if ncols == 1 else 4), 0
             out = torch.empty(Kpad, cols, device=w.device, dtype=torch.float32)
@@ -270,6 +283,7 @@ class ConvGeom:
         d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
         d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
         d.mma = _MMA
+        d.korder = lib.KORDER_SLICE if (rows and self.kslice and not self.narrow) else lib.KORDER_TAP
         return d
 
     # ---- forward -------------------------------------------------------------------
@@ -314,6 +328,7 @@ class ConvGeom:
         d.KH = d.KW = self.k
         d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
         d.mma = _MMA
+        d.korder = lib.KORDER_SLICE if (self.kslice and ci > 4) else lib.KORDER_TAP
         d.Co = ci
         dev = dy.device
         t, l, b, r = self.pads

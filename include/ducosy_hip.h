@@ -72,7 +72,18 @@ typedef struct dcs_conv_desc {
     int32_t epi_act;                /* DCS_ACT_NONE / DCS_ACT_TANH / DCS_ACT_LRELU        */
     int32_t mma;                    /* MFMA operands: DCS_MMA_F32 (exact; 0 = zeroed desc) */
                                     /* or DCS_MMA_BF16 / _BF16X3 / _BF16X6 (f32 accum.)   */
+    int32_t korder;                 /* GEMM K order of the rows pass (and of its packed    */
+                                    /* weights): DCS_KORDER_TAP (tap-major) or            */
+                                    /* DCS_KORDER_SLICE (16-channel slices, taps inside)  */
 } dcs_conv_desc;
+
+/* K order of the rows pass.  TAP: k = tap * Cs + c.  SLICE: k = (c / 16) * taps * 16 + tap * 16 +
+ * c % 16 — every tap of a 16-channel slice before the next slice, so the gathered source rows
+ * of a slice are re-read from L2 / L1 by the next taps instead of after a whole tap sweep
+ * (regular stride-1 rows, Cs % 16 == 0; pack the weights with DCS_PACK_KSLICE). */
+#define DCS_KORDER_TAP 0
+#define DCS_KORDER_SLICE 1
+#define DCS_PACK_KSLICE 8
 
 /* MFMA operand modes of the MFMA convolution passes (dcs_conv_desc.mma).  F32 is exact fp32
  * (the reference's precision).  BF16 rounds both GEMM operands to bf16 (BASELINE config 5's
@@ -99,6 +110,7 @@ int dcs_version(void);
  * kind 3 / 4      : sub-pixel forward / data gradient of nearest-x2 upsample + 3x3 conv
  * kind 5 fwd-pad  : B[(ty*KW+tx)*ci_count + ci][co] = ci < Cin ? W[co][ci][ty][tx] : 0
  *                   (forward over a source whose channels are zero-padded to ci_count)
+ * kind | DCS_PACK_KSLICE (kinds 0 and 1): the same B with its K rows in DCS_KORDER_SLICE order
  * ci_count limits the packed input channels (dgrad of a concat input needs only the first). */
 int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                      int Kpad, int ncols, int nmajor, float* out, void* stream);

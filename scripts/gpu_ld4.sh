@@ -1,0 +1,14 @@
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_mma.py tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_precision.py tests/test_gpu_train.py > gpurun_out/ld4_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAIL|Error|assert" gpurun_out/ld4_tests.log | head -30; tail -30 gpurun_out/ld4_tests.log; exit 1; }
+tail -1 gpurun_out/ld4_tests.log
+for v in ld4 no ld4 no; do
+  LIB=$R/ducosy-gan_amd/lib/libducosy_hip.so; [ $v = no ] && LIB=$R/ducosy-gan_amd/lib/libducosy_hip_noLD4.so
+  DUCOSY_HIP_LIB=$LIB timeout -k 10 200 python scripts/kbench.py --only res --mma bf16x6 --reps 7 > gpurun_out/ld4_kb_$v.log 2>&1 || exit 1
+  echo "$v"; grep res gpurun_out/ld4_kb_$v.log | head -2
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU -d $R/gpurun_out/pmc_ld4_1 -o p --output-format csv -- python3 $R/scripts/kbench.py --only res --mma bf16x6 --reps 2 > $R/gpurun_out/pmc_ld4.log 2>&1 || exit 1
+timeout -k 10 200 python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/ld4_bench.log 2>&1 || exit 1
+tail -1 $R/gpurun_out/ld4_bench.log | cut -c1-200

@@ -12,3 +12,6 @@ for v in full nodma nobar nolds old; do
   echo "$v"; grep res $R/gpurun_out/skel_$v.log | head -2
   DUCOSY_HIP_LIB=$LIB DUCOSY_X6P=$X DCS_X6P_VARIANT=3 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $R/gpurun_out/pmc_skel_${v}_1 -o p --output-format csv -- python3 $R/scripts/kbench.py --only res --mma bf16x6 --reps 2 > $R/gpurun_out/pmc_skel_$v.log 2>&1 || exit 1
 done
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r02_step_trace -o k --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/r02_step_trace.log 2>&1 || exit 1
+echo trace ok

@@ -24,16 +24,18 @@ def _res():
 
 
 def _run(x6p, fn):
+    """fn(packed forward weights, packed dgrad weights) with the x6p pass on, or with conv.hip's
+    bf16x6 rows kernel in the same (tap-major) K order."""
     from modules.hip import ops
-    prev_mode, prev = ops.get_mma(), ops._X6P
+    prev_mode, prev, prev_ks = ops.get_mma(), ops._X6P, ops._KSLICE
     ops.set_mma("bf16x6")
-    ops._X6P = x6p
+    ops._X6P, ops._KSLICE = x6p, False
     try:
         out = fn()
         torch.cuda.synchronize()
         return out
     finally:
-        ops._X6P = prev
+        ops._X6P, ops._KSLICE = prev, prev_ks
         ops.set_mma(prev_mode)
 
 
@@ -44,17 +46,16 @@ def test_x6p_forward_and_dgrad_bit_exact(n, h):
     x = torch.from_numpy(prng.normal(61, f"x{n}{h}", (n, h, h, 256))).float().to(DEV)
     w = torch.from_numpy(prng.normal(62, "w", (256, 256, 3, 3), 0, 0.02)).float().to(DEV)
     dy = torch.from_numpy(prng.normal(63, f"dy{n}{h}", (n, h, h, 256))).float().to(DEV)
-    wp, wd = g.pack_fwd(w), g.pack_dgrad(w)
-    d = g._desc_fwd(ops.Src.nhwc(x), wp.shape[1], 0, 0)
-    d.mma = 6
+    d = g._desc_fwd(ops.Src.nhwc(x), 2304, 0, 0)
+    d.mma, d.korder = 6, 0
     from modules.hip import lib
     import ctypes
     assert lib.query("dcs_conv_rows_x6p_ok", ctypes.byref(d)) == 1
-    f_new = _run(True, lambda: g.forward(ops.Src.nhwc(x), wp))
-    f_old = _run(False, lambda: g.forward(ops.Src.nhwc(x), wp))
+    f_new = _run(True, lambda: g.forward(ops.Src.nhwc(x), g.pack_fwd(w)))
+    f_old = _run(False, lambda: g.forward(ops.Src.nhwc(x), g.pack_fwd(w)))
     assert torch.equal(f_new, f_old), float((f_new - f_old).abs().max())
-    b_new = _run(True, lambda: g.dgrad(dy, wd, h, h))
-    b_old = _run(False, lambda: g.dgrad(dy, wd, h, h))
+    b_new = _run(True, lambda: g.dgrad(dy, g.pack_dgrad(w), h, h))
+    b_old = _run(False, lambda: g.dgrad(dy, g.pack_dgrad(w), h, h))
     assert torch.equal(b_new, b_old), float((b_new - b_old).abs().max())
     # and against float64 (reflect pad + conv), at the fp32-class bar of tests/test_gpu_mma.py
     xd = x.double().permute(0, 3, 1, 2)
