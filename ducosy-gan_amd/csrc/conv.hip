@@ -99,6 +99,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
+#ifndef DCS_X6_BM256
+#define DCS_X6_BM256 1  // bf16x6 residual rows: 256 x 128 tiles (512 threads)
+#endif
 
 
 // ---------------------------------------------------------------------------------------
@@ -467,16 +470,20 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
 
 // VEC: 0 scalar gather (any layout), 1 = 16 consecutive k of one tap per thread (Cs % 16 == 0),
 //      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
+// BM = 256 (bf16x6, 128 columns): 512 threads as 4 x 2 waves of 64 x 64, one workgroup per CU;
+// every staged weight k-tile then feeds twice the pixels (0.75 of the 128-row tile's bytes per MFMA)
 template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
-__global__ __launch_bounds__(NT, MMA == MMA_BF16X6 ? DCS_X6_OCC : 2) void conv_rows_kernel(
+__global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    static_assert(BM == 128, "A loader assumes 128 rows (2 threads per row)");
-    constexpr int WM = BM / 2, WN = BN / 2;        // per-wave tile
+    static_assert(BM == 128 || (BM == 256 && MMA == MMA_BF16X6 && BN == 128 && VEC == 1),
+                  "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
+    constexpr int NTH = 2 * BM;                    // threads (two per A row)
+    constexpr int WM = 64, WN = BN / 2;            // per-wave tile
     constexpr int IM = WM / 32, JN = WN / 32;      // 32x32 blocks per wave
-    constexpr int BTPR = NT / BN;                  // B loader threads per row (2 or 4)
+    constexpr int BTPR = NTH / BN;                 // B loader threads per row (2 or 4)
     // bf16: 64-deep k-tiles (twice the MFMA work per round of global loads: the bf16 passes are
     // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
     constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : BK;  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
@@ -1627,7 +1634,14 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
     if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64)) {  // x6: 128- or 64-column tiles
-        if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        // 256-row tiles where they divide the pixels evenly (the forward over whole 128 x 128
+        // images); the 130 x 130 padded data gradient keeps 128-row tiles (measured: its partial
+        // last dispatch round and zero-padded border rows make the big tile 7 % slower there)
+        if (BN == 128 && res && DCS_X6_BM256 && Mmax % 256 == 0) {
+            const int gx2 = (int)cdiv(Mmax, 256);
+            hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16X6>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
+                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy);
+        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
         else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
         else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
         return check_launch("conv_rows");
