@@ -126,8 +126,12 @@ __global__ __launch_bounds__(XP_NT, 2) void conv_rows_x6p_kernel(const dcs_conv_
     unsigned abase = tap_base(0);
     auto issue = [&](int kt, int stage) {
         unsigned char* s = lds + stage * XP_STAGE_BYTES + wid * 1024;
-        const unsigned ao = abase == XP_OOB ? XP_OOB : abase + (unsigned)dc * 96u;
-        const unsigned bo = bbase + (unsigned)kt * 96u;
+        unsigned ao = abase == XP_OOB ? XP_OOB : abase + (unsigned)dc * 96u;
+        unsigned bo = bbase + (unsigned)kt * 96u;
+#ifdef DCS_XP_L2PROBE  // skeleton probe: every A piece from a 64 KiB window (L2/L1 hits), B from 64 KiB
+        ao &= 0xffffu;
+        bo &= 0xffffu;
+#endif
 #pragma unroll
         for (int q = 0; q < 3; ++q) xp_dma(ra, s + q * XP_PLANE_BYTES, ao + 16u * q);
 #pragma unroll
