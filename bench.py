@@ -76,26 +76,19 @@ def cpu_baseline(img, blocks, cin, threads):
                       f"({dt:.2f} s)"}
 
 
-def _pmc_traffic(mode):
-    """HBM bytes per launch of the dominant kernel in this mode from the committed rocprofv3 PMC
-    passes (profiles/pmc_resconv_MODE.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+def _pmc_record(mode):
+    """HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction) and MFMA-busy of the
+    dominant kernel from the committed rocprofv3 PMC passes (profiles/pmc_resconv_MODE.json, written
+    by scripts/hbm_table.py).  PMC passes cannot run inside the timed loop, so these are NOT
+    measured in this run: the record carries the profile's commit and source next to them."""
     p = os.path.join(ROOT, "profiles", f"pmc_resconv_{mode}.json")
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            j = json.load(f)
     except (OSError, ValueError):
-        return None
-
-
-def _pmc_mfma_busy(mode):
-    """MFMA-busy fraction of the dominant kernel in this mode from the committed rocprofv3 pass
-    (profiles/mfma_busy.json: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8))."""
-    p = os.path.join(ROOT, "profiles", "mfma_busy.json")
-    try:
-        with open(p) as f:
-            return json.load(f).get(mode, {}).get("mfma_busy_fraction")
-    except (OSError, ValueError):
-        return None
+        return None, None, None
+    src = f"{j.get('source', p)} at commit {j.get('commit', '?')}"
+    return j.get("hbm_bytes_per_launch"), j.get("mfma_busy_fraction"), src
 
 
 def main():
@@ -196,6 +189,7 @@ def main():
     if rank == 0:
         value = world * models * args.batch * args.steps / elapsed
         achieved = flop_launch / (ms_launch * 1e-3) / 1e12 if ms_launch > 0 else 0.0
+        pmc = _pmc_record(args.mma)
         if args.workload == "g_a2b":
             workload = ("Generator_A2B (ResNet-9 + CBAM) forward + backward (weight and input gradients), "
                         "BASELINE config 2")
@@ -230,14 +224,18 @@ def main():
                 "parallelism": f"2 groups x dp{world // 2}" if groups else f"dp{world}",
             },
             "roofline": {
-                "kernel": f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)",
+                "kernel": (f"256-ch 3x3 residual conv rows pass: forward conv_rows_kernel<256,128,1,1,{MODE_TAG[args.mma]}>, "
+                           f"data gradient conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}>"
+                           if args.mma == "bf16x6" else
+                           f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)"),
                 "bound": "mfma",
                 "achieved": round(achieved, 3),
                 "peak": round(MODE_PEAK[args.mma], 1),
                 "unit": "TFLOP/s",
                 "frac": round(achieved / MODE_PEAK[args.mma], 4),
-                "traffic": _pmc_traffic(args.mma),
-                "mfma_busy": _pmc_mfma_busy(args.mma),
+                "traffic": pmc[0],
+                "mfma_busy": pmc[1],
+                "traffic_source": pmc[2],
                 "launches": n_launch,
                 "ms_per_launch": round(ms_launch, 4),
                 "gflop_per_launch": round(flop_launch / 1e9, 3),
