@@ -513,6 +513,12 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         return ((pl * 2 + buf) * (BM + BN) + row) * 16 + 8 * (h ^ ((row >> 3) & 1));
     };
     __shared__ long long rowoff[BM];
+    // bf16x6 prologue (TAG 0): the per-(image, channel) scale / shift of the <= 2 images a tile
+    // spans, staged once, so the affine at the LDS store reads LDS instead of issuing global
+    // loads that would wait behind the prefetched gathers
+    constexpr bool PRO_LDS = MMA == MMA_BF16X6 && TAG != 1;
+    constexpr int PRO_CMAX = 512;
+    __shared__ __attribute__((aligned(16))) float prol[PRO_LDS ? 4 * PRO_CMAX : 4];
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -544,6 +550,25 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     const float* srow = src + ri.n * d.s_n;
     const long long so = (long long)ri.n * d.Cs;
     const __amdgpu_buffer_rsrc_t arsrc = src_rsrc(src);
+    bool pro_lds = false;  // block-uniform
+    int pro_base = 0;      // n_lo * Cs: psc/psh index of prol[0]
+    if constexpr (PRO_LDS) {
+        if (d.pro_act != DCS_ACT_NONE && d.Cs <= PRO_CMAX && d.parity != 2) {
+            const long long per = (long long)g.My * g.Mx;
+            const int n_lo = (int)(m0 / per);
+            const int n_hi = (int)(((m0 + BM < M ? m0 + BM : M) - 1) / per);
+            if (n_hi - n_lo <= 1) {
+                pro_lds = true;
+                pro_base = n_lo * d.Cs;
+                for (int i = tid; i < 2 * d.Cs; i += NTH) {
+                    const bool ok = n_lo + i / d.Cs < d.N;
+                    prol[i] = ok ? psc[pro_base + i] : 0.f;
+                    prol[2 * PRO_CMAX + i] = ok ? psh[pro_base + i] : 0.f;
+                }
+            }
+        }
+        __syncthreads();
+    }
 
     // incremental (tap, channel) state of the next k-tile to load, for A and B.  TAG 1 (the
     // residual convs) runs the DCS_KORDER_SLICE K order: all taps of a 16-channel slice, then
@@ -573,7 +598,10 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     float4 ra[ACH];
     float4 rb[BCH];
 
-    auto load_a = [&](int kt, auto& dst) {
+    // pa: bf16x6 defers the prologue affine to the LDS store (a load consumed at once would make
+    // the next tile's gather wait); it records the channel offset into psc/psh, -1 for none
+    auto load_a = [&](int kt, auto& dst, int& pa) {
+        pa = -1;
         if (VEC == 2) {  // Cs == 4: taps aj .. aj+3, one float4 each (no prologue)
             dst[0] = dst[1] = dst[2] = dst[3] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid) {
@@ -594,7 +622,9 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
             // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
             int sy = 0, sx = 0, off = OOB_OFF;
-            if (aj < g.ntaps) {
+            // past the last k-tile (the x6 pipeline's unconditional prefetch) the walk leaves the
+            // range through aj (tap-major) or through ac (slice-major): both must stay in range
+            if (aj < g.ntaps && ac < d.Cs) {
                 int ady, adx, bt;
                 tap_decode(d, g, aj, ady, adx, bt);
                 const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
@@ -603,7 +633,9 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             }
 #pragma unroll
             for (int i = 0; i < ACH; ++i) dst[i] = buf_load4(arsrc, off + 16 * i);
-            if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
+            if constexpr (MMA == MMA_BF16X6) {
+                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa = (int)so + ac;
+            } else if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
 #pragma unroll
                 for (int i = 0; i < ACH; ++i) dst[i] = affine_act4(dst[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
             }
@@ -648,6 +680,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             }
         }
     };
+    const __amdgpu_buffer_rsrc_t brsrc = src_rsrc(wp);
     auto load_b = [&](int kt, auto& dst) {
         long long col;
         bool ok = true;
@@ -660,11 +693,33 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             col = (long long)bt * d.Cs + bc;
             advance(bj, bc);
         }
+        if constexpr (MMA == MMA_BF16X6) {  // branch-free: k-tiles past the end read zeros
+            const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
 #pragma unroll
-        for (int i = 0; i < BCH; ++i)
-            dst[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int i = 0; i < BCH; ++i) dst[i] = buf_load4(brsrc, off + 16 * i);
+        } else {
+#pragma unroll
+            for (int i = 0; i < BCH; ++i)
+                dst[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     };
-    auto store_tiles = [&](int buf, const auto& sa, const auto& sb) {
+    auto store_tiles = [&](int buf, const auto& sa0, const auto& sb, int pa) {
+        float4 sa[ACH];
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) sa[i] = sa0[i];
+        if constexpr (MMA == MMA_BF16X6) {
+            if (d.pro_act != DCS_ACT_NONE && pa >= 0) {
+                if (pro_lds) {
+                    const int q = pa - pro_base;
+#pragma unroll
+                    for (int i = 0; i < ACH; ++i)
+                        sa[i] = affine_act4(sa[i], prol + q + 4 * i, prol + 2 * PRO_CMAX + q + 4 * i, d.pro_act);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < ACH; ++i) sa[i] = affine_act4(sa[i], psc + pa + 4 * i, psh + pa + 4 * i, d.pro_act);
+                }
+            }
+        }
         if constexpr (MMA == MMA_F32) {
 #pragma unroll
             for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = sa[i];
@@ -729,9 +784,10 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    load_a(0, ra);
+    int pa0 = -1, pa1 = -1;
+    load_a(0, ra, pa0);
     load_b(0, rb);
-    store_tiles(0, ra, rb);
+    store_tiles(0, ra, rb, pa0);
     __syncthreads();
 
     const int l32 = lane & 31, lk = (lane >> 5) * 16;
@@ -803,19 +859,26 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         if constexpr (MMA == MMA_BF16X6 && DCS_X6_PIPE) {
             // two register sets: tile kt+2's gather is in flight while tile kt computes, so
             // staging tile kt+1 waits only for loads issued a whole k-tile earlier
+            // The loads are issued unconditionally (k-tiles past the end gather zeros from the
+            // buffer descriptors): a load under a branch makes the compiler's vmcnt bookkeeping
+            // assume it may be missing and wait for every load at the next LDS store.
             float4 ra2[ACH], rb2[BCH];
-            if (1 < nkt) { load_a(1, ra); load_b(1, rb); }
+            int pa2 = -1;
+            load_a(1, ra, pa1);
+            load_b(1, rb);
             for (int kt = 0; kt < nkt; kt += 2) {
-                if (kt + 2 < nkt) { load_a(kt + 2, ra2); load_b(kt + 2, rb2); }
+                load_a(kt + 2, ra2, pa2);
+                load_b(kt + 2, rb2);
                 step(0, 0);
                 fold_t(kt);
-                if (kt + 1 < nkt) store_tiles(1, ra, rb);
+                if (kt + 1 < nkt) store_tiles(1, ra, rb, pa1);
                 __syncthreads();
                 if (kt + 1 >= nkt) break;
-                if (kt + 3 < nkt) { load_a(kt + 3, ra); load_b(kt + 3, rb); }
+                load_a(kt + 3, ra, pa1);
+                load_b(kt + 3, rb);
                 step(1, 0);
                 fold_t(kt + 1);
-                if (kt + 2 < nkt) store_tiles(0, ra2, rb2);
+                if (kt + 2 < nkt) store_tiles(0, ra2, rb2, pa2);
                 __syncthreads();
             }
         } else {
@@ -823,11 +886,11 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 const int cur = kt & 1;
 #pragma unroll
                 for (int st = 0; st < NST / 2; ++st) step(cur, st);
-                if (kt + 1 < nkt) { load_a(kt + 1, ra); load_b(kt + 1, rb); }
+                if (kt + 1 < nkt) { load_a(kt + 1, ra, pa1); load_b(kt + 1, rb); }
 #pragma unroll
                 for (int st = NST / 2; st < NST; ++st) step(cur, st);
                 fold_t(kt);
-                if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb);
+                if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb, pa1);
                 __syncthreads();
             }
         }
@@ -848,7 +911,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         // MFMAs of the tile in two halves with the next tile's gather in between; the inner
         // chain t spans KT2 k-tiles (two-level summation, see mfma_ktile)
         mfma_chain<IM, JN, 0, 2>(af, bf, t);
-        if (kt + 1 < nkt) { load_a(kt + 1, ra); load_b(kt + 1, rb); }
+        if (kt + 1 < nkt) { load_a(kt + 1, ra, pa1); load_b(kt + 1, rb); }
         mfma_chain<IM, JN, 2, 4>(af, bf, t);
         if ((kt % KT2) == KT2 - 1 || kt + 1 == nkt) {
 #pragma unroll
@@ -860,7 +923,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                     for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                 }
         }
-        if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb);
+        if (kt + 1 < nkt) store_tiles(cur ^ 1, ra, rb, pa1);
         __syncthreads();
     }
 
@@ -1764,16 +1827,21 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
             pqx = rem - pqy * g.Mx;
         }
     }
-    float4 ra[2], rb[2];
-    auto load = [&](long long kt) {
+    // Two register sets: the global loads of tile kt+2 are issued while tile kt is multiplied and
+    // consumed (split + stored to LDS) only at the end of tile kt+1, two tiles of MFMA work later.
+    float4 ra0[2], rb0[2], ra1[2], rb1[2];
+    // Branch-free loads (buffer loads; out-of-range offsets read zeros) so that the wait for one
+    // register set never waits for the other; the prologue affine is applied at the store.
+    const __amdgpu_buffer_rsrc_t dyrsrc = src_rsrc(dy);
+    int pro0 = -1, pro1 = -1;  // per set: pixel-image channel offset of the prologue, -1 = none
+    auto load = [&](long long kt, float4 (&ra)[2], float4 (&rb)[2], int& pro) {
         long long p = kt * BKP + kr;
         const bool pok = p < P;
         const int co = m0 + cc;
         if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            ra[i] = (pok && co + 4 * i < d.Co) ? *reinterpret_cast<const float4*>(dy + p * d.Co + co + 4 * i)
-                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[i] = buf_load4(dyrsrc, (pok && co + 4 * i < d.Co) ? (int)((p * d.Co + co + 4 * i) * 4) : OOB_OFF);
         // sub-pixel phases: the tap offsets already include the padding
         const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
         const int vx = d.parity == 2 ? pqx + badx : pqx * d.stride - d.pl + badx;
@@ -1784,23 +1852,24 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
 #pragma unroll
         for (int i = 0; i < 2; ++i) rb[i] = buf_load4(rsrc, off + 16 * i);
-        if (d.pro_act != DCS_ACT_NONE && ok) {
-            const long long o = (long long)pn * d.Cs + bchan;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) rb[i] = affine_act4(rb[i], psc + o + 4 * i, psh + o + 4 * i, d.pro_act);
-        }
+        pro = (d.pro_act != DCS_ACT_NONE && ok) ? pn * d.Cs + bchan : -1;
         pqx += BKP;
         while (pqx >= g.Mx) {
             pqx -= g.Mx;
             if (++pqy == g.My) { pqy = 0; ++pn; }
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const float4 (&ra)[2], const float4 (&rbl)[2], int pro) {
         bf16x8 hi, mid, lo;
         split8x3(ra[0], ra[1], hi, mid, lo);
         *reinterpret_cast<bf16x8*>(X + xo(0, 0, buf, kr, cc)) = hi;
         *reinterpret_cast<bf16x8*>(X + xo(0, 1, buf, kr, cc)) = mid;
         *reinterpret_cast<bf16x8*>(X + xo(0, 2, buf, kr, cc)) = lo;
+        float4 rb[2] = {rbl[0], rbl[1]};
+        if (d.pro_act != DCS_ACT_NONE && pro >= 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) rb[i] = affine_act4(rb[i], psc + pro + 4 * i, psh + pro + 4 * i, d.pro_act);
+        }
         split8x3(rb[0], rb[1], hi, mid, lo);
         *reinterpret_cast<bf16x8*>(X + xo(1, 0, buf, kr, cc)) = hi;
         *reinterpret_cast<bf16x8*>(X + xo(1, 1, buf, kr, cc)) = mid;
@@ -1828,12 +1897,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    if (kt_beg < kt_end) {
-        load(kt_beg);
-        store(0);
-    }
-    __syncthreads();
-    for (long long kt = kt_beg; kt < kt_end; ++kt) {
+    auto tile = [&](long long kt, float4 (&nra)[2], float4 (&nrb)[2], int& npro, const float4 (&ora)[2],
+                    const float4 (&orb)[2], int opro) {
         const int cur = (int)((kt - kt_beg) & 1);
         bf16x8 ah[IM], am[IM], al[IM], bh[JN], bm[JN], bl[JN];
 #pragma unroll
@@ -1850,7 +1915,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
             bm[j] = frag(1, 1, cur, c0);
             bl[j] = frag(1, 2, cur, c0);
         }
-        if (kt + 1 < kt_end) load(kt + 1);
+        load(kt + 2, nra, nrb, npro);  // unconditional (past the range: zeros or unused), so the
+                                        // vmcnt bookkeeping stays exact across the loop
 #pragma unroll
         for (int i = 0; i < IM; ++i)
 #pragma unroll
@@ -1873,8 +1939,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
                     for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                 }
         }
-        if (kt + 1 < kt_end) store(cur ^ 1);
+        if (kt + 1 < kt_end) store(cur ^ 1, ora, orb, opro);
         __syncthreads();
+    };
+    if (kt_beg < kt_end) {
+        load(kt_beg, ra0, rb0, pro0);
+        store(0, ra0, rb0, pro0);
+        load(kt_beg + 1, ra1, rb1, pro1);
+    }
+    __syncthreads();
+    for (long long kt = kt_beg; kt < kt_end; kt += 2) {
+        tile(kt, ra0, rb0, pro0, ra1, rb1, pro1);  // tile kt+1 waits in set 1; tile kt+2 lands in set 0
+        if (kt + 1 < kt_end) tile(kt + 1, ra1, rb1, pro1, ra0, rb0, pro0);
     }
 
     float* slab = ws + ((long long)split * ncls + z) * d.Co * Ktot;
@@ -1979,7 +2055,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (d.mma == MMA_BF16X6 && vec && p.BM == 128 && d.parity != 1 && DCS_WGRAD_X6) {
+    } else if (d.mma == MMA_BF16X6 && vec && dy_small && p.BM == 128 && d.parity != 1 && DCS_WGRAD_X6) {
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs
         if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);

@@ -212,4 +212,226 @@ int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const flo
     return check_launch("narrow_wgrad_tiled");
 }
 
+// Data gradient of a KxK convolution whose OUTPUT has one channel (the Generator head,
+// modules/model.py:112: ReflectionPad(3) + Conv 7x7 64->1), onto the unpadded input:
+//   dx[n][y][x][c] = sum_{ty,tx} W[c][ty][tx] * g[n][y][x][ty][tx],
+//   g = sum over the padded positions (a, b) that pad to (y, x) of dy[n][a-ty][b-tx]
+// (zero outside dy).  The padding adjoint (reflection fold) is applied to the one-channel dy
+// before the channel expansion, so the 64-channel padded gradient is never materialised, and
+// the K*K*C MACs per pixel run on the VALU with the weights as wave-uniform scalar operands
+// (an N = 1 GEMM would waste 31/32 of every MFMA).  One thread per input pixel, all C channels.
+__device__ __forceinline__ int pad_preimages(int i, int H, int pad, int mode, int* a) {
+    int n = 0;
+    a[n++] = i + pad;
+    if (mode == DCS_PAD_REFLECT) {
+        if (i >= 1 && i <= pad) a[n++] = pad - i;
+        if (i >= H - 1 - pad && i <= H - 2) a[n++] = 2 * (H - 1) - i + pad;
+    }
+    return n;
+}
+
+template <int C, int K>
+__global__ __launch_bounds__(256) void dgrad_c1_kernel(const float* __restrict__ dy, int N, int H, int W,
+                                                       const float* __restrict__ wk, int mode,
+                                                       float* __restrict__ dx) {
+    constexpr int pad = (K - 1) / 2;
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)N * H * W) return;
+    const int n = (int)(p / ((long long)H * W));
+    const int rem = (int)(p - (long long)n * H * W);
+    const int y = rem / W, x = rem - (rem / W) * W;
+    // interior pixels (one preimage — reflection also maps rows 1..pad and H-1-pad..H-2 — and
+    // every tap inside dy) take unconditional loads
+    const bool inner = y > pad && y < H - 1 - pad && x > pad && x < W - 1 - pad;
+    int ay[3], ax[3], ny = 1, nx = 1;
+    if (!inner) {
+        ny = pad_preimages(y, H, pad, mode, ay);
+        nx = pad_preimages(x, W, pad, mode, ax);
+    }
+    const float* d = dy + (long long)n * H * W;
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+#pragma unroll 1
+    for (int ty = 0; ty < K; ++ty) {
+        float g[K];
+        if (inner) {
+            const float* b = d + (long long)(y + pad - ty) * W + x + pad;
+#pragma unroll
+            for (int tx = 0; tx < K; ++tx) g[tx] = b[-tx];
+        } else {
+#pragma unroll
+            for (int tx = 0; tx < K; ++tx) {
+                float s = 0.f;
+                for (int i = 0; i < ny; ++i) {
+                    const int r = ay[i] - ty;
+                    if ((unsigned)r >= (unsigned)H) continue;
+                    for (int j = 0; j < nx; ++j) {
+                        const int q = ax[j] - tx;
+                        if ((unsigned)q < (unsigned)W) s += d[(long long)r * W + q];
+                    }
+                }
+                g[tx] = s;
+            }
+        }
+#pragma unroll
+        for (int tx = 0; tx < K; ++tx) {
+            const float* wt = wk + (ty * K + tx) * C;  // wave-uniform: scalar loads
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[c] = fmaf(wt[c], g[tx], acc[c]);
+        }
+    }
+    float4* o = reinterpret_cast<float4*>(dx + p * C);
+#pragma unroll
+    for (int c = 0; c < C / 4; ++c) o[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+}
+
+
+// Data gradient onto ONE input channel (the image channel of the Generator stem, Conv 7x7
+// cin->64 with ReflectionPad(3); the PatchGAN's first layer, Conv 4x4 s2 1->64), in two passes
+// instead of a 64->1 transposed convolution that re-gathers every dy pixel for every output:
+//   pass 1 (per dy pixel q): z[t][q] = sum_c W[c][0][t] * dy[q][c]        (K*K dot products of C)
+//   pass 2 (per input pixel): dx[y][x] = sum over the padded positions (a, b) that pad to (y, x)
+//          and the taps t = (ty, tx) with (a - ty) and (b - tx) divisible by the stride of
+//          z[t][((a-ty)/s, (b-tx)/s)]
+// z is tap-planar ([K*K][Q]) so that both passes touch it with unit stride across the lanes.
+// Pass 1 stages 64 dy pixels x 32 channels at a time through LDS (coalesced 128-B row segments
+// in, one pixel row per lane out).
+template <int T, int C>
+__global__ __launch_bounds__(64) void to1_zproj_kernel(const float* __restrict__ dy, long long Q,
+                                                       const float* __restrict__ wk, float* __restrict__ z) {
+    constexpr int HC = 32, PITCH = HC + 4, SEG = HC / 4;  // channels per stage, LDS row pitch (floats)
+    static_assert(C == 2 * HC, "two staging rounds");
+    __shared__ __attribute__((aligned(16))) float sm[64 * PITCH];
+    const long long q0 = (long long)blockIdx.x * 64;
+    const int lane = threadIdx.x;
+    float4 row[C / 4];  // this lane's dy pixel, all channels
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int k = 0; k < SEG; ++k) {
+            const int idx = k * 64 + lane, pix = idx / SEG, c4 = idx - (idx / SEG) * SEG;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q0 + pix < Q) v = *reinterpret_cast<const float4*>(dy + (q0 + pix) * C + h * HC + 4 * c4);
+            *reinterpret_cast<float4*>(sm + pix * PITCH + 4 * c4) = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c4 = 0; c4 < SEG; ++c4) row[h * SEG + c4] = *reinterpret_cast<const float4*>(sm + lane * PITCH + 4 * c4);
+        __syncthreads();
+    }
+    const long long q = q0 + lane;
+    const bool live = q < Q;
+    // tap-outer: one tap's C weights (wave-uniform scalar loads) against the register row
+#pragma unroll 7
+    for (int t = 0; t < T; ++t) {
+        const float* w = wk + t * C;
+        float a0 = 0.f, a1 = 0.f;  // two chains
+#pragma unroll
+        for (int c4 = 0; c4 < C / 4; c4 += 2) {
+            a0 = fmaf(w[4 * c4 + 0], row[c4].x, fmaf(w[4 * c4 + 1], row[c4].y,
+                 fmaf(w[4 * c4 + 2], row[c4].z, fmaf(w[4 * c4 + 3], row[c4].w, a0))));
+            a1 = fmaf(w[4 * c4 + 4], row[c4 + 1].x, fmaf(w[4 * c4 + 5], row[c4 + 1].y,
+                 fmaf(w[4 * c4 + 6], row[c4 + 1].z, fmaf(w[4 * c4 + 7], row[c4 + 1].w, a1))));
+        }
+        if (live) z[t * Q + q] = a0 + a1;
+    }
+}
+
+// taps of one axis that reach padded position a: all K (stride 1), or the K/2 of a's parity
+// (stride 2, K even)
+template <int K, int S>
+__global__ __launch_bounds__(256) void to1_gather_kernel(const float* __restrict__ z, int N, int Hy, int Wy, int pt,
+                                                         int pl, int mode, int H, int W, float* __restrict__ dx) {
+    static_assert(S == 1 || (S == 2 && K % 2 == 0), "stride-2 taps come in parity pairs");
+    constexpr int KS = K / S;
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)N * H * W) return;
+    const int n = (int)(p / ((long long)H * W));
+    const int rem = (int)(p - (long long)n * H * W);
+    const int y = rem / W, x = rem - (rem / W) * W;
+    int ay[3], ax[3];
+    const int ny = pad_preimages(y, H, pt, mode, ay), nx = pad_preimages(x, W, pl, mode, ax);
+    const long long Q = (long long)N * Hy * Wy;
+    const float* zn = z + (long long)n * Hy * Wy;
+    float s = 0.f;
+    for (int i = 0; i < ny; ++i) {
+        const int a = ay[i];
+#pragma unroll
+        for (int my = 0; my < KS; ++my) {
+            const int ty = S == 2 ? (a & 1) + 2 * my : my;
+            const int u = a - ty;
+            if (u < 0) continue;
+            const int oy = S == 2 ? (u >> 1) : u;
+            if (oy >= Hy) continue;
+            for (int j = 0; j < nx; ++j) {
+                const int b = ax[j];
+#pragma unroll
+                for (int mx = 0; mx < KS; ++mx) {
+                    const int tx = S == 2 ? (b & 1) + 2 * mx : mx;
+                    const int v = b - tx;
+                    const int ox = S == 2 ? (v >> 1) : v;
+                    if (v >= 0 && ox < Wy) s += zn[(ty * K + tx) * Q + (long long)oy * Wy + ox];
+                }
+            }
+        }
+    }
+    dx[p] = s;
+}
+
 }  // namespace dcs
+
+using namespace dcs;
+
+extern "C" size_t dcs_conv_dgrad_to1_workspace_size(int N, int Hy, int Wy, int K) {
+    return (size_t)N * Hy * Wy * K * K * sizeof(float);
+}
+
+// dy: NHWC [N][Hy][Wy][C] (C = 64); wk[(ty*K + tx)*C + c] = W[c][0][ty][tx] (dcs_pack_weights kind 2,
+// nmajor 0, ncols 1, ci_count 1); dx: [N][H][W], the unpadded input of the forward conv (stride s,
+// padding pt/pl of pad_mode, Hy = (H + 2*pt - K)/s + 1).
+extern "C" int dcs_conv_dgrad_to1(const float* dy, int N, int Hy, int Wy, int C, const float* wk, int K, int stride,
+                                  int pt, int pl, int pad_mode, int H, int W, float* dx, void* ws, size_t ws_bytes,
+                                  void* stream) {
+    if (!dy || !wk || !dx || !ws || N <= 0 || Hy <= 0 || Wy <= 0 || H <= 0 || W <= 0 || (stride != 1 && stride != 2) ||
+        pt < 0 || pl < 0 || (pad_mode != DCS_PAD_ZERO && pad_mode != DCS_PAD_REFLECT) ||
+        (pad_mode == DCS_PAD_REFLECT && (pt >= H || pl >= W)) || (reinterpret_cast<uintptr_t>(dy) & 15))
+        return fail(DCS_E_INVALID, "conv_dgrad_to1: bad arguments");
+    if (C != 64 || !((K == 7 && stride == 1) || (K == 4 && stride == 2)))
+        return fail(DCS_E_INVALID, "conv_dgrad_to1: C == 64 and (K, stride) = (7, 1) or (4, 2)");
+    if (ws_bytes < dcs_conv_dgrad_to1_workspace_size(N, Hy, Wy, K))
+        return fail(DCS_E_WORKSPACE, "conv_dgrad_to1: workspace too small");
+    hipStream_t s = as_stream(stream);
+    float* z = reinterpret_cast<float*>(ws);
+    const long long Q = (long long)N * Hy * Wy;
+    if (K == 7) hipLaunchKernelGGL((to1_zproj_kernel<49, 64>), dim3((unsigned)cdiv(Q, 64)), dim3(64), 0, s, dy, Q, wk, z);
+    else hipLaunchKernelGGL((to1_zproj_kernel<16, 64>), dim3((unsigned)cdiv(Q, 64)), dim3(64), 0, s, dy, Q, wk, z);
+    int e = check_launch("conv_dgrad_to1_zproj");
+    if (e) return e;
+    const dim3 grid((unsigned)cdiv((long long)N * H * W, 256));
+    if (K == 7) hipLaunchKernelGGL((to1_gather_kernel<7, 1>), grid, dim3(256), 0, s, z, N, Hy, Wy, pt, pl, pad_mode, H, W, dx);
+    else hipLaunchKernelGGL((to1_gather_kernel<4, 2>), grid, dim3(256), 0, s, z, N, Hy, Wy, pt, pl, pad_mode, H, W, dx);
+    return check_launch("conv_dgrad_to1_gather");
+}
+
+// wk: the forward conv's K-major packed weights ([K*K][C] x 1 column: dcs_pack_weights kind 0,
+// nmajor 0, ncols 1), i.e. wk[(ty*K + tx)*C + c] = W[0][c][ty][tx].
+extern "C" int dcs_conv_dgrad_c1(const float* dy, int N, int H, int W, const float* wk, int C, int K, int pad,
+                                 int pad_mode, float* dx, void* stream) {
+    if (!dy || !wk || !dx || N <= 0 || H <= 0 || W <= 0 || K <= 0 || K > 9 || pad < 0 || pad >= K ||
+        (pad_mode != DCS_PAD_ZERO && pad_mode != DCS_PAD_REFLECT) || (pad_mode == DCS_PAD_REFLECT && (pad >= H || pad >= W)) ||
+        (reinterpret_cast<uintptr_t>(dx) & 15))
+        return fail(DCS_E_INVALID, "conv_dgrad_c1: bad arguments");
+    if (2 * pad != K - 1) return fail(DCS_E_INVALID, "conv_dgrad_c1: 'same' convolutions only (2*pad == K-1)");
+    const long long total = (long long)N * H * W;
+    const dim3 grid((unsigned)cdiv(total, 256));
+    hipStream_t s = as_stream(stream);
+#define DCS_C1(CC, KK) hipLaunchKernelGGL((dgrad_c1_kernel<CC, KK>), grid, dim3(256), 0, s, dy, N, H, W, wk, pad_mode, dx)
+    if (C == 64 && K == 7) DCS_C1(64, 7);
+    else if (C == 64 && K == 3) DCS_C1(64, 3);
+    else if (C == 32 && K == 7) DCS_C1(32, 7);
+    else if (C == 32 && K == 3) DCS_C1(32, 3);
+    else return fail(DCS_E_INVALID, "conv_dgrad_c1: C must be 32 or 64 and K 3 or 7");
+#undef DCS_C1
+    return check_launch("conv_dgrad_c1");
+}

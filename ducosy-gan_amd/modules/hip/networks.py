@@ -159,8 +159,9 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     return out, saved
 
 
-def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int):
-    """Returns (dx NHWC [N,H,W,dx_channels] or None, grads dict keyed like gen_param_names)."""
+def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, dx_from: int = 0):
+    """Returns (dx NHWC [N,H,W,dx_channels] or None, grads dict keyed like gen_param_names).
+    dx is computed for samples dx_from.. only (zero before)."""
     L, W = S["L"], S["W"]
     nb, use_cbam = S["nb"], S["use_cbam"]
     grads: Dict[str, torch.Tensor] = {}
@@ -200,7 +201,13 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int):
     dx = None
     if need_dx:
         stem = L["stem"]
-        dx = stem.dgrad(dy, stem.pack_dgrad(W["stem.w"], dx_channels), H, Wd, ci_count=dx_channels)
+        wd = stem.pack_dgrad(W["stem.w"], dx_channels)
+        if dx_from > 0:
+            dx = torch.zeros(N, H, Wd, dx_channels, device=dy.device, dtype=torch.float32)
+            if dx_from < N:
+                dx[dx_from:] = stem.dgrad(dy[dx_from:], wd, H, Wd, ci_count=dx_channels)
+        else:
+            dx = stem.dgrad(dy, wd, H, Wd, ci_count=dx_channels)
     # biases feeding an InstanceNorm: exact zero gradient
     for key in ("stem.b", "down1.b", "down2.b", "up1.b", "up2.b"):
         grads[key] = torch.zeros_like(W[key])
@@ -215,7 +222,8 @@ class GeneratorFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x2, cfg, *params):
-        keys, nb, use_cbam = cfg
+        keys, nb, use_cbam = cfg[:3]
+        ctx.dx_from = cfg[3] if len(cfg) > 3 else 0
         W = dict(zip(keys, params))
         keep = any(ctx.needs_input_grad)
         out, saved = generator_forward(W, x, x2, nb, use_cbam, keep)
@@ -231,7 +239,7 @@ class GeneratorFunction(torch.autograd.Function):
         S = ctx.saved
         S["out"] = ctx.saved_tensors[0]
         need_dx = ctx.needs_input_grad[0]
-        dx_nhwc, grads = generator_backward(S, dout, need_dx, ctx.x_channels)
+        dx_nhwc, grads = generator_backward(S, dout, need_dx, ctx.x_channels, ctx.dx_from)
         ctx.saved = None
         dx = None
         if need_dx:

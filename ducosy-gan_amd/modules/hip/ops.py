@@ -241,8 +241,28 @@ class ConvGeom:
         K = self.k * self.k * self.cin
         return self._pack(w, 0, self.cin, K, self.cout)
 
+    @property
+    def c1_dgrad(self) -> bool:
+        """One output channel, 'same' stride-1 padding (the Generator head): the data gradient runs
+        on the VALU with the padding adjoint folded into the one-channel dy (dcs_conv_dgrad_c1)."""
+        t, l, b, r = self.pads
+        return (self.cout == 1 and self.cin in (32, 64) and self.k in (3, 7) and self.stride == 1 and self.up == 1
+                and t == l == b == r and 2 * t == self.k - 1)
+
+    def to1_dgrad(self, ci: int) -> bool:
+        """Data gradient onto one input channel from 64 output channels (the image channel of the
+        Generator stem, 7x7 reflect; the PatchGAN's first layer, 4x4 stride 2): two VALU passes,
+        per-dy-pixel tap projections then a gather (dcs_conv_dgrad_to1)."""
+        t, l, b, r = self.pads
+        return (ci == 1 and self.cout == 64 and self.up == 1 and (self.k, self.stride) in ((7, 1), (4, 2))
+                and (self.pad_mode == DCS_PAD_ZERO or (t == b and l == r)))
+
     def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
         ci = self.cin if ci_count is None else ci_count
+        if self.c1_dgrad and ci == self.cin:  # forward K-major weights: [(ty*K+tx)*cin + c]
+            return self._pack(w, 0, self.cin, self.k * self.k * self.cin, 1)
+        if self.to1_dgrad(ci):  # un-flipped taps, K-major: [(ty*K+tx)*cout + co] = w[co][0][ty][tx]
+            return self._pack(w, 2, 1, self.k * self.k * self.cout, 1)
         if self.subpixel and ci > 4:
             return self._pack(w, 4, ci, 16 * self.cout, ci)
         kind = 2 if self.stride == 2 else 1
@@ -318,6 +338,23 @@ class ConvGeom:
         N, Ho, Wo, Co = dy.shape
         assert Co == self.cout
         ci = self.cin if ci_count is None else ci_count
+        if self.c1_dgrad and ci == self.cin:
+            out = torch.empty(N, H, W, ci, device=dy.device, dtype=torch.float32)
+            lib.call("dcs_conv_dgrad_c1", _p(dy.contiguous()), N, H, W, _p(wpack_d), ci, self.k, self.pads[0],
+                     self.pad_mode, _p(out), _stream())
+            if addend is not None:
+                lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
+            return out
+        if self.to1_dgrad(ci):
+            out = torch.empty(N, H, W, 1, device=dy.device, dtype=torch.float32)
+            dyc = dy.contiguous()
+            ws = torch.empty(lib.query("dcs_conv_dgrad_to1_workspace_size", N, Ho, Wo, self.k) // 4,
+                             device=dy.device, dtype=torch.float32)
+            lib.call("dcs_conv_dgrad_to1", _p(dyc), N, Ho, Wo, Co, _p(wpack_d), self.k, self.stride,
+                     self.pads[0], self.pads[1], self.pad_mode, H, W, _p(out), _p(ws), ws.numel() * 4, _stream())
+            if addend is not None:
+                lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
+            return out
         narrow = ci <= 4
         fn = "dcs_conv_rows_narrow" if narrow else "dcs_conv_rows"
         d = lib.ConvDesc()

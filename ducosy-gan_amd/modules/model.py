@@ -128,12 +128,15 @@ class Generator(nn.Module):
         inv = {v: k for k, v in _net.gen_param_names(num_residual_blocks, use_cbam).items()}
         self._keys = tuple(inv[name] for name, _ in self.named_parameters())
 
-    def forward(self, x, masks=None):
+    def forward(self, x, masks=None, input_grad_from=0):
         """x: [N, input_channels, H, W] (the reference's concat input) — or the image channels
-        with ``masks`` given separately, in which case the concat is fused into the stem."""
+        with ``masks`` given separately, in which case the concat is fused into the stem.
+        ``input_grad_from``: the samples before this index are data whose input gradient nobody
+        reads (a batch concatenated from real images and one generated tensor); the input
+        gradient is computed for x[input_grad_from:] only and is zero before it."""
         params = [p for _, p in self.named_parameters()]
-        return _net.GeneratorFunction.apply(x, masks, (self._keys, self.num_residual_blocks, self.use_cbam),
-                                            *params)
+        cfg = (self._keys, self.num_residual_blocks, self.use_cbam, int(input_grad_from))
+        return _net.GeneratorFunction.apply(x, masks, cfg, *params)
 
 
 class Discriminator(nn.Module):

@@ -110,7 +110,8 @@ class CycleGANSystem:
         self.optimizer_G.zero_grad()
         ab = G_AB(torch.cat([real_A, real_B]), mk(2))              # [fake_B ; id_B]
         fake_B, id_B = ab[:N], ab[N:]
-        ba = G_BA(torch.cat([real_B, real_A, fake_B]), mk(3))      # [fake_A ; id_A ; rec_A]
+        ba = G_BA(torch.cat([real_B, real_A, fake_B]), mk(3),      # [fake_A ; id_A ; rec_A]
+                  input_grad_from=2 * N)                          # only fake_B needs dL/dx
         fake_A, id_A, rec_A = ba[:N], ba[N:2 * N], ba[2 * N:]
         loss_id = (self.criterion_identity(id_A, real_A) + self.criterion_identity(id_B, real_B)) / 2
         loss_GAN = (self.criterion_GAN(D_B(fake_B, params_require_grad=False), 1.0)

@@ -142,6 +142,29 @@ int dcs_conv_wgrad(const dcs_conv_desc* d, const float* dy, const float* x, cons
                    const float* pro_scale, const float* pro_shift, float* dw, void* ws,
                    size_t ws_bytes, void* stream);
 
+/* Data gradient of a 'same' K x K stride-1 convolution with ONE output channel (the Generator
+ * head, modules/model.py:112: ReflectionPad(3) + Conv 7x7 64->1; aten convolution_backward
+ * grad_input + reflection_pad2d_backward) onto its unpadded NHWC input:
+ *   dx[n][y][x][c] = sum_{ty,tx} W[0][c][ty][tx] * sum_{(a,b) padding to (y,x)} dy[n][a-ty][b-tx]
+ * dy: [N][H][W] (one channel); wk: the forward K-major pack ([(ty*K+tx)*C + c], dcs_pack_weights
+ * kind 0, nmajor 0, ncols 1); dx: NHWC [N][H][W][C], C = 32 or 64; K = 3 or 7; 2*pad == K-1. */
+int dcs_conv_dgrad_c1(const float* dy, int N, int H, int W, const float* wk, int C, int K, int pad, int pad_mode,
+                      float* dx, void* stream);
+
+/* Data gradient onto ONE input channel from C = 64 output channels: the image channel of the
+ * Generator stem (modules/model.py:96-97, ReflectionPad(3) + Conv 7x7, stride 1) and the
+ * PatchGAN's first layer (modules/model.py:121, Conv 4x4 stride 2 padding 1); aten
+ * convolution_backward grad_input (+ reflection_pad2d_backward for the stem).  Two passes:
+ *   z[q][t] = sum_c W[c][0][t] * dy[q][c]                                  (per dy pixel q)
+ *   dx[n][y][x] = sum over padded positions (a,b) of (y,x) and taps t with (a-ty), (b-tx)
+ *                 divisible by `stride` of z[n][(a-ty)/stride][(b-tx)/stride][t]
+ * dy: NHWC [N][Hy][Wy][C]; wk[(ty*K+tx)*C + c] = W[c][0][ty][tx] (dcs_pack_weights kind 2, nmajor 0,
+ * ncols 1, ci_count 1); (K, stride) = (7, 1) or (4, 2); pt/pl: top/left padding of pad_mode (reflect:
+ * symmetric); dx: [N][H][W]; ws: dcs_conv_dgrad_to1_workspace_size(N, Hy, Wy, K) bytes. */
+size_t dcs_conv_dgrad_to1_workspace_size(int N, int Hy, int Wy, int K);
+int dcs_conv_dgrad_to1(const float* dy, int N, int Hy, int Wy, int C, const float* wk, int K, int stride, int pt,
+                       int pl, int pad_mode, int H, int W, float* dx, void* ws, size_t ws_bytes, void* stream);
+
 /* Pack up to 4 NCHW planes (x: [N][c1][H][W], x2: [N][c2][H][W] or NULL) into one NHWC
  * [N][H][W][4] tensor with zero channels after c1+c2 (c1 + c2 <= 4): the 4-channel layout the
  * vectorised stem convolution gathers (modules/model.py:94 input, trainer.py:451 concat). */

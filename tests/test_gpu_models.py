@@ -88,6 +88,28 @@ def test_generator_split_masks_matches_concat():
     assert rel2(img.grad, z["dx"][:, :1]) < GTOL
 
 
+def test_generator_input_grad_from():
+    """input_grad_from=k: the input gradient of samples k.. is the full one (same kernels over the
+    same per-sample data), zero before k; parameter gradients unchanged."""
+    from modules.model import Generator
+    z = np.load(os.path.join(GOLDEN, "gen_cin3_nb1_32.npz"))
+    G = Generator(3, 1).to(DEV)
+    G.load_state_dict(_sd(orc.generator_param_shapes(3, 1, True), 101))
+    x = torch.from_numpy(z["x"]).to(DEV)
+    img, masks = x[:, :1].contiguous(), x[:, 1:].contiguous()
+    R = torch.from_numpy(z["R"]).to(DEV)
+    out = {}
+    for k in (0, 1):
+        G.zero_grad()
+        xi = img.clone().requires_grad_(True)
+        (G(xi, masks, input_grad_from=k) * R).sum().backward()
+        out[k] = (xi.grad.clone(), [p.grad.clone() for p in G.parameters()])
+    assert x.shape[0] == 2
+    assert float(out[1][0][0].abs().max()) == 0.0
+    assert rel(out[1][0][1], out[0][0][1]) < 1e-6
+    assert all(rel(a, b) < 1e-6 for a, b in zip(out[0][1], out[1][1]) if float(b.abs().max()) > 0)
+
+
 def test_resblock_golden():
     from modules.model import ResidualBlockWithCBAM
     z = np.load(os.path.join(GOLDEN, "resblock_cbam_16.npz"))

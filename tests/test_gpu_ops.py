@@ -54,6 +54,7 @@ CONV_CASES = [
     (256, 128, 3, 1, (1, 1, 1, 1), "zero", 2, 5),       # up1
     (128, 64, 3, 1, (1, 1, 1, 1), "zero", 2, 6),        # up2
     (64, 1, 7, 1, (3, 3, 3, 3), "reflect", 1, 12),      # head (narrow)
+    (32, 1, 3, 1, (1, 1, 1, 1), "zero", 1, 10),         # 'same' 3x3 onto one channel (dcs_conv_dgrad_c1)
     (1, 64, 4, 2, (1, 1, 1, 1), "zero", 1, 32),         # D layer 0 (cin 1)
     (64, 128, 4, 2, (1, 1, 1, 1), "zero", 1, 16),       # D layer 1
     (256, 512, 4, 2, (1, 1, 1, 1), "zero", 1, 8),       # D layer 3
@@ -265,25 +266,35 @@ def test_reflect_dgrad_direct_and_accumulate(ops, H):
                                                       (1, 0, 4, 2, (1, 1, 1, 1), "zero")])
 def test_four_channel_stem_path(ops, c1, c2, k, stride, pads, mode):
     """Image (+ mask planes) packed NHWC x 4 (dcs_pack_nhwc4) and the float4-per-tap gather
-    (stem 7x7 and PatchGAN layer 0): forward and weight gradient vs torch on the concat."""
+    (stem 7x7 and PatchGAN layer 0): forward and weight gradient vs torch on the concat, and the
+    data gradient onto the image channel (dcs_conv_dgrad_to1; odd width)."""
     from modules.hip.ops import ConvGeom, Src
     from modules.hip.lib import DCS_PAD_REFLECT, DCS_PAD_ZERO
-    cin, H = c1 + c2, 36
+    cin, H, W = c1 + c2, 36, 37
     g = ConvGeom(cin, 64, k, stride, pads, DCS_PAD_REFLECT if mode == "reflect" else DCS_PAD_ZERO)
-    x = rnd((2, c1, H, H), 41, "x")
-    m = rnd((2, c2, H, H), 41, "m") if c2 else None
+    x = rnd((2, c1, H, W), 41, "x").requires_grad_(True)
+    m = rnd((2, c2, H, W), 41, "m") if c2 else None
     w = rnd((64, cin, k, k), 41, "w", -0.1, 0.1).requires_grad_(True)
     xc = torch.cat([x, m], 1) if c2 else x
     y_ref = torch_conv(xc, w, g)
     dy = rnd(tuple(y_ref.shape), 41, "dy")
     y_ref.backward(dy)
-    x4 = ops.pack_nhwc4(x.cuda(), m.cuda() if c2 else None)
-    assert x4.shape == (2, H, H, 4)
-    assert torch.equal(x4[..., :cin].cpu(), xc.permute(0, 2, 3, 1))
+    xd = x.detach().cuda()
+    x4 = ops.pack_nhwc4(xd, m.cuda() if c2 else None)
+    assert x4.shape == (2, H, W, 4)
+    assert torch.equal(x4[..., :cin].cpu(), xc.detach().permute(0, 2, 3, 1))
     assert float(x4[..., cin:].abs().max()) == 0.0 if cin < 4 else True
     s4 = Src.nhwc(x4)
     y = g.forward(s4, g.pack_fwd(w.detach().cuda(), cin_pad=4))
     assert rel(y.permute(0, 3, 1, 2), y_ref) < 1e-4
-    dw = g.wgrad(dy.permute(0, 2, 3, 1).contiguous().cuda(), s4)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().cuda()
+    dw = g.wgrad(dyn, s4)
     assert dw.shape == w.shape
     assert rel(dw, w.grad) < 1e-4
+    assert g.to1_dgrad(1)
+    dx = g.dgrad(dyn, g.pack_dgrad(w.detach().cuda(), 1), H, W, ci_count=1)
+    assert dx.shape == (2, H, W, 1)
+    assert rel(dx.permute(0, 3, 1, 2), x.grad) < 1e-5
+    add = rnd((2, H, W, 1), 42, "add").cuda()
+    got = g.dgrad(dyn, g.pack_dgrad(w.detach().cuda(), 1), H, W, ci_count=1, addend=add)
+    assert rel(got, dx + add) < 1e-6
