@@ -121,6 +121,9 @@ def main():
     from modules.hip import ops
     from modules.trainer import CycleGANSystem
 
+    if args.dual and args.dual_schedule == "concurrent" and args.mma != "f32":
+        raise SystemExit("--dual-schedule concurrent runs the f32 operand mode (pass --mma f32): "
+                         "DESIGN.md §3, Config 5")
     ops.set_mma(args.mma)
     rank, world, local = parallel.init_from_env()
     device = torch.device(f"cuda:{local}")

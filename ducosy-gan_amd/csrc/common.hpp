@@ -91,4 +91,13 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
+// Per-chunk InstanceNorm statistics of one (image, channel): count, mean, sum of squared
+// deviations, and the maximum with its first pixel index.  Written by the statistics pass
+// (norm.hip) or by the conv rows epilogue (conv.hip), merged by in_stats_finalize8_kernel.
+struct Part {
+    float cnt, mean, m2, mx;
+    int amax;
+    int pad[3];
+};
+
 }  // namespace dcs

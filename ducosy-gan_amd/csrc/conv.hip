@@ -93,6 +93,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_BN64
 #define DCS_X6_BN64 1  // bf16x6 rows also for 64-column tiles
 #endif
+#ifndef DCS_ROWS_F32
+#define DCS_ROWS_F32 0  // A/B only: the rows pass ignores the bf16 operand modes (exact f32)
+#endif
 #ifndef DCS_X6_PIPE
 #define DCS_X6_PIPE 1  // bf16x6 rows: global loads two k-tiles ahead (two register sets)
 #endif
@@ -468,6 +471,89 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
     return d;
 }
 
+// InstanceNorm statistics of a rows tile, fused into the epilogue (dcs_conv_rows_in_stats): the
+// tile's BM rows lie in one image (the host requires rows-per-image % BM == 0), so each of its
+// columns contributes one Part (mean / M2 / max over BM pixels): chunk (z, tile) of image n, where
+// z is the sub-pixel phase of a parity-2 forward (one class otherwise).  A lane holds
+// 32 rows of one column per 32-column block (IM blocks of 16): two-pass mean / M2 in registers,
+// the partner lane (lane ^ 32) merged by shuffle, the BM/64 waves along M through LDS, all in a
+// fixed order (deterministic).  The value is the stored one (bias and epilogue activation).
+template <int BM, int BN, int IM, int JN>
+__device__ __forceinline__ void rows_in_stats(const dcs_conv_desc& d, const floatx16 (&acc)[IM][JN],
+                                              const float* __restrict__ bias, int n0, long long m0, const ClassGeom& g,
+                                              int z, int wm, int wn, int lane, int tid, float* lds,
+                                              Part* __restrict__ parts) {
+    constexpr int WN = BN / 2, WMN = BM / 64;
+    static_assert(IM == 2, "64-row waves");
+    Part* sp = reinterpret_cast<Part*>(lds);  // [WMN][BN]; the k-loop's last barrier freed the LDS
+    const int hi = lane >> 5;
+    const long long per = (long long)g.My * g.Mx;  // rows of one image (of one phase)
+    const int base = (int)(m0 % per);              // the tile's first row within its image
+    const int ncls = d.parity == 2 ? 4 : 1;
+    auto pixel = [&](int row) {  // output pixel index within the image
+        if (d.parity != 2) return base + row;
+        const int q = base + row, qy = q / g.Mx, qx = q - (q / g.Mx) * g.Mx;
+        return (2 * qy + g.ry) * d.Wo + 2 * qx + g.rx;
+    };
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int colL = wn * WN + j * 32 + (lane & 31), col = n0 + colL;
+        const float bv = (bias && col < d.Co) ? bias[col] : 0.f;
+        auto val = [&](int i, int r) {
+            float v = acc[i][j][r] + bv;
+            if (d.epi_act != DCS_ACT_NONE) v = act_apply(v, d.epi_act);
+            return v;
+        };
+        float s = 0.f, mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {  // rows increase with (i, r): strict > keeps the first maximum
+                const float v = val(i, r);
+                s += v;
+                if (v > mx) { mx = v; am = pixel(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi); }
+            }
+        float mean = s * (1.f / 32.f), m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float dv = val(i, r) - mean;
+                m2 = fmaf(dv, dv, m2);
+            }
+        const float mb = __shfl_xor(mean, 32, 64), m2b = __shfl_xor(m2, 32, 64), mxb = __shfl_xor(mx, 32, 64);
+        const int amb = __shfl_xor(am, 32, 64);
+        if (hi == 0) {  // left operand: this lane; equal counts (32 + 32)
+            const float dl = mb - mean;
+            Part p;
+            p.cnt = 64.f;
+            p.mean = mean + 0.5f * dl;
+            p.m2 = m2 + m2b + dl * dl * 16.f;
+            p.mx = mx;
+            p.amax = am;
+            if (mxb > mx || (mxb == mx && amb < am)) { p.mx = mxb; p.amax = amb; }
+            p.pad[0] = p.pad[1] = p.pad[2] = 0;
+            sp[wm * BN + colL] = p;
+        }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < d.Co) {
+        Part a = sp[tid];
+#pragma unroll
+        for (int w = 1; w < WMN; ++w) {
+            const Part b = sp[w * BN + tid];
+            const float tot = a.cnt + b.cnt, dl = b.mean - a.mean;
+            a.mean += dl * (b.cnt / tot);
+            a.m2 += b.m2 + dl * dl * (a.cnt * b.cnt / tot);
+            a.cnt = tot;
+            if (b.mx > a.mx || (b.mx == a.mx && b.amax < a.amax)) { a.mx = b.mx; a.amax = b.amax; }
+        }
+        const long long tiles = per / BM, n = m0 / per;
+        parts[((n * ncls + z) * tiles + base / BM) * d.Co + n0 + tid] = a;
+    }
+}
+
 // VEC: 0 scalar gather (any layout), 1 = 16 consecutive k of one tap per thread (Cs % 16 == 0),
 //      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
 // BM = 256 (bf16x6, 128 columns): 512 threads as 4 x 2 waves of 64 x 64, one workgroup per CU;
@@ -476,7 +562,7 @@ template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
 __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
-    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy) {
+    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts) {
     const dcs_conv_desc d = specialise<TAG>(din);
     static_assert(BM == 128 || (BM == 256 && MMA == MMA_BF16X6 && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
@@ -645,7 +731,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             //  slower here: invalid taps would issue loads that the branch now skips)
 #pragma unroll
             for (int i = 0; i < ACH; ++i) dst[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (rvalid && aj < g.ntaps) {
+            if (rvalid && aj < g.ntaps && ac < d.Cs) {
                 int ady, adx, bt;
                 tap_decode(d, g, aj, ady, adx, bt);
                 int sy, sx;
@@ -693,14 +779,15 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             col = (long long)bt * d.Cs + bc;
             advance(bj, bc);
         }
-        if constexpr (MMA == MMA_BF16X6) {  // branch-free: k-tiles past the end read zeros
+        if constexpr (MMA == MMA_BF16X6 && DCS_BF16_BUFGATHER) {  // branch-free: k-tiles past the end read zeros
             const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
 #pragma unroll
             for (int i = 0; i < BCH; ++i) dst[i] = buf_load4(brsrc, off + 16 * i);
         } else {
 #pragma unroll
             for (int i = 0; i < BCH; ++i)
-                dst[i] = ok ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+                dst[i] = (ok && col < d.ldb) ? *reinterpret_cast<const float4*>(bsrc + col + 4 * i)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto store_tiles = [&](int buf, const auto& sa0, const auto& sb, int pa) {
@@ -946,6 +1033,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             }
         }
     }
+    if (parts) rows_in_stats<BM, BN, IM, JN>(d, acc, bias, n0, m0, g, z, wm, wn, lane, tid, lds, parts);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1663,8 +1751,9 @@ extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int K
     return check_launch("pack_weights");
 }
 
-extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack,
-                             const float* bias, const float* psc, const float* psh, float* out, void* stream) {
+namespace {
+int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
+                   const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream) {
     int e = validate(dp, true);
     if (e) return e;
     const dcs_conv_desc& d = *dp;
@@ -1684,6 +1773,7 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
     }
     const int gx = (int)cdiv(Mmax, 128), gy = (int)cdiv(d.Co, BN);
     dim3 grid((unsigned)(gx * gy * ncls));
+    if (bm_used) *bm_used = 128;
     const bool vec = vec_ok(dp, src);
     const bool v4 = !vec && vec4_ok(dp, src) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool res_geom = d.Cs == 256 && d.Co == 256 && d.KH == 3 && d.KW == 3 && !d.parity && d.up == 1 &&
@@ -1696,40 +1786,77 @@ extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const fl
                                    "residual geometry with a vectorisable source");
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
-    if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64)) {  // x6: 128- or 64-column tiles
+    if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64) && !DCS_ROWS_F32) {  // x6: 128- or 64-column tiles
         // 256-row tiles where they divide the pixels evenly (the forward over whole 128 x 128
         // images); the 130 x 130 padded data gradient keeps 128-row tiles (measured: its partial
         // last dispatch round and zero-padded border rows make the big tile 7 % slower there)
-        if (BN == 128 && res && DCS_X6_BM256 && Mmax % 256 == 0) {
+        if (BN == 128 && res && DCS_X6_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
             const int gx2 = (int)cdiv(Mmax, 256);
             hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16X6>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
-                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy);
-        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts);
+            if (bm_used) *bm_used = 256;
+        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
         return check_launch("conv_rows");
     }
-    const bool mma_ok = vec && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
+    const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \
-    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy); \
-    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);  \
-    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts); \
+    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);  \
+    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
         if (d.mma == MMA_BF16) { DCS_ROWS_MMA(MMA_BF16) } else { DCS_ROWS_MMA(MMA_BF16X3) }
 #undef DCS_ROWS_MMA
         return check_launch("conv_rows");
     }
     if (BN == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
     }
     return check_launch("conv_rows");
+}
+}  // namespace
+
+extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack,
+                             const float* bias, const float* psc, const float* psh, float* out, void* stream) {
+    return conv_rows_impl(dp, src, src2, wpack, bias, psc, psh, out, nullptr, nullptr, stream);
+}
+
+namespace {
+// parity 0 rows, or the sub-pixel forward's four phases (each phase's rows per image % 128)
+bool rows_stats_ok(const dcs_conv_desc& d) {
+    if (d.parity == 1 || d.Co <= 4 || d.Co % 4 != 0) return false;
+    const ClassGeom g = class_geom(d, 0);
+    return ((long long)g.My * g.Mx) % 128 == 0;
+}
+}  // namespace
+
+extern "C" size_t dcs_conv_rows_in_stats_parts_size(const dcs_conv_desc* dp) {
+    if (!dp || !rows_stats_ok(*dp)) return 0;
+    return (size_t)dp->N * ((size_t)dp->Ho * dp->Wo / 128) * dp->Co * sizeof(Part);  // phases: 4 x (Ho*Wo/4)
+}
+
+extern "C" int dcs_conv_rows_in_stats(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack,
+                                      const float* bias, const float* psc, const float* psh, float* out, void* parts,
+                                      size_t parts_bytes, int* nchunk, void* stream) {
+    if (!dp || !parts || !nchunk) return fail(DCS_E_INVALID, "conv_rows_in_stats: null pointer");
+    if (!rows_stats_ok(*dp))
+        return fail(DCS_E_INVALID, "conv_rows_in_stats: needs parity 0 / 2 rows, Co > 4 and rows per image % 128 == 0");
+    if (parts_bytes < dcs_conv_rows_in_stats_parts_size(dp))
+        return fail(DCS_E_WORKSPACE, "conv_rows_in_stats: parts buffer too small");
+    int bm = 128;
+    const int e = conv_rows_impl(dp, src, src2, wpack, bias, psc, psh, out, reinterpret_cast<Part*>(parts), &bm, stream);
+    if (e) return e;
+    const ClassGeom g = class_geom(*dp, 0);
+    *nchunk = (int)((dp->parity == 2 ? 4 : 1) * (long long)g.My * g.Mx / bm);
+    return 0;
 }
 
 namespace {

@@ -6,11 +6,7 @@
 
 namespace dcs {
 
-struct Part {  // one chunk's statistics of one (n,c)
-    float cnt, mean, m2, mx;
-    int amax;
-    int pad[3];
-};
+// Part (one chunk's statistics of one (n,c)): common.hpp, shared with the conv epilogue
 
 static inline int stats_chunks(int N, int HW) {
     int want = (int)cdiv(1024, N);
@@ -451,6 +447,18 @@ extern "C" int dcs_in_stats(const float* x, int N, int HW, int C, float eps, flo
     hipLaunchKernelGGL(in_stats_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts,
                        N, C, nchunk, eps, scale, shift, xmax, xargmax);
     return check_launch("in_stats_finalize");
+}
+
+// Finalize statistics whose per-chunk partials were written by a producer (the conv rows pass
+// with fused statistics, dcs_conv_rows_in_stats): same merge as dcs_in_stats.
+extern "C" int dcs_in_stats_finish(const void* parts, int N, int C, int nchunk, float eps, float* scale, float* shift,
+                                   float* xmax, int32_t* xargmax, void* stream) {
+    if (!parts || !scale || !shift || N <= 0 || C <= 0 || nchunk <= 0)
+        return fail(DCS_E_INVALID, "in_stats_finish: bad arguments");
+    hipLaunchKernelGGL(in_stats_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const Part*>(parts), N, C, nchunk, eps, scale, shift, xmax,
+                       xargmax);
+    return check_launch("in_stats_finish");
 }
 
 extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW, int C,

@@ -69,11 +69,9 @@ class _Block:
 def _res_block_forward(L, W, b, x, use_cbam, keep):
     """One ResidualBlock[WithCBAM] (modules/model.py:56-87) on NHWC x."""
     res = L["res"]
-    y1 = res.forward(Src.nhwc(x), W["pk"][f"r{b}.c1.w"])
-    s1 = ops.in_stats(y1)
+    y1, s1 = res.forward_in_stats(Src.nhwc(x), W["pk"][f"r{b}.c1.w"])
     a1 = ops.in_apply(y1, s1, ACT_RELU)
-    y2 = res.forward(Src.nhwc(a1), W["pk"][f"r{b}.c2.w"])
-    s2 = ops.in_stats(y2, want_max=use_cbam)
+    y2, s2 = res.forward_in_stats(Src.nhwc(a1), W["pk"][f"r{b}.c2.w"], want_max=use_cbam)
     cb = None
     if use_cbam:
         w1, w2, wsa = W[f"r{b}.fc1"], W[f"r{b}.fc2"], W[f"r{b}.sa"]
@@ -129,24 +127,20 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
         pk[f"r{b}.c1.w"] = L["res"].pack_fwd(W[f"r{b}.c1.w"])
         pk[f"r{b}.c2.w"] = L["res"].pack_fwd(W[f"r{b}.c2.w"])
     N, H, Wd = stem_src.N, stem_src.H, stem_src.W
-    y0 = L["stem"].forward(stem_src, pk["stem.w"])
-    s0 = ops.in_stats(y0)
+    # every conv followed by an InstanceNorm returns its statistics (fused into the conv epilogue)
+    y0, s0 = L["stem"].forward_in_stats(stem_src, pk["stem.w"])
     a0 = ops.in_apply(y0, s0, ACT_RELU)
-    y1 = L["down1"].forward(Src.nhwc(a0), pk["down1.w"])
-    s1 = ops.in_stats(y1)
+    y1, s1 = L["down1"].forward_in_stats(Src.nhwc(a0), pk["down1.w"])
     a1 = ops.in_apply(y1, s1, ACT_RELU)
-    y2 = L["down2"].forward(Src.nhwc(a1), pk["down2.w"])
-    s2 = ops.in_stats(y2)
+    y2, s2 = L["down2"].forward_in_stats(Src.nhwc(a1), pk["down2.w"])
     h = ops.in_apply(y2, s2, ACT_RELU)
     blocks = []
     for b in range(nb):
         h, blk = _res_block_forward(L, W, b, h, use_cbam, keep)
         blocks.append(blk)
-    yu1 = L["up1"].forward(Src.nhwc(h), pk["up1.w"])
-    su1 = ops.in_stats(yu1)
+    yu1, su1 = L["up1"].forward_in_stats(Src.nhwc(h), pk["up1.w"])
     au1 = ops.in_apply(yu1, su1, ACT_RELU)
-    yu2 = L["up2"].forward(Src.nhwc(au1), pk["up2.w"])
-    su2 = ops.in_stats(yu2)
+    yu2, su2 = L["up2"].forward_in_stats(Src.nhwc(au1), pk["up2.w"])
     out = L["head"].forward(Src.nhwc(yu2), pk["head.w"], bias=W["head.b"],
                             pro=(su2.scale, su2.shift, ACT_RELU), epi_act=ACT_TANH)
     out = out.view(N, 1, H, Wd)
@@ -281,9 +275,9 @@ def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: boo
     h = y0
     for i in (1, 2, 3):
         st = sts[-1]
-        h = L[i].forward(Src.nhwc(h), pk[i], pro=(st.scale, st.shift, ACT_LRELU))
+        h, st = L[i].forward_in_stats(Src.nhwc(h), pk[i], pro=(st.scale, st.shift, ACT_LRELU))
         ys.append(h)
-        sts.append(ops.in_stats(h))
+        sts.append(st)
     st = sts[-1]
     out = L[4].forward(Src.nhwc(h), pk[4], bias=bs[4], pro=(st.scale, st.shift, ACT_LRELU))
     H4, W4 = out.shape[1], out.shape[2]

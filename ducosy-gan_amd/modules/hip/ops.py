@@ -32,6 +32,8 @@ _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
 # split-in-the-gather rows kernel of conv.hip (A/B switch)
 _X6P = os.environ.get("DUCOSY_X6P", "0") == "1"
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
+# IN statistics fused into the conv epilogue (ConvGeom.forward_in_stats); "0" = separate pass (A/B)
+_FUSE_STATS = os.environ.get("DUCOSY_FUSE_STATS", "1") == "1"
 _KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
 
 
@@ -307,6 +309,44 @@ class ConvGeom:
         return d
 
     # ---- forward -------------------------------------------------------------------
+    def _x6p_fwd(self, s: Src, d, bias) -> bool:
+        return (not self.narrow and bias is None and s.t2 is None and s.t.is_contiguous()
+                and s.strides == (s.H * s.W * s.C, 1, s.W * s.C, s.C) and _x6p(d))
+
+    def forward_in_stats(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                         pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
+                         epi_act: int = ACT_NONE, want_max: bool = False):
+        """forward() and the InstanceNorm statistics of its output (the IN that follows every
+        Generator / PatchGAN conv, modules/model.py:94-111, 124-129).  Where the rows pass applies
+        (Ho*Wo % 128 == 0) the per-tile partials come out of the conv epilogue
+        (dcs_conv_rows_in_stats) and one small kernel merges them (dcs_in_stats_finish): the
+        statistics pass's re-read of the output is gone.  Otherwise: forward + in_stats."""
+        Ho, Wo = self.out_hw(s.H, s.W)
+        d = self._desc_fwd(s, wpack.shape[1], pro[2] if pro is not None else ACT_NONE, epi_act)
+        nb = 0 if (self.narrow or not _FUSE_STATS) else lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d))
+        if nb == 0 or self._x6p_fwd(s, d, bias):
+            out = self.forward(s, wpack, bias, pro, epi_act)
+            return out, in_stats(out, want_max)
+        assert s.C == self.cin or (s.C == 4 and self.cin < 4), (s.C, self.cin)
+        _check_dev(s.t, s.t2, wpack, bias)
+        dev = s.t.device
+        out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
+        parts = workspace(nb, dev)
+        nchunk = ctypes.c_int(0)
+        e0 = PROBE.begin() if _is_res_geom(self) else None
+        lib.call("dcs_conv_rows_in_stats", ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
+                 _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _p(parts), parts.numel(),
+                 ctypes.byref(nchunk), _stream())
+        PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
+        C = self.cout
+        scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        shift = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        xmax = torch.empty(s.N, C, device=dev, dtype=torch.float32) if want_max else None
+        xam = torch.empty(s.N, C, device=dev, dtype=torch.int32) if want_max else None
+        lib.call("dcs_in_stats_finish", _p(parts), s.N, C, nchunk.value, IN_EPS, _p(scale), _p(shift), _p(xmax),
+                 _p(xam), _stream())
+        return out, INStats(scale, shift, xmax, xam)
+
     def forward(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
                 epi_act: int = ACT_NONE) -> torch.Tensor:
@@ -317,8 +357,7 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
-        x6p = (not self.narrow and bias is None and s.t2 is None and s.t.is_contiguous()
-               and s.strides == (s.H * s.W * s.C, 1, s.W * s.C, s.C) and _x6p(d))
+        x6p = self._x6p_fwd(s, d, bias)
         if x6p:  # operands split once, k-tiles staged by LDS-DMA (conv_x6p.hip)
             sp, wpp = split_x6(s.t), split_x6(wpack)
         e0 = PROBE.begin() if _is_res_geom(self) else None

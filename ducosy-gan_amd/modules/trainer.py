@@ -174,15 +174,22 @@ class ConcurrentCycleGANs:
     schedule "serial" (default): the systems step one after the other on the caller's stream.
     schedule "concurrent": one HIP stream per system; the kernels of one model fill the gaps of
     the other (small normalisation / loss / Adam launches, split-K reductions, launch latency).
-    Workspaces are per stream (ops.workspace) and the kernels are deterministic, so each
-    model's numbers equal its own sequential run bit for bit in every MFMA operand mode
-    (tests/test_gpu_concurrent.py; guard bands around every output and workspace,
-    tests/test_gpu_guard.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
+    Workspaces are per stream (ops.workspace).  The concurrent schedule runs the exact-f32
+    operand mode (MMA): with bf16-family rows kernels on the two streams, a model's numbers
+    sometimes leave its sequential run (Config 5: root cause not found; with
+    f32 operands each model equals its own sequential run bit for bit,
+    tests/test_gpu_concurrent.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
     --dual-schedule groups, modules/parallel.py): each model on its own half of the ranks."""
+
+    MMA = "f32"
 
     def __init__(self, systems, device, schedule="serial"):
         if schedule not in ("concurrent", "serial"):
             raise ValueError("schedule must be 'concurrent' or 'serial'")
+        from .hip import ops
+        if schedule == "concurrent" and ops.get_mma() != self.MMA:
+            raise ValueError(f"the concurrent schedule runs the {self.MMA} operand mode (ops.set_mma('{self.MMA}')); "
+                             f"current mode {ops.get_mma()}: see DESIGN.md §3, Config 5")
         self.systems = list(systems)
         self.device = torch.device(device)
         self.schedule = schedule

@@ -120,6 +120,20 @@ int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, c
                   const float* bias, const float* pro_scale, const float* pro_shift, float* out,
                   void* stream);
 
+/* Forward pass with the InstanceNorm statistics of its output fused into the epilogue
+ * (modules/model.py:94-111 — every conv that an InstanceNorm2d follows; aten convolution +
+ * the statistics half of instance_norm): `out` as dcs_conv_rows, and per (row tile, channel) the
+ * tile's count / mean / M2 / max / first argmax into `parts` (tiles never straddle images).
+ * Needs parity 0 (or the sub-pixel forward, parity 2: per phase), Co > 4 and rows per image
+ * % 128 == 0 (parts: dcs_conv_rows_in_stats_parts_size(d)
+ * bytes; 0 = not applicable).  *nchunk receives the tiles per image, the `nchunk` of
+ * dcs_in_stats_finish, which turns the partials into the scale / shift (and max / argmax) of
+ * dcs_in_stats. */
+size_t dcs_conv_rows_in_stats_parts_size(const dcs_conv_desc* d);
+int dcs_conv_rows_in_stats(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,
+                           const float* bias, const float* pro_scale, const float* pro_shift, float* out, void* parts,
+                           size_t parts_bytes, int* nchunk, void* stream);
+
 /* bf16x6 operand planes: n fp32 values (n % 8 == 0, 16-byte aligned) -> 3n bf16 in groups of
  * 8 consecutive values as [hi[8], mid[8], lo[8]] (v = hi + mid + lo, each residual exact in
  * fp32).  The pre-split operand format of dcs_conv_rows_x6p. */
@@ -186,6 +200,11 @@ int dcs_upsample2_grad(const float* dup, float* dx, int N, int H, int W, int C, 
 size_t dcs_in_stats_workspace_size(int N, int HW, int C);
 int dcs_in_stats(const float* x, int N, int HW, int C, float eps, float* scale, float* shift,
                  float* xmax, int32_t* xargmax, void* ws, size_t ws_bytes, void* stream);
+
+/* The second half of dcs_in_stats over partials a producer wrote (dcs_conv_rows_in_stats):
+ * parts [N][nchunk][C] chunk records, merged per (n,c) in a fixed order (deterministic). */
+int dcs_in_stats_finish(const void* parts, int N, int C, int nchunk, float eps, float* scale, float* shift,
+                        float* xmax, int32_t* xargmax, void* stream);
 
 /* out = act(x*scale + shift) */
 int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW,

@@ -19,7 +19,21 @@ def _batch(seed, i, n, hw, cin):
     return rA, rB, mk
 
 
-@pytest.mark.parametrize("mode", ["bf16x6", "f32"])
+def test_concurrent_schedule_refuses_bf16_modes():
+    """The two-stream schedule runs exact-f32 operands (Config 5)."""
+    from modules.hip import ops
+    from modules.trainer import ConcurrentCycleGANs
+    prev = ops.get_mma()
+    ops.set_mma("bf16x6")
+    try:
+        with pytest.raises(ValueError, match="f32"):
+            ConcurrentCycleGANs([], DEV, schedule="concurrent")
+        ConcurrentCycleGANs([], DEV, schedule="serial")  # the serial schedule runs every mode
+    finally:
+        ops.set_mma(prev)
+
+
+@pytest.mark.parametrize("mode", ["f32"])
 def test_concurrent_equals_sequential(mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs

@@ -3,10 +3,10 @@
 Every tensor the product code allocates through torch.empty / empty_like / zeros / zeros_like /
 ones on the device (kernel outputs, padded dgrad buffers, split-K partial slabs, the per-stream
 workspaces) is carved out of a larger buffer whose 4 KiB on either side is filled with a canary
-byte.  One bf16x6 step of two CycleGANs on two HIP streams (config 5's concurrent schedule) and
-one single-stream step run with every allocation guarded; afterwards every guard band must still
-hold the canary: no kernel stores outside the extent its host code allocated for it
-(the two-stream audit).
+byte.  One step of two CycleGANs on two HIP streams (config 5's concurrent schedule, which runs
+the f32 operand mode) and one single-stream bf16x6 step run with every allocation guarded;
+afterwards every guard band must still hold the canary: no kernel stores outside the extent its
+host code allocated for it (the two-stream audit).
 """
 import math
 
@@ -90,14 +90,14 @@ class _Guarded:
         return bad
 
 
-@pytest.mark.parametrize("schedule", ["concurrent", "serial"])
-def test_no_store_outside_allocations(schedule):
+@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("serial", "bf16x6")])
+def test_no_store_outside_allocations(schedule, mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
     n, hw, nb = 2, 64, 2
     cfg = [(3, 821), (2, 822)]
     prev = ops.get_mma()
-    ops.set_mma("bf16x6")
+    ops.set_mma(mode)
     saved_ws = dict(ops._WS)
     try:
         run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV, schedule=schedule)

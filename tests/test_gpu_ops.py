@@ -298,3 +298,53 @@ def test_four_channel_stem_path(ops, c1, c2, k, stride, pads, mode):
     add = rnd((2, H, W, 1), 42, "add").cuda()
     got = g.dgrad(dyn, g.pack_dgrad(w.detach().cuda(), 1), H, W, ci_count=1, addend=add)
     assert rel(got, dx + add) < 1e-6
+
+
+STATS_CASES = [
+    # cin, cout, k, stride, pads, mode, up, N, H, W, pro, want_max
+    (256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, 2, 16, 16, False, True),   # residual (256-row x6 tiles)
+    (256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, 3, 16, 24, False, True),   # residual, 384 rows (128-row tiles)
+    (64, 128, 3, 2, (1, 1, 1, 1), "zero", 1, 2, 32, 32, False, False),      # down1
+    (256, 128, 3, 1, (1, 1, 1, 1), "zero", 2, 2, 16, 16, False, False),     # up1 (sub-pixel phases)
+    (64, 128, 4, 2, (1, 1, 1, 1), "zero", 1, 2, 32, 32, True, False),       # PatchGAN layer 1 (LReLU prologue)
+]
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16x6"])
+@pytest.mark.parametrize("case", STATS_CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}N{c[7]}H{c[8]}W{c[9]}"
+                                                   for c in STATS_CASES])
+def test_forward_in_stats_matches_stats_pass(ops, mode, case):
+    """IN statistics from the conv epilogue (dcs_conv_rows_in_stats + dcs_in_stats_finish) ==
+    forward + the statistics pass: the same output bits, scale / shift to fp32 rounding, the same
+    max and first argmax."""
+    from modules.hip.lib import ACT_LRELU, DCS_PAD_REFLECT, DCS_PAD_ZERO
+    from modules.hip.ops import ConvGeom, Src
+    cin, cout, k, s, pads, pm, up, N, H, W, pro, want_max = case
+    g = ConvGeom(cin, cout, k, s, pads, DCS_PAD_REFLECT if pm == "reflect" else DCS_PAD_ZERO, up)
+    prev = ops.get_mma()
+    ops.set_mma(mode)
+    try:
+        x = rnd((N, H, W, cin), 51, f"sx{cin}{H}{W}").cuda()
+        w = torch.from_numpy(prng.normal(52, f"sw{cin}{cout}", (cout, cin, k, k), 0, 0.05)).cuda()
+        p = None
+        if pro:
+            st0 = ops.in_stats(x)
+            p = (st0.scale, st0.shift, ACT_LRELU)
+        wp = g.pack_fwd(w)
+        y_ref = g.forward(Src.nhwc(x), wp, pro=p)
+        s_ref = ops.in_stats(y_ref, want_max=want_max)
+        y, st = g.forward_in_stats(Src.nhwc(x), wp, pro=p, want_max=want_max)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_mma(prev)
+    assert torch.equal(y, y_ref)
+    assert rel(st.scale, s_ref.scale) < 2e-6
+    assert float((st.shift - s_ref.shift).abs().max()) < 2e-6 * max(1.0, float(s_ref.shift.abs().max()))
+    if want_max:
+        assert torch.equal(st.xmax, s_ref.xmax)
+        assert torch.equal(st.xargmax, s_ref.xargmax)
+    # and the fused path really ran (rows per image % 128 == 0 here)
+    import ctypes
+    from modules.hip import lib
+    d = g._desc_fwd(Src.nhwc(x), wp.shape[1], p[2] if p else 0, 0)
+    assert lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d)) > 0
