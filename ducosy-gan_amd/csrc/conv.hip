@@ -90,6 +90,10 @@ constexpr int NT = 256;
 #ifndef DCS_WGRAD_X6
 #define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
 #endif
+#ifndef DCS_WGRAD_X6_CO64
+#define DCS_WGRAD_X6_CO64 0  // ... also for 64 output channels (128-row tile, half masked): measured
+                             // 3.49 ms vs 2.58 ms f32 on up2 at bs 16, off
+#endif
 #ifndef DCS_X6_BN64
 #define DCS_X6_BN64 1  // bf16x6 rows also for 64-column tiles
 #endif
@@ -2182,8 +2186,10 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (d.mma == MMA_BF16X6 && vec && dy_small && p.BM == 128 && d.parity != 1 && DCS_WGRAD_X6) {
-        // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs
+    } else if (d.mma == MMA_BF16X6 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64)) &&
+               d.parity != 1 && DCS_WGRAD_X6) {
+        // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
+        // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
         if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
     } else if (p.BM == 128) {

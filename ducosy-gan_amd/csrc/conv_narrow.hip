@@ -178,6 +178,85 @@ __global__ __launch_bounds__(256) void narrow_wgrad_tiled_kernel(const dcs_conv_
         }
 }
 
+// weight gradient, Co == 1, with a register window along x: thread (row group rg, ty, c) keeps
+// the KW tap sums of (ty, tx = 0..KW-1, c) and walks the tile's pixel rows of its group; each
+// staged source value it reads feeds KW multiply-adds (the per-item kernel above read one LDS
+// value per multiply-add).  Per-thread sums persist across the block's tiles; the row groups are
+// added in a fixed order at the end (deterministic).  Same partial layout as the kernel above.
+template <int KH, int KW, int NCH>
+__global__ __launch_bounds__(256) void narrow_wgrad_win_kernel(const dcs_conv_desc d, const float* __restrict__ dy,
+                                                               const float* __restrict__ src,
+                                                               const float* __restrict__ psc,
+                                                               const float* __restrict__ psh,
+                                                               float* __restrict__ part, int tiles_x, int tiles_y) {
+    constexpr int HH = NT_TH + KH - 1, HW_ = NT_TW + KW - 1;
+    constexpr int ITEMS = KH * NT_CC;            // (ty, c) pairs per chunk
+    constexpr int RG = 256 / ITEMS;              // row groups (4 for 7x7)
+    constexpr int RPG = (NT_TH + RG - 1) / RG;   // tile rows per group
+    __shared__ __attribute__((aligned(16))) float lin[HH * HW_ * NT_CC];
+    __shared__ float ldy[NT_TH * NT_TW];
+    const int rg = threadIdx.x / ITEMS, item = threadIdx.x - (threadIdx.x / ITEMS) * ITEMS;
+    const bool live = rg < RG;
+    const int ty = item / NT_CC, c = item - (item / NT_CC) * NT_CC;
+    float acc[NCH][KW];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) acc[k][tx] = 0.f;
+    const int ntiles = tiles_x * tiles_y * d.N;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int n = tile / (tiles_x * tiles_y);
+        const int rem = tile - n * tiles_x * tiles_y;
+        const int oy0 = (rem / tiles_x) * NT_TH, ox0 = (rem % tiles_x) * NT_TW;
+        __syncthreads();
+        for (int i = threadIdx.x; i < NT_TH * NT_TW; i += blockDim.x) {
+            const int yy = oy0 + i / NT_TW, xx = ox0 + i % NT_TW;
+            ldy[i] = (yy < d.Ho && xx < d.Wo) ? dy[((long long)n * d.Ho + yy) * d.Wo + xx] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            __syncthreads();
+            stage_halo<KH, KW>(d, src, psc, psh, n, oy0, ox0, k * NT_CC, lin);
+            __syncthreads();
+            if (live) {
+                for (int r = 0; r < RPG; ++r) {
+                    const int yy = rg * RPG + r;
+                    if (yy >= NT_TH) break;
+                    const float* row = lin + (yy + ty) * HW_ * NT_CC + c;
+                    const float* g = ldy + yy * NT_TW;
+                    float w[KW];
+#pragma unroll
+                    for (int tx = 0; tx < KW - 1; ++tx) w[tx] = row[tx * NT_CC];
+#pragma unroll
+                    for (int xx = 0; xx < NT_TW; ++xx) {
+                        w[(xx + KW - 1) % KW] = row[(xx + KW - 1) * NT_CC];
+                        const float gv = g[xx];
+#pragma unroll
+                        for (int tx = 0; tx < KW; ++tx) acc[k][tx] = fmaf(gv, w[(xx + tx) % KW], acc[k][tx]);
+                    }
+                }
+            }
+        }
+    }
+    // add the row groups in order, through LDS (one chunk at a time)
+    float* red = lin;  // [RG][ITEMS][KW]
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+        __syncthreads();
+        if (live)
+#pragma unroll
+            for (int tx = 0; tx < KW; ++tx) red[(rg * ITEMS + item) * KW + tx] = acc[k][tx];
+        __syncthreads();
+        for (int i = threadIdx.x; i < ITEMS * KW; i += blockDim.x) {
+            const int it = i / KW, tx = i - (i / KW) * KW;
+            float sum = 0.f;
+            for (int q = 0; q < RG; ++q) sum += red[(q * ITEMS + it) * KW + tx];
+            const int tyy = it / NT_CC, cc = it - (it / NT_CC) * NT_CC;
+            part[(long long)blockIdx.x * (KH * KW * d.Cs) + (long long)(tyy * KW + tx) * d.Cs + k * NT_CC + cc] = sum;
+        }
+    }
+}
+
 bool narrow_tiled_ok(const dcs_conv_desc& d, const float* src) {
     return !d.parity && d.Co == 1 && d.up == 1 && d.stride == 1 && d.Cs % NT_CC == 0 && d.s_c == 1 &&
            d.csplit == d.Cs && (d.s_w % 4 == 0) && (d.s_h % 4 == 0) && (d.s_n % 4 == 0) &&
@@ -207,8 +286,13 @@ int narrow_wgrad_tiled_blocks(const dcs_conv_desc& d) {
 int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const float* src, const float* psc,
                               const float* psh, float* part, hipStream_t s) {
     const int tx = (int)cdiv(d.Wo, NT_TW), ty = (int)cdiv(d.Ho, NT_TH);
+#ifdef DCS_NARROW_WGRAD_ITEMS  // A/B: one LDS read per multiply-add
     hipLaunchKernelGGL((narrow_wgrad_tiled_kernel<7, 7, 8>), dim3(narrow_wgrad_tiled_blocks(d)), dim3(256), 0, s, d,
                        dy, src, psc, psh, part, tx, ty);
+#else
+    hipLaunchKernelGGL((narrow_wgrad_win_kernel<7, 7, 8>), dim3(narrow_wgrad_tiled_blocks(d)), dim3(256), 0, s, d,
+                       dy, src, psc, psh, part, tx, ty);
+#endif
     return check_launch("narrow_wgrad_tiled");
 }
 
