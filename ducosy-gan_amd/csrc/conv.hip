@@ -1731,6 +1731,9 @@ static bool vec_ok(const dcs_conv_desc* d, const float* src) {
 bool narrow_tiled_ok(const dcs_conv_desc& d, const float* src);
 int launch_narrow_rows_tiled(const dcs_conv_desc& d, const float* src, const float* wp, const float* bias,
                              const float* psc, const float* psh, float* out, hipStream_t s);
+bool narrow_small_ok(const dcs_conv_desc& d, const float* src);
+int launch_narrow_rows_small(const dcs_conv_desc& d, const float* src, const float* wp, const float* bias,
+                             const float* psc, const float* psh, float* out, hipStream_t s);
 bool narrow_wgrad_tiled_ok(const dcs_conv_desc& d, const float* src);
 int narrow_wgrad_tiled_blocks(const dcs_conv_desc& d);
 int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const float* src, const float* psc,
@@ -2237,6 +2240,7 @@ extern "C" int dcs_conv_rows_narrow(const dcs_conv_desc* dp, const float* src, c
         if (M > Mmax) Mmax = M;
     }
     hipStream_t s = as_stream(stream);
+    if (narrow_small_ok(d, src)) return launch_narrow_rows_small(d, src, wpack, bias, psc, psh, out, s);
     if (narrow_tiled_ok(d, src)) return launch_narrow_rows_tiled(d, src, wpack, bias, psc, psh, out, s);
     dim3 grid((unsigned)cdiv(Mmax, 256), ncls);
     const bool vec = vec_ok(dp, src);

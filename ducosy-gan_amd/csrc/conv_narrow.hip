@@ -257,6 +257,96 @@ __global__ __launch_bounds__(256) void narrow_wgrad_win_kernel(const dcs_conv_de
     }
 }
 
+// One output channel over many input channels on small images (the PatchGAN last layer,
+// modules/model.py:129: Conv 4x4 512->1 on 32 x 32): a tiled kernel gets one block per 16 x 64
+// output tile, 32 blocks for a batch of 16, so here one WAVE computes one output pixel, its 64
+// lanes splitting the channels (CPL each; a tap's pixel row is one coalesced 2 KiB read), the
+// weights of the lane's channels held in registers, the prologue (IN + LeakyReLU of the
+// previous layer) applied per element, then a fixed-order cross-lane sum.
+template <int KH, int KW, int CPL>
+__global__ __launch_bounds__(256) void narrow_rows_small_kernel(const dcs_conv_desc d, const float* __restrict__ src,
+                                                                const float* __restrict__ wp,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ psc,
+                                                                const float* __restrict__ psh,
+                                                                float* __restrict__ out) {
+    static_assert(CPL % 4 == 0, "float4 channel groups");
+    const int lane = threadIdx.x & 63;
+    const int c0 = lane * CPL;
+    float w[KH * KW][CPL];
+#pragma unroll
+    for (int t = 0; t < KH * KW; ++t)
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) w[t][j] = wp[((long long)t * d.Cs + c0 + j) * d.ldb];
+    const float b = bias ? bias[0] : 0.f;
+    const long long P = (long long)d.N * d.Ho * d.Wo;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long p = wave; p < P; p += nwaves) {
+        const int n = (int)(p / ((long long)d.Ho * d.Wo));
+        const int rem = (int)(p - (long long)n * d.Ho * d.Wo);
+        const int oy = rem / d.Wo, ox = rem - (rem / d.Wo) * d.Wo;
+        float sc[CPL], sh[CPL];
+        if (d.pro_act != DCS_ACT_NONE) {
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+                sc[j] = psc[(long long)n * d.Cs + c0 + j];
+                sh[j] = psh[(long long)n * d.Cs + c0 + j];
+            }
+        }
+        float acc = 0.f;
+#pragma unroll
+        for (int ty = 0; ty < KH; ++ty) {
+            const int iy = oy * d.stride + ty - d.pt;
+            if (iy < 0 || iy >= d.Hs) continue;  // zero padding
+#pragma unroll
+            for (int tx = 0; tx < KW; ++tx) {
+                const int ix = ox * d.stride + tx - d.pl;
+                if (ix < 0 || ix >= d.Ws) continue;
+                const float* sp = src + n * d.s_n + iy * d.s_h + ix * d.s_w + c0;
+#pragma unroll
+                for (int j4 = 0; j4 < CPL / 4; ++j4) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(sp + 4 * j4);
+                    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = 4 * j4 + e;
+                        const float a = d.pro_act != DCS_ACT_NONE ? act_apply(fmaf(v[e], sc[j], sh[j]), d.pro_act) : v[e];
+                        acc = fmaf(a, w[ty * KW + tx][j], acc);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) {
+            float v = acc + b;
+            if (d.epi_act != DCS_ACT_NONE) v = act_apply(v, d.epi_act);
+            out[p] = v;
+        }
+    }
+}
+
+bool narrow_small_ok(const dcs_conv_desc& d, const float* src) {
+    return !d.parity && d.Co == 1 && d.up == 1 && d.pad_mode == DCS_PAD_ZERO && d.KH == 4 && d.KW == 4 &&
+           (d.Cs == 256 || d.Cs == 512) && d.s_c == 1 && d.csplit == d.Cs && d.s_w % 4 == 0 && d.s_h % 4 == 0 &&
+           d.s_n % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (long long)d.Ho * d.Wo <= 64 * 64;
+}
+
+int launch_narrow_rows_small(const dcs_conv_desc& d, const float* src, const float* wp, const float* bias,
+                             const float* psc, const float* psh, float* out, hipStream_t s) {
+    const long long P = (long long)d.N * d.Ho * d.Wo;
+    long long blocks = cdiv(P, 4);  // one wave per pixel, 4 waves per block
+    if (blocks > 2048) blocks = 2048;
+    if (d.Cs == 512)
+        hipLaunchKernelGGL((narrow_rows_small_kernel<4, 4, 8>), dim3((unsigned)blocks), dim3(256), 0, s, d, src, wp, bias,
+                           psc, psh, out);
+    else
+        hipLaunchKernelGGL((narrow_rows_small_kernel<4, 4, 4>), dim3((unsigned)blocks), dim3(256), 0, s, d, src, wp, bias,
+                           psc, psh, out);
+    return check_launch("narrow_rows_small");
+}
+
 bool narrow_tiled_ok(const dcs_conv_desc& d, const float* src) {
     return !d.parity && d.Co == 1 && d.up == 1 && d.stride == 1 && d.Cs % NT_CC == 0 && d.s_c == 1 &&
            d.csplit == d.Cs && (d.s_w % 4 == 0) && (d.s_h % 4 == 0) && (d.s_n % 4 == 0) &&

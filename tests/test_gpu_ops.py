@@ -59,6 +59,7 @@ CONV_CASES = [
     (64, 128, 4, 2, (1, 1, 1, 1), "zero", 1, 16),       # D layer 1
     (256, 512, 4, 2, (1, 1, 1, 1), "zero", 1, 8),       # D layer 3
     (512, 1, 4, 1, (2, 2, 1, 1), "zero", 1, 4),         # D last (narrow, asymmetric pad)
+    (256, 1, 4, 1, (2, 2, 1, 1), "zero", 1, 9),         # one-wave-per-pixel kernel, 4 channels per lane
     # the layer shapes of a 64x64 generator at batch 1 (split-K wgrad, multi-tile rows)
     (256, 128, 3, 1, (1, 1, 1, 1), "zero", 2, 16),
     (128, 64, 3, 1, (1, 1, 1, 1), "zero", 2, 32),
