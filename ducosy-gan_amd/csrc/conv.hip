@@ -97,6 +97,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_BN64
 #define DCS_X6_BN64 1  // bf16x6 rows also for 64-column tiles
 #endif
+#ifndef DCS_X6_V4
+#define DCS_X6_V4 1  // bf16x6 rows also for the 4-channel NHWC gather (stem, PatchGAN layer 0)
+#endif
 #ifndef DCS_ROWS_F32
 #define DCS_ROWS_F32 0  // A/B only: the rows pass ignores the bf16 operand modes (exact f32)
 #endif
@@ -692,11 +695,12 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // the next tile's gather wait); it records the channel offset into psc/psh, -1 for none
     auto load_a = [&](int kt, auto& dst, int& pa) {
         pa = -1;
-        if (VEC == 2) {  // Cs == 4: taps aj .. aj+3, one float4 each (no prologue)
-            dst[0] = dst[1] = dst[2] = dst[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (VEC == 2) {  // Cs == 4: taps aj .. aj+ACH-1, one float4 each (no prologue)
+#pragma unroll
+            for (int e = 0; e < ACH; ++e) dst[e] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < ACH; ++e) {
                     const int j = aj + e;
                     if (j < g.ntaps) {
                         int ady, adx, bt;
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                     }
                 }
             }
-            aj += BK / 4;
+            aj += BKT / 4;
         } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
             // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
             int sy = 0, sx = 0, off = OOB_OFF;
@@ -1805,6 +1809,11 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
         else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
         else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        return check_launch("conv_rows");
+    }
+    if (v4 && d.mma == MMA_BF16X6 && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
+        if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
         return check_launch("conv_rows");
     }
     const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
