@@ -169,24 +169,28 @@ __device__ __forceinline__ void chan_merge(double& cnt, double& mean, double& m2
     if (mxb > mx || (mxb == mx && amb < am)) { mx = mxb; am = amb; }
 }
 
+// SUB sub-lanes per (n,c): 8, or 32 for the many-chunk partials of the conv epilogue
+// (dcs_in_stats_finish: Ho*Wo/128 chunks per image)
+template <int SUB>
 __global__ __launch_bounds__(256) void in_stats_finalize8_kernel(const Part* __restrict__ parts, int N, int C,
                                                                   int nchunk, float eps, float* __restrict__ scale,
                                                                   float* __restrict__ shift, float* __restrict__ xmax,
                                                                   int* __restrict__ xam) {
-    const int idx = blockIdx.x * 32 + (threadIdx.x >> 3), sub = threadIdx.x & 7;
+    constexpr int LOG = SUB == 32 ? 5 : 3;
+    const int idx = blockIdx.x * (256 / SUB) + (threadIdx.x >> LOG), sub = threadIdx.x & (SUB - 1);
     const bool live = idx < N * C;
     const int n = live ? idx / C : 0, c = live ? idx - n * C : 0;
     double cnt = 0.0, mean = 0.0, m2 = 0.0;
     float mx = -INFINITY;
     int am = 0x7fffffff;
     if (live) {
-        for (int k = sub; k < nchunk; k += 8) {
+        for (int k = sub; k < nchunk; k += SUB) {
             const Part p = parts[((long long)n * nchunk + k) * C + c];
             chan_merge(cnt, mean, m2, mx, am, p.cnt, p.mean, p.m2, p.mx, p.amax);
         }
     }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
+    for (int o = 1; o < SUB; o <<= 1) {
         const double nb = __shfl_xor(cnt, o, 64), mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
         const float mxb = __shfl_xor(mx, o, 64);
         const int amb = __shfl_xor(am, o, 64);
@@ -444,7 +448,7 @@ extern "C" int dcs_in_stats(const float* x, int N, int HW, int C, float eps, flo
         hipLaunchKernelGGL(in_stats_partial_kernel, dim3(N, nchunk), dim3(256), 0, s, x, HW, C, nchunk, parts);
     int e = check_launch("in_stats_partial");
     if (e) return e;
-    hipLaunchKernelGGL(in_stats_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts,
+    hipLaunchKernelGGL(in_stats_finalize8_kernel<8>, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts,
                        N, C, nchunk, eps, scale, shift, xmax, xargmax);
     return check_launch("in_stats_finalize");
 }
@@ -455,9 +459,14 @@ extern "C" int dcs_in_stats_finish(const void* parts, int N, int C, int nchunk, 
                                    float* xmax, int32_t* xargmax, void* stream) {
     if (!parts || !scale || !shift || N <= 0 || C <= 0 || nchunk <= 0)
         return fail(DCS_E_INVALID, "in_stats_finish: bad arguments");
-    hipLaunchKernelGGL(in_stats_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0,
-                       as_stream(stream), reinterpret_cast<const Part*>(parts), N, C, nchunk, eps, scale, shift, xmax,
-                       xargmax);
+    if (nchunk >= 64)
+        hipLaunchKernelGGL(in_stats_finalize8_kernel<32>, dim3((unsigned)cdiv((long long)N * C, 8)), dim3(256), 0,
+                           as_stream(stream), reinterpret_cast<const Part*>(parts), N, C, nchunk, eps, scale, shift,
+                           xmax, xargmax);
+    else
+        hipLaunchKernelGGL(in_stats_finalize8_kernel<8>, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0,
+                           as_stream(stream), reinterpret_cast<const Part*>(parts), N, C, nchunk, eps, scale, shift,
+                           xmax, xargmax);
     return check_launch("in_stats_finish");
 }
 
