@@ -1,15 +1,20 @@
 """Loss-curve parity: 50 training steps of CycleGANSystem (HIP, default bf16x6 operands) at
 BASELINE config 1 (128x128, bs 2, 1 residual block, cin 3) against the reference's own step loop
-(modules/trainer.py:447-525, tests/golden/make_golden.py --curve) run at 1, 2, 4 and 8 torch
+(modules/trainer.py:447-525, tests/golden/make_golden.py --curve) run at 1, 2, 3, 4, 6 and 8 torch
 threads.
 
 The reference does not agree with itself across thread counts: summation order changes the
-rounding, Adam turns rounding into +-lr moves, and the GAN game amplifies them (at step 49 the
-runs spread by 0.2 % on the cycle loss and by 10 % on the adversarial terms).  The tolerance is
-that spread: at every step and for every one of the 12 loss terms, the HIP value must lie within
-ENV x (the reference runs' largest spread up to that step) + FLOOR x |value| of the reference
-runs' median.  ENV = 3 admits one more run of the same family; FLOOR = 1e-3 is north_star's
-forward tolerance (the step-0 spread is ~1e-7).
+rounding, Adam turns rounding into +-lr moves, and the GAN game amplifies them (by step 19 the
+runs spread by 40 % on the contrast-edge term).  The bar is therefore calibrated on the reference
+runs themselves.  For a curve g and a set of reference runs r, at every step and for every one of
+the 12 loss terms,
+
+    q = |g - median(r)| / (spread(r) + FLOOR * |median(r)|)
+
+with spread the largest max-min of the runs up to that step and FLOOR = 1e-3 (north_star's
+forward tolerance).  Q_ref = the largest q of any reference run judged against the other five
+(leave-one-out); the HIP curve, judged against all six, must stay within it at every step.  So the
+HIP run deviates no more than the reference's own most deviant run does.
 """
 import json
 import os
@@ -25,7 +30,14 @@ from test_gpu_train import _system
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-ENV, FLOOR = 3.0, 1e-3
+FLOOR = 1e-3
+
+
+def _q(g, r):
+    """Deviation of curve g from runs r ([runs, steps]) in units of their running spread."""
+    mid = np.median(r, 0)
+    env = np.maximum.accumulate(r.max(0) - r.min(0))
+    return np.abs(g - mid) / (env + FLOOR * np.abs(mid))
 
 
 def test_loss_curve_within_reference_spread():
@@ -43,20 +55,23 @@ def test_loss_curve_within_reference_spread():
         out = s.train_step(rA, rB, mk)
         for k in keys:
             got[k].append(float(out[k]))
-    report, bad = {}, []
+    q_ref = 0.0  # leave-one-out: each reference run against the others
+    for i in range(len(threads)):
+        for k in keys:
+            q_ref = max(q_ref, float(_q(ref[k][i], np.delete(ref[k], i, 0)).max()))
+    report, bad = {"q_ref": q_ref}, []
     for k in keys:
         r = ref[k]
-        mid = np.median(r, 0)
-        env = np.maximum.accumulate(r.max(0) - r.min(0))
         g = np.array(got[k])
-        tol = ENV * env + FLOOR * np.abs(mid)
-        dev = np.abs(g - mid)
-        report[k] = {"hip": g.tolist(), "ref_median": mid.tolist(), "ref_spread": (r.max(0) - r.min(0)).tolist(),
-                     "max_dev_over_tol": float((dev / tol).max())}
-        for i in np.nonzero(dev > tol)[0][:3]:
-            bad.append((k, int(i), float(g[i]), float(mid[i]), float(tol[i])))
+        q = _q(g, r)
+        report[k] = {"hip": g.tolist(), "ref_median": np.median(r, 0).tolist(),
+                     "ref_spread": (r.max(0) - r.min(0)).tolist(), "q_max": float(q.max()),
+                     "q_mean": float(q.mean())}
+        for i in np.nonzero(q > q_ref)[0][:3]:
+            bad.append((k, int(i), float(g[i]), float(np.median(r[:, i])), float(q[i]), q_ref))
     out_dir = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(out_dir):
         with open(os.path.join(out_dir, "curve_hip.json"), "w") as f:
             json.dump(report, f)
+    assert q_ref >= 1.0, q_ref  # the reference runs do spread
     assert not bad, bad
