@@ -106,6 +106,21 @@ constexpr int NT = 256;
 #ifndef DCS_X6_PIPE
 #define DCS_X6_PIPE 1  // bf16x6 rows: global loads two k-tiles ahead (two register sets)
 #endif
+#ifndef DCS_X6_SELGATHER
+#define DCS_X6_SELGATHER 1  // bf16x6 rows: gather address by selects, no exec-mask branch
+#endif
+#ifndef DCS_X6_STORE_FIRST
+#define DCS_X6_STORE_FIRST 1  // bf16x6 rows: stage the next tile before folding the chain
+#endif
+#ifndef DCS_KSLICE_ALL
+#define DCS_KSLICE_ALL 1  // bf16x6 rows: slice-major K walk for every 16-channel-aligned source
+#endif
+#ifndef DCS_X6_SGB
+#define DCS_X6_SGB 5  // bf16x6 residual rows: VALU instructions scheduled after each MFMA (0 = compiler)
+#endif
+#ifndef DCS_X6_SGB0
+#define DCS_X6_SGB0 0  // ... the same for the other bf16x6 rows kernels
+#endif
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
@@ -565,6 +580,22 @@ __device__ __forceinline__ void rows_in_stats(const dcs_conv_desc& d, const floa
 //      2 = four float4 taps per thread over a 4-channel NHWC source (Cs == 4, the stem)
 // BM = 256 (bf16x6, 128 columns): 512 threads as 4 x 2 waves of 64 x 64, one workgroup per CU;
 // every staged weight k-tile then feeds twice the pixels (0.75 of the 128-row tile's bytes per MFMA)
+// bf16x6 rows k-loop body: the fragment reads first, then each MFMA followed by DCS_X6_SGB
+// VALU instructions (the next tile's split and address arithmetic), then the LDS stores, so the
+// split runs in the shadow of the wave's own MFMAs instead of after them (0 = compiler order)
+template <int NMFMA, int NV>
+__device__ __forceinline__ void x6_interleave() {
+    if constexpr (NV > 0) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // DS read
+#pragma unroll
+        for (int i = 0; i < NMFMA; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);  // DS write
+    }
+}
+
 template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
 __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
@@ -667,7 +698,10 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // residual convs) runs the DCS_KORDER_SLICE K order: all taps of a 16-channel slice, then
     // the next slice, so the source rows a slice gathers are re-read by its next taps from
     // L1/L2 instead of after a sweep over all channels (the dispatch requires d.korder == SLICE)
-    constexpr bool KS = TAG == 1;
+    // TAG 0 bf16x6 kernels with 16-channel-aligned sources walk the same slice-major order over
+    // tap-major packed weights (KSB: the B column is rebuilt from (tap, channel) per k-tile)
+    constexpr bool KSB = TAG != 1 && MMA == MMA_BF16X6 && VEC == 1 && DCS_KSLICE_ALL;
+    constexpr bool KS = TAG == 1 || KSB;
     int aj, ac;
     if constexpr (KS) {
         const int p0 = akq >> 4;
@@ -677,7 +711,15 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         aj = akq / d.Cs;
         ac = akq - (akq / d.Cs) * d.Cs;
     }
-    int bj = bkq / d.Cs, bc = bkq - (bkq / d.Cs) * d.Cs;
+    int bj, bc;
+    if constexpr (KSB) {
+        const int p0 = bkq >> 4;
+        bj = p0 % g.ntaps;
+        bc = (p0 / g.ntaps) * 16 + (bkq & 15);
+    } else {
+        bj = bkq / d.Cs;
+        bc = bkq - (bkq / d.Cs) * d.Cs;
+    }
     auto advance = [&](int& j, int& c) {
         if constexpr (KS) {
             j += BKT / 16;
@@ -718,7 +760,18 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             int sy = 0, sx = 0, off = OOB_OFF;
             // past the last k-tile (the x6 pipeline's unconditional prefetch) the walk leaves the
             // range through aj (tap-major) or through ac (slice-major): both must stay in range
-            if (aj < g.ntaps && ac < d.Cs) {
+            if constexpr (MMA == MMA_BF16X6 && DCS_X6_SELGATHER) {
+                // select form (tap 0 stands in for a tap past the end): no exec-mask branch
+                // splits the k-loop body, so the scheduler can spread the next tile's split
+                // arithmetic over this tile's MFMAs
+                const bool kin = aj < g.ntaps && ac < d.Cs;
+                int ady, adx, bt;
+                tap_decode(d, g, kin ? aj : 0, ady, adx, bt);
+                const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                off = (kin && rvalid && yok && xok) ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4
+                                                    : OOB_OFF;
+            } else if (aj < g.ntaps && ac < d.Cs) {
                 int ady, adx, bt;
                 tap_decode(d, g, aj, ady, adx, bt);
                 const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
@@ -778,10 +831,10 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     auto load_b = [&](int kt, auto& dst) {
         long long col;
         bool ok = true;
-        if (!d.parity) {
+        if (!d.parity && !KSB) {
             col = kt * BKT + bkq;
         } else {  // the BKPT k of this thread share one tap (Cs % 16 == 0)
-            ok = bj < g.ntaps;
+            ok = bj < g.ntaps && bc < d.Cs;
             int ady, adx, bt = 0;
             if (ok) tap_decode(d, g, bj, ady, adx, bt);
             col = (long long)bt * d.Cs + bc;
@@ -965,15 +1018,29 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 load_a(kt + 2, ra2, pa2);
                 load_b(kt + 2, rb2);
                 step(0, 0);
-                fold_t(kt);
-                if (kt + 1 < nkt) store_tiles(1, ra, rb, pa1);
+                if (DCS_X6_STORE_FIRST) {
+                    // staging before the chain fold and unconditional (a tile past the end is
+                    // zeros into a buffer nobody reads again): one basic block with the MFMAs
+                    store_tiles(1, ra, rb, pa1);
+                    x6_interleave<IM * JN * 6, TAG == 1 ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    fold_t(kt);
+                } else {
+                    fold_t(kt);
+                    if (kt + 1 < nkt) store_tiles(1, ra, rb, pa1);
+                }
                 __syncthreads();
                 if (kt + 1 >= nkt) break;
                 load_a(kt + 3, ra, pa1);
                 load_b(kt + 3, rb);
                 step(1, 0);
-                fold_t(kt + 1);
-                if (kt + 2 < nkt) store_tiles(0, ra2, rb2, pa2);
+                if (DCS_X6_STORE_FIRST) {
+                    store_tiles(0, ra2, rb2, pa2);
+                    x6_interleave<IM * JN * 6, TAG == 1 ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    fold_t(kt + 1);
+                } else {
+                    fold_t(kt + 1);
+                    if (kt + 2 < nkt) store_tiles(0, ra2, rb2, pa2);
+                }
                 __syncthreads();
             }
         } else {
