@@ -118,6 +118,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_SGB
 #define DCS_X6_SGB 5  // bf16x6 residual rows: VALU instructions scheduled after each MFMA (0 = compiler)
 #endif
+#ifndef DCS_WGRAD_SGB
+#define DCS_WGRAD_SGB 5  // bf16x6 weight gradient: VALU instructions scheduled after each MFMA
+#endif
 #ifndef DCS_X6_SGB0
 #define DCS_X6_SGB0 0  // ... the same for the other bf16x6 rows kernels
 #endif
@@ -2063,11 +2066,15 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
 #pragma unroll
         for (int i = 0; i < 2; ++i) rb[i] = buf_load4(rsrc, off + 16 * i);
         pro = (d.pro_act != DCS_ACT_NONE && ok) ? pn * d.Cs + bchan : -1;
+        // next k-tile: at most one row wrap (the dispatch requires Mx >= BKP), as selects so the
+        // tile body stays one basic block
         pqx += BKP;
-        while (pqx >= g.Mx) {
-            pqx -= g.Mx;
-            if (++pqy == g.My) { pqy = 0; ++pn; }
-        }
+        const bool wx = pqx >= g.Mx;
+        pqx -= wx ? g.Mx : 0;
+        pqy += wx ? 1 : 0;
+        const bool wy = pqy == g.My;
+        pqy = wy ? 0 : pqy;
+        pn += wy ? 1 : 0;
     };
     auto store = [&](int buf, const float4 (&ra)[2], const float4 (&rbl)[2], int pro) {
         bf16x8 hi, mid, lo;
@@ -2138,6 +2145,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
                 t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], t[i][j], 0, 0, 0);
                 t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
             }
+        // stage tile kt+1 before the chain fold, unconditionally (past the range: a buffer nobody
+        // reads again), with the split spread over this tile's MFMAs
+        store(cur ^ 1, ora, orb, opro);
+        if constexpr (DCS_WGRAD_SGB > 0) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);  // DS read (transposed fragments)
+#pragma unroll
+            for (int i = 0; i < IM * JN * 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, DCS_WGRAD_SGB, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);  // DS write
+        }
         const long long rel = kt - kt_beg;
         if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
 #pragma unroll
@@ -2149,7 +2168,6 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
                     for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
                 }
         }
-        if (kt + 1 < kt_end) store(cur ^ 1, ora, orb, opro);
         __syncthreads();
     };
     if (kt_beg < kt_end) {
@@ -2266,7 +2284,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
     } else if (d.mma == MMA_BF16X6 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64)) &&
-               d.parity != 1 && DCS_WGRAD_X6) {
+               d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
         if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
