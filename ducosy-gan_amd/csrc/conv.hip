@@ -61,24 +61,44 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
 
 // three-way split for bf16x6: v = hi + mid + lo (each bf16, residuals exact in f32); the six
 // products that matter (all but mid*lo, lo*mid, lo*lo, each <= 2^-27 relative) give ~2^-24
-// relative error per product: fp32-class
+// relative error per product: fp32-class.  Each rounded pair is re-expanded from its packed
+// register (low half << 16, high half & 0xffff0000): one op per value instead of a second
+// single-value conversion plus a shift
+__device__ __forceinline__ floatx8 unpack8(const bf16x8& h) {
+    u32x4v w;
+    __builtin_memcpy(&w, &h, 16);
+    floatx8 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r[2 * q] = __uint_as_float(w[q] << 16);
+        r[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+    return r;
+}
 __device__ __forceinline__ void split8x3(const float4& a, const float4& b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
     const floatx8 f = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     hi = __builtin_convertvector(f, bf16x8);
-    const floatx8 r1 = f - __builtin_convertvector(hi, floatx8);
+    const floatx8 r1 = f - unpack8(hi);
     mid = __builtin_convertvector(r1, bf16x8);
-    const floatx8 r2 = r1 - __builtin_convertvector(mid, floatx8);
+    const floatx8 r2 = r1 - unpack8(mid);
     lo = __builtin_convertvector(r2, bf16x8);
 }
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x4v unpack4(const bf16x4& h) {
+    u32x2v w;
+    __builtin_memcpy(&w, &h, 8);
+    return f32x4v{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u),
+                  __uint_as_float(w[1] << 16), __uint_as_float(w[1] & 0xffff0000u)};
+}
 __device__ __forceinline__ void split4x3(const float4& a, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
     const f32x4v f = {a.x, a.y, a.z, a.w};
     hi = __builtin_convertvector(f, bf16x4);
-    const f32x4v r1 = f - __builtin_convertvector(hi, f32x4v);
+    const f32x4v r1 = f - unpack4(hi);
     mid = __builtin_convertvector(r1, bf16x4);
-    const f32x4v r2 = r1 - __builtin_convertvector(mid, f32x4v);
+    const f32x4v r2 = r1 - unpack4(mid);
     lo = __builtin_convertvector(r2, bf16x4);
 }
 

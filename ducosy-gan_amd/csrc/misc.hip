@@ -98,6 +98,40 @@ __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* _
     }
 }
 
+// per-channel sums for C a power of two <= 256: the tensor is read as flat 1024-float groups
+// (a float4 per thread, coalesced); element 4t+k of a group is channel (4t+k) % C in every group,
+// so each thread keeps 4 running sums and a fixed LDS tree folds them to C values per chunk
+__global__ __launch_bounds__(256) void channel_sum_flat_kernel(const float* __restrict__ x, long long n, int C,
+                                                               long long groups_per_chunk, float* __restrict__ part) {
+    __shared__ float red[1024];
+    const int t = threadIdx.x;
+    const long long g0 = (long long)blockIdx.x * groups_per_chunk;
+    long long g1 = g0 + groups_per_chunk;
+    const long long ng = (n + 1023) / 1024;
+    if (g1 > ng) g1 = ng;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long long g = g0; g < g1; ++g) {
+        const long long i = g * 1024 + 4 * t;
+        float4 v;
+        if (i + 3 < n) {
+            v = *reinterpret_cast<const float4*>(x + i);
+        } else {
+            v.x = i < n ? x[i] : 0.f;
+            v.y = i + 1 < n ? x[i + 1] : 0.f;
+            v.z = i + 2 < n ? x[i + 2] : 0.f;
+            v.w = 0.f;
+        }
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    red[4 * t] = acc.x; red[4 * t + 1] = acc.y; red[4 * t + 2] = acc.z; red[4 * t + 3] = acc.w;
+    __syncthreads();
+    for (int stride = 512; stride >= C; stride >>= 1) {
+        for (int i = t; i < stride; i += 256) red[i] += red[i + stride];
+        __syncthreads();
+    }
+    if (t < C) part[(long long)blockIdx.x * C + t] = red[t];
+}
+
 // one wave per channel: lane l sums chunks l, l+64, ... in order, then a fixed butterfly
 __global__ __launch_bounds__(64) void channel_sum_final_kernel(const float* __restrict__ part, int C, int nchunk,
                                                                float* __restrict__ out) {
@@ -148,8 +182,20 @@ extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, voi
     if (ws_bytes < dcs_channel_sum_workspace_size(P, C)) return fail(DCS_E_WORKSPACE, "channel_sum: workspace too small");
     int nch = csum_chunks(P);
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(channel_sum_partial_kernel, dim3((unsigned)cdiv(C, 256), nch), dim3(256), 0, s, x,
-                       (long long)P, C, nch, reinterpret_cast<float*>(ws));
+    const long long n = (long long)P * C;
+    if (C <= 256 && (C & (C - 1)) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        // flat pass: chunks of whole 1024-float groups, at most csum_chunks(P) of them
+        const long long ng = cdiv(n, 1024);
+        long long want = cdiv(ng, 4);
+        if (want > nch) want = nch;
+        const long long gpc = cdiv(ng, want);
+        nch = (int)cdiv(ng, gpc);
+        hipLaunchKernelGGL(channel_sum_flat_kernel, dim3((unsigned)nch), dim3(256), 0, s, x, n, C, gpc,
+                           reinterpret_cast<float*>(ws));
+    } else {
+        hipLaunchKernelGGL(channel_sum_partial_kernel, dim3((unsigned)cdiv(C, 256), nch), dim3(256), 0, s, x,
+                           (long long)P, C, nch, reinterpret_cast<float*>(ws));
+    }
     int e = check_launch("channel_sum_partial");
     if (e) return e;
     hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)C), dim3(64), 0, s,

@@ -349,3 +349,14 @@ def test_forward_in_stats_matches_stats_pass(ops, mode, case):
     from modules.hip import lib
     d = g._desc_fwd(Src.nhwc(x), wp.shape[1], p[2] if p else 0, 0)
     assert lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d)) > 0
+
+
+@pytest.mark.parametrize("P,C", [(1, 1), (1000, 1), (512 * 512 * 2 + 3, 1), (4097, 3), (33 * 33, 64),
+                                 (256 * 256, 64), (70, 256), (5000, 512)])
+def test_channel_sum(ops, P, C):
+    """Bias gradients (sum over pixels per channel), both the flat power-of-two pass and the
+    per-channel one, against a float64 sum; ragged tails included."""
+    x = rnd((P, C), 17, f"cs{P}_{C}").to(DEV)
+    got = ops.channel_sum(x)
+    ref = x.double().sum(0)
+    assert float((got.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(x.abs().sum(0).max()))
