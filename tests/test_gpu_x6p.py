@@ -1,9 +1,9 @@
 """The pre-split LDS-DMA bf16x6 residual conv (csrc/conv_x6p.hip) against the split-in-the-gather
 bf16x6 rows kernel of conv.hip and against float64.
 
-Both kernels issue the same six bf16 products per operand pair in the same order into the same
-two-level fp32 chains (inner chains of 128 k), from the same hi/mid/lo split: their outputs
-must be bit-identical.  Cases: the forward (reflection padding 1) and the stride-1 data
+Both kernels issue the same six bf16 products per operand pair into two-level fp32 chains
+(inner chains of 128 k) from the same hi/mid/lo split; the rows kernel walks K in 16-channel
+slices, so the two are compared through their error against float64.  Cases: the forward (reflection padding 1) and the stride-1 data
 gradient (zero padding 2 onto the padded grid), a pixel count that is not a multiple of the
 128-row tile, and more than one image.
 """
@@ -40,7 +40,11 @@ def _run(x6p, fn):
 
 
 @pytest.mark.parametrize("n,h", [(2, 16), (3, 13), (1, 32)])
-def test_x6p_forward_and_dgrad_bit_exact(n, h):
+def test_x6p_forward_and_dgrad_vs_float64(n, h):
+    """The x6p pass (tap-major K order) and conv.hip's bf16x6 rows kernel (which walks its K in
+    16-channel slices, so its chains hold different terms) against a float64 forward and data
+    gradient: the x6p error stays within 1.5x of the rows kernel's (the fp32-class bar of
+    tests/test_gpu_mma.py)."""
     from modules.hip import ops
     g = _res()
     x = torch.from_numpy(prng.normal(61, f"x{n}{h}", (n, h, h, 256))).float().to(DEV)
@@ -53,15 +57,19 @@ def test_x6p_forward_and_dgrad_bit_exact(n, h):
     assert lib.query("dcs_conv_rows_x6p_ok", ctypes.byref(d)) == 1
     f_new = _run(True, lambda: g.forward(ops.Src.nhwc(x), g.pack_fwd(w)))
     f_old = _run(False, lambda: g.forward(ops.Src.nhwc(x), g.pack_fwd(w)))
-    assert torch.equal(f_new, f_old), float((f_new - f_old).abs().max())
     b_new = _run(True, lambda: g.dgrad(dy, g.pack_dgrad(w), h, h))
     b_old = _run(False, lambda: g.dgrad(dy, g.pack_dgrad(w), h, h))
-    assert torch.equal(b_new, b_old), float((b_new - b_old).abs().max())
-    # and against float64 (reflect pad + conv), at the fp32-class bar of tests/test_gpu_mma.py
-    xd = x.double().permute(0, 3, 1, 2)
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
     ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xd, (1, 1, 1, 1), mode="reflect"), w.double())
-    err = float((f_new.double().permute(0, 3, 1, 2) - ref).abs().max() / ref.abs().max())
-    assert err < 2e-6, err
+    ref.backward(dy.double().permute(0, 3, 1, 2))
+    gref = xd.grad
+
+    def err(a, r):
+        return float((a.double().permute(0, 3, 1, 2) - r).abs().max() / r.abs().max())
+
+    for new, old, r in ((f_new, f_old, ref.detach()), (b_new, b_old, gref)):
+        e_new, e_old = err(new, r), err(old, r)
+        assert e_new < 2e-6 and e_new <= 1.5 * e_old + 1e-7, (e_new, e_old)
 
 
 def test_split_x6_planes():
