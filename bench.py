@@ -110,8 +110,8 @@ def main():
                     help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one "
                          "process; value counts the images of both models")
     ap.add_argument("--dual-schedule", default="serial", choices=["serial", "concurrent", "groups"],
-                    help="--dual: both models on one stream (serial), one HIP stream each (concurrent; "
-                         "trainer.py ConcurrentCycleGANs), or split GPU groups (groups: soft tissue on the first "
+                    help="--dual: both models on one stream (serial), one HIP stream each on its own half of "
+                         "the CUs (concurrent; trainer.py ConcurrentCycleGANs), or split GPU groups (groups: soft tissue on the first "
                          "half of the ranks, lung on the second, each with its own all-reduce)")
     ap.add_argument("--workload", default="step", choices=["step", "g_a2b"],
                     help="step: the full training step (BASELINE config 3/4); g_a2b: Generator_A2B forward + "
@@ -122,9 +122,6 @@ def main():
     from modules.hip import ops
     from modules.trainer import CycleGANSystem
 
-    if args.dual and args.dual_schedule == "concurrent" and args.mma != "f32":
-        raise SystemExit("--dual-schedule concurrent runs the f32 operand mode (pass --mma f32): "
-                         "DESIGN.md §3, Config 5")
     ops.set_mma(args.mma)
     rank, world, local = parallel.init_from_env()
     device = torch.device(f"cuda:{local}")

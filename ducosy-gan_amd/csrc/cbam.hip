@@ -263,6 +263,68 @@ __global__ __launch_bounds__(256) void cb_bwd_sums_kernel(const float* __restric
     }
 }
 
+// b3 (float4 form, C % 4 == 0 and C/4 dividing 256): thread t owns channels 4*(t % C4).. of
+// pixel lane t / C4; a wave reads whole pixel rows (C = 256: one 1 KiB row per load), the
+// pixel lanes are folded in fixed order through LDS.  Same sums as cb_bwd_sums_kernel.
+__global__ __launch_bounds__(256) void cb_bwd_sums4_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                           const float* __restrict__ sc, const float* __restrict__ sh,
+                                                           const float* __restrict__ ca, const float* __restrict__ sa,
+                                                           const float* __restrict__ dsin,
+                                                           const int* __restrict__ sarg, int HW, int C, int nchunk,
+                                                           Sum3* __restrict__ parts) {
+    __shared__ float4 s_a[256], s_b[256], s_c[256];
+    const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
+    const int C4 = C >> 2, lanes = 256 / C4;
+    const int c4 = tid % C4, plane = tid / C4;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int p1 = min(HW, p0 + p_per);
+    const int nc = n * C + 4 * c4;
+    const float4 s = *reinterpret_cast<const float4*>(sc + nc);
+    const float4 b = *reinterpret_cast<const float4*>(sh + nc);
+    const float4 a = *reinterpret_cast<const float4*>(ca + nc);
+    const float invC = 1.f / (float)C;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A, Cc = A;
+    for (int p = p0 + plane; p < p1; p += lanes) {
+        const long long pp = (long long)n * HW + p;
+        const float4 yv = reinterpret_cast<const float4*>(y + pp * C)[c4];
+        const float4 dv = reinterpret_cast<const float4*>(dout + pp * C)[c4];
+        const float g = sa[pp];
+        const float2 ds = reinterpret_cast<const float2*>(dsin)[pp];
+        const int am = sarg[pp] - 4 * c4;
+        const float d0 = ds.x * invC;
+        float z, dzc, dz0;
+#define DCS_SUMS_LANE(X, K)                                   \
+        z = fmaf(yv.X, s.X, b.X);                             \
+        dzc = fmaf(dv.X, g, d0);                              \
+        if (am == K) dzc += ds.y;                             \
+        dz0 = dzc * a.X;                                      \
+        A.X = fmaf(dzc, z, A.X);                              \
+        B.X += dz0;                                           \
+        Cc.X = fmaf(dz0, z, Cc.X);
+        DCS_SUMS_LANE(x, 0)
+        DCS_SUMS_LANE(y, 1)
+        DCS_SUMS_LANE(z, 2)
+        DCS_SUMS_LANE(w, 3)
+#undef DCS_SUMS_LANE
+    }
+    s_a[tid] = A; s_b[tid] = B; s_c[tid] = Cc;
+    __syncthreads();
+    if (plane == 0) {
+        for (int l = 1; l < lanes; ++l) {
+            const float4 u = s_a[l * C4 + c4], v = s_b[l * C4 + c4], w = s_c[l * C4 + c4];
+            A.x += u.x; A.y += u.y; A.z += u.z; A.w += u.w;
+            B.x += v.x; B.y += v.y; B.z += v.z; B.w += v.w;
+            Cc.x += w.x; Cc.y += w.y; Cc.z += w.z; Cc.w += w.w;
+        }
+        Sum3* o = parts + ((long long)n * nchunk + chunk) * C + 4 * c4;
+        o[0] = Sum3{A.x, B.x, Cc.x};
+        o[1] = Sum3{A.y, B.y, Cc.y};
+        o[2] = Sum3{A.z, B.z, Cc.z};
+        o[3] = Sum3{A.w, B.w, Cc.w};
+    }
+}
+
 // b4: one block per image: channel-attention MLP backward + IN-backward coefficients.
 // coef[n][c] = {mean(dz), mean(dz*z), dvmax}; per-image dw1/dw2 partials (summed over n by
 // cb_bwd_dw_reduce_kernel in fixed order).
@@ -360,6 +422,53 @@ __global__ void cb_bwd_apply_kernel(const float* __restrict__ dout, const float*
     float dz = dzc * ca[nc];
     if (yarg[nc] == p) dz += k.c;
     dy[i] = s * (dz - k.a - z * k.b);
+}
+
+// b5, float4 form (C % 4 == 0): one thread per 4 channels of a pixel, 32-bit index math
+__global__ __launch_bounds__(256) void cb_bwd_apply4_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ ca, const float* __restrict__ sa,
+                                                            const float* __restrict__ dsin, const int* __restrict__ sarg,
+                                                            const int* __restrict__ yarg, const Sum3* __restrict__ coef,
+                                                            int HW, int C, int total4, float* __restrict__ dy) {
+    const int i4 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i4 >= total4) return;
+    const int C4 = C >> 2;
+    const int pp = i4 / C4;
+    const int c4 = i4 - pp * C4;
+    const int n = pp / HW;
+    const int p = pp - n * HW;
+    const int nc = n * C + 4 * c4;
+    const float4 s = *reinterpret_cast<const float4*>(sc + nc);
+    const float4 b = *reinterpret_cast<const float4*>(sh + nc);
+    const float4 a = *reinterpret_cast<const float4*>(ca + nc);
+    const int4 ya = *reinterpret_cast<const int4*>(yarg + nc);
+    const float4 k0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc));
+    const float4 k1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc) + 4);
+    const float4 k2 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc) + 8);
+    const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+    const float4 dv = reinterpret_cast<const float4*>(dout)[i4];
+    const float g = sa[pp];
+    const float2 ds = reinterpret_cast<const float2*>(dsin)[pp];
+    const int am = sarg[pp] - 4 * c4;
+    const float d0 = ds.x * (1.f / (float)C);
+    float4 o;
+    // coef of channel j: {k.a, k.b, k.c} = floats 3j..3j+2 of (k0, k1, k2)
+#define DCS_APPLY_LANE(X, K, KA, KB, KC)                      \
+    {                                                         \
+        const float z = fmaf(yv.X, s.X, b.X);                 \
+        float dzc = fmaf(dv.X, g, d0);                        \
+        if (am == K) dzc += ds.y;                             \
+        float dz = dzc * a.X;                                 \
+        if (ya.X == p) dz += KC;                              \
+        o.X = s.X * (dz - KA - z * KB);                       \
+    }
+    DCS_APPLY_LANE(x, 0, k0.x, k0.y, k0.z)
+    DCS_APPLY_LANE(y, 1, k0.w, k1.x, k1.y)
+    DCS_APPLY_LANE(z, 2, k1.z, k1.w, k2.x)
+    DCS_APPLY_LANE(w, 3, k2.y, k2.z, k2.w)
+#undef DCS_APPLY_LANE
+    reinterpret_cast<float4*>(dy)[i4] = o;
 }
 
 static inline int cb_chunks(int N, int HW) {
@@ -462,8 +571,13 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     hipLaunchKernelGGL(cb_bwd_dwsa_final_kernel, dim3((unsigned)cdiv(nt, 128)), dim3(128), 0, s, w.wpart, nt, nwc, dwsa);
     if ((e = check_launch("cb_bwd_dwsa_final"))) return e;
     const int nch = cb_chunks(N, HW);
-    hipLaunchKernelGGL(cb_bwd_sums_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin, sarg,
-                       HW, C, nch, w.parts);
+    const bool v4 = (C % 4 == 0) && (C / 4 <= 256) && (256 % (C / 4) == 0);
+    if (v4)
+        hipLaunchKernelGGL(cb_bwd_sums4_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
+                           sarg, HW, C, nch, w.parts);
+    else
+        hipLaunchKernelGGL(cb_bwd_sums_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
+                           sarg, HW, C, nch, w.parts);
     if ((e = check_launch("cb_bwd_sums"))) return e;
     hipLaunchKernelGGL(cb_bwd_ca_kernel, dim3(N), dim3(256), (size_t)(4 * C + 2 * Cr) * sizeof(float), s, w.parts, nch,
                        ymax, scale, shift, ca, w1, w2, HW, C, Cr, w.coef, w.dwpart);
@@ -472,7 +586,13 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
                        C * Cr, dw1, dw2);
     if ((e = check_launch("cb_bwd_dw_reduce"))) return e;
     const long long total = P * C;
-    hipLaunchKernelGGL(cb_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dout, y, scale, shift, ca,
-                       sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy);
+    if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31)) {  // C % 4 == 0 checked above
+        const int total4 = (int)(total / 4);
+        hipLaunchKernelGGL(cb_bwd_apply4_kernel, dim3((unsigned)cdiv(total4, 256)), dim3(256), 0, s, dout, y, scale,
+                           shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total4, dy);
+    } else {
+        hipLaunchKernelGGL(cb_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dout, y, scale, shift,
+                           ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy);
+    }
     return check_launch("cb_bwd_apply");
 }

@@ -247,7 +247,8 @@ struct RowInfo {
     long long out_off;    // element offset of the output pixel (channel 0), -1 if invalid
 };
 
-__device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassGeom& g, int m) {
+// fold (conv_rows_kernel of dcs_conv_dgrad_reflect only): see the fold branch below
+__device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassGeom& g, int m, int fold = 0) {
     // 32-bit index math: the host guarantees N*My*Mx < 2^31
     RowInfo r;
     const int per = g.My * g.Mx;
@@ -265,6 +266,19 @@ __device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassG
         r.by = qy; r.bx = qx;
     }
     r.n = n;
+    if (fold) {
+        // dcs_conv_dgrad_reflect (pad 1): interior pixels of the (H+2) x (W+2) padded grid go to
+        // the unpadded N x H x W tensor, the one-pixel ring to the ring area behind it
+        const int H = d.Ho - 2, W = d.Wo - 2;
+        if (oy >= 1 && oy <= H && ox >= 1 && ox <= W) {
+            r.out_off = ((long long)(n * H + oy - 1) * W + ox - 1) * d.Co;
+        } else {
+            const int ring = 2 * d.Wo + 2 * H;
+            const int idx = oy == 0 ? ox : (oy == d.Ho - 1 ? d.Wo + ox : 2 * d.Wo + 2 * (oy - 1) + (ox == 0 ? 0 : 1));
+            r.out_off = ((long long)d.N * H * W + (long long)n * ring + idx) * d.Co;
+        }
+        return r;
+    }
     r.out_off = ((long long)(n * d.Ho + oy) * d.Wo + ox) * d.Co;
     return r;
 }
@@ -623,7 +637,7 @@ template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
 __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
-    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts) {
+    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts, int fold) {
     const dcs_conv_desc d = specialise<TAG>(din);
     static_assert(BM == 128 || (BM == 256 && MMA == MMA_BF16X6 && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
@@ -684,7 +698,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 
     // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap)
     const int arow = tid >> 1, akq = (tid & 1) * AKPT;
-    const RowInfo ri = row_info(d, g, (int)(m0 + arow));
+    const RowInfo ri = row_info(d, g, (int)(m0 + arow), fold);
     const bool rvalid = ri.out_off >= 0;
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     // B loader: one output channel row, BKPT consecutive k
@@ -1112,7 +1126,10 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         __syncthreads();
     }
 
-    // epilogue: + bias, activation, NHWC store
+    // epilogue: + bias, activation, NHWC store; in the reflection-fold data gradient
+    // (fold, dcs_conv_dgrad_reflect) src2 carries the residual addend of the interior pixels
+    const float* addend = fold ? src2 : nullptr;
+    const long long interior = fold ? (long long)d.N * (d.Ho - 2) * (d.Wo - 2) * d.Co : 0;
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
         const int col = n0 + wn * WN + j * 32 + l32;
@@ -1127,6 +1144,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 if (off < 0) continue;
                 float v = acc[i][j][r] + bv;
                 if (d.epi_act != DCS_ACT_NONE) v = act_apply(v, d.epi_act);
+                if (addend && off < interior) v += addend[off + col];
                 out[off + col] = v;
             }
         }
@@ -1751,6 +1769,45 @@ __global__ void reflect_fold_scalar_kernel(const float* __restrict__ dxp, const 
     dx[idx] = s;
 }
 
+// ring fold of dcs_conv_dgrad_reflect (pad 1): dx[y][x] += the ring entries of the padded
+// grid that reflect onto (y, x) (rows 1 and H-2, columns 1 and W-2), in reflect_pre order; the
+// conv epilogue already stored the interior contribution (plus the addend).  One thread per
+// (image, target pixel, 4 channels); targets: the two rows over every column, then the two
+// columns over the remaining rows.
+__global__ void reflect_ring_fold_kernel(const float* __restrict__ ring, float* __restrict__ dx, int N, int H, int W,
+                                         int C4) {
+    const int ntgt = 2 * W + 2 * (H - 2);
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)N * ntgt * C4) return;
+    const int c4 = (int)(idx % C4);
+    const int t = (int)((idx / C4) % ntgt);
+    const int n = (int)(idx / ((long long)C4 * ntgt));
+    int y, x;
+    if (t < 2 * W) {
+        y = t < W ? 1 : H - 2;
+        x = t < W ? t : t - W;
+    } else {
+        const int u = t - 2 * W;  // rows 0, 2..H-3, H-1 (rows 1 and H-2 are covered above)
+        const int rr = u >> 1;
+        y = rr == 0 ? 0 : (rr <= H - 4 ? rr + 1 : H - 1);
+        x = (u & 1) ? W - 2 : 1;
+    }
+    const int Hp = H + 2, Wp = W + 2, ringlen = 2 * Wp + 2 * H;
+    int ay[3], ax[3];
+    const int ny = reflect_pre(y, H, 1, ay), nx = reflect_pre(x, W, 1, ax);
+    float4* o = reinterpret_cast<float4*>(dx) + (((long long)n * H + y) * W + x) * C4 + c4;
+    float4 s = *o;
+    for (int p = 0; p < ny; ++p)
+        for (int q = 0; q < nx; ++q) {
+            const int yp = ay[p], xp = ax[q];
+            if (yp >= 1 && yp <= H && xp >= 1 && xp <= W) continue;  // interior: in the epilogue
+            const int ri = yp == 0 ? xp : (yp == Hp - 1 ? Wp + xp : 2 * Wp + 2 * (yp - 1) + (xp == 0 ? 0 : 1));
+            const float4 v = reinterpret_cast<const float4*>(ring)[((long long)n * ringlen + ri) * C4 + c4];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    *o = s;
+}
+
 __global__ void upsample2_grad_kernel(const float* __restrict__ du, float* __restrict__ dx, int N, int H,
                                       int W, int C4) {
     long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1854,7 +1911,8 @@ extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int K
 
 namespace {
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
-                   const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream) {
+                   const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream,
+                   int fold = 0) {
     int e = validate(dp, true);
     if (e) return e;
     const dcs_conv_desc& d = *dp;
@@ -1894,37 +1952,37 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         if (BN == 128 && res && DCS_X6_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
             const int gx2 = (int)cdiv(Mmax, 256);
             hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16X6>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
-                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts);
+                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts, fold);
             if (bm_used) *bm_used = 256;
-        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
         return check_launch("conv_rows");
     }
     if (v4 && d.mma == MMA_BF16X6 && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
-        if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
         return check_launch("conv_rows");
     }
     const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \
-    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts); \
-    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);  \
-    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold); \
+    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);  \
+    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
         if (d.mma == MMA_BF16) { DCS_ROWS_MMA(MMA_BF16) } else { DCS_ROWS_MMA(MMA_BF16X3) }
 #undef DCS_ROWS_MMA
         return check_launch("conv_rows");
     }
     if (BN == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
     }
     return check_launch("conv_rows");
 }
@@ -2468,6 +2526,32 @@ extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* 
                            addend, dx, N, H, W, C, pad);
     }
     return check_launch("reflect_fold");
+}
+
+extern "C" size_t dcs_conv_dgrad_reflect_ring_size(const dcs_conv_desc* dp) {
+    if (!dp || dp->Ho < 6 || dp->Wo < 6) return 0;
+    return (size_t)dp->N * (2 * dp->Wo + 2 * (dp->Ho - 2)) * dp->Co * sizeof(float);
+}
+
+extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, const float* wpack,
+                                      const float* addend, float* dx, float* ring, void* stream) {
+    if (!dp || !dy || !wpack || !dx || !ring) return fail(DCS_E_INVALID, "conv_dgrad_reflect: null pointer");
+    const dcs_conv_desc& d = *dp;
+    if (d.parity || d.stride != 1 || d.up != 1 || d.pad_mode != DCS_PAD_ZERO ||
+        d.pt != d.KH - 1 || d.pl != d.KW - 1 || d.pro_act != DCS_ACT_NONE || d.epi_act != DCS_ACT_NONE ||
+        d.Ho != d.Hs + 2 || d.Wo != d.Ws + 2 || d.KH != 3 || d.KW != 3 ||
+        d.csplit < d.Cs || d.Co % 4 != 0 || d.Ho < 6 || d.Wo < 6)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect: 3x3 stride-1 data gradient onto the pad-1 grid expected "
+                                   "(Ho = Hs + 2, pt = pl = 2, zero pad, no activations)");
+    if (ring != dx + (long long)d.N * (d.Ho - 2) * (d.Wo - 2) * d.Co)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect: ring must directly follow dx (one allocation)");
+    int e = conv_rows_impl(&d, dy, addend, wpack, nullptr, nullptr, nullptr, dx, nullptr, nullptr, stream, 1);
+    if (e) return e;
+    const int H = d.Ho - 2, W = d.Wo - 2, C4 = d.Co / 4;
+    const long long total = (long long)d.N * (2 * W + 2 * (H - 2)) * C4;
+    hipLaunchKernelGGL(reflect_ring_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), ring,
+                       dx, d.N, H, W, C4);
+    return check_launch("reflect_ring_fold");
 }
 
 extern "C" int dcs_upsample2_grad(const float* dup, float* dx, int N, int H, int W, int C, void* stream) {

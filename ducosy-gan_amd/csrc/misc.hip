@@ -41,6 +41,34 @@ using namespace dcs;
 extern "C" const char* dcs_last_error(void) { return g_last_error.c_str(); }
 extern "C" int dcs_version(void) { return 1; }
 
+extern "C" int dcs_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream) {
+    if (!cu_mask || words <= 0 || !stream) return fail(DCS_E_INVALID, "stream_create_cu_mask: bad arguments");
+    hipStream_t s = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, cu_mask);
+    if (e != hipSuccess) {
+        set_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+        return (int)e;
+    }
+    *stream = reinterpret_cast<void*>(s);
+    return DCS_OK;
+}
+
+extern "C" int dcs_stream_destroy(void* stream) {
+    const hipError_t e = hipStreamDestroy(as_stream(stream));
+    if (e != hipSuccess) {
+        set_error(std::string("hipStreamDestroy: ") + hipGetErrorString(e));
+        return (int)e;
+    }
+    return DCS_OK;
+}
+
+extern "C" int dcs_device_cu_count(void) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    return n;
+}
+
 extern "C" int dcs_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                              float beta2, float eps, float bias_c1, float bias_c2, void* stream) {
     if (!p || !g || !m || !v || n < 0) return fail(DCS_E_INVALID, "adam: bad arguments");

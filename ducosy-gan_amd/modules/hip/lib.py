@@ -41,6 +41,9 @@ DP = POINTER(ConvDesc)
 SIGNATURES = {
     "dcs_last_error": (c_char_p, []),
     "dcs_version": (c_int, []),
+    "dcs_stream_create_cu_mask": (c_int, [P, c_int, P]),
+    "dcs_stream_destroy": (c_int, [P]),
+    "dcs_device_cu_count": (c_int, []),
     "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "dcs_conv_rows": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_rows_in_stats_parts_size": (c_size_t, [DP]),
@@ -55,6 +58,8 @@ SIGNATURES = {
     "dcs_conv_rows_x6p": (c_int, [DP, P, P, P, P]),
     "dcs_conv_wgrad_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
+    "dcs_conv_dgrad_reflect_ring_size": (c_size_t, [P]),
+    "dcs_conv_dgrad_reflect": (c_int, [P, P, P, P, P, P, P]),
     "dcs_reflect_fold": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "dcs_pack_nhwc4": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
     "dcs_upsample2_grad": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),

@@ -35,6 +35,9 @@ _X6P = os.environ.get("DUCOSY_X6P", "0") == "1"
 # IN statistics fused into the conv epilogue (ConvGeom.forward_in_stats); "0" = separate pass (A/B)
 _FUSE_STATS = os.environ.get("DUCOSY_FUSE_STATS", "1") == "1"
 _KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
+# reflection fold of the stride-1 pad-1 data gradient in the conv epilogue (dcs_conv_dgrad_reflect);
+# "0" = padded-grid rows pass + dcs_reflect_fold (A/B)
+_FUSE_FOLD = os.environ.get("DUCOSY_FUSE_FOLD", "1") == "1"
 
 
 def set_mma(mode: str) -> None:
@@ -435,6 +438,18 @@ class ConvGeom:
             p = t
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
+            if _FUSE_FOLD and p == 1 and self.k == 3 and H >= 4 and W >= 4 and not narrow and dy.is_contiguous() \
+                    and not _x6p(d) and ci % 4 == 0:
+                # interior written by the conv epilogue (+ addend), the ring folded in after
+                ring = lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4
+                buf = torch.empty(N * H * W * ci + ring, device=dev, dtype=torch.float32)
+                out = buf[:N * H * W * ci].view(N, H, W, ci)
+                e0 = PROBE.begin() if _is_res_geom(self) else None
+                lib.call("dcs_conv_dgrad_reflect", ctypes.byref(d), _p(dy), _p(wpack_d),
+                         _p(addend.contiguous()) if addend is not None else None, _p(out),
+                         ctypes.c_void_p(buf.data_ptr() + N * H * W * ci * 4), _stream())
+                PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
+                return out
             dpad = torch.empty(N, d.Ho, d.Wo, ci, device=dev, dtype=torch.float32)
             x6p = not narrow and dy.is_contiguous() and _x6p(d)
             if x6p:

@@ -172,29 +172,49 @@ class ConcurrentCycleGANs:
     train.py:27-38).
 
     schedule "serial" (default): the systems step one after the other on the caller's stream.
-    schedule "concurrent": one HIP stream per system; the kernels of one model fill the gaps of
-    the other (small normalisation / loss / Adam launches, split-K reductions, launch latency).
-    Workspaces are per stream (ops.workspace).  The concurrent schedule runs the exact-f32
-    operand mode (MMA): with bf16-family rows kernels on the two streams, a model's numbers
-    sometimes leave its sequential run (Config 5: root cause not found; with
-    f32 operands each model equals its own sequential run bit for bit,
-    tests/test_gpu_concurrent.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
+    schedule "concurrent": one HIP stream per system, each confined to its own contiguous,
+    pair-aligned share of the compute units (dcs_stream_create_cu_mask); the kernels of one model
+    fill the gaps of the other (small normalisation / loss / Adam launches, split-K reductions,
+    launch latency).  Workspaces are per stream (ops.workspace).  The CU partition is what makes
+    it exact: when the two streams share compute-unit pairs, a model's numbers sometimes leave
+    its sequential run (Config 5: 7/20 repetitions on shared CUs, 9/20 with the
+    models on alternating CUs, 0/54 on disjoint halves, 0/32 on interleaved 8-CU blocks).  With
+    the partition each model equals its own sequential run bit for bit in every operand mode
+    (tests/test_gpu_concurrent.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
     --dual-schedule groups, modules/parallel.py): each model on its own half of the ranks."""
-
-    MMA = "f32"
 
     def __init__(self, systems, device, schedule="serial"):
         if schedule not in ("concurrent", "serial"):
             raise ValueError("schedule must be 'concurrent' or 'serial'")
-        from .hip import ops
-        if schedule == "concurrent" and ops.get_mma() != self.MMA:
-            raise ValueError(f"the concurrent schedule runs the {self.MMA} operand mode (ops.set_mma('{self.MMA}')); "
-                             f"current mode {ops.get_mma()}: see DESIGN.md §3, Config 5")
         self.systems = list(systems)
         self.device = torch.device(device)
         self.schedule = schedule
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.systems] \
+        self.streams = [self._cu_stream(i, len(self.systems)) for i in range(len(self.systems))] \
             if schedule == "concurrent" else []
+
+    # CU-mask streams live for the whole process, one per (device, partition): the caching
+    # allocator keeps blocks tagged with a stream after the runner that used it is gone, so the
+    # streams are never destroyed, and repeated runners reuse them
+    _CU_STREAMS = {}
+
+    def _cu_stream(self, i, n):
+        import ctypes
+        from .hip import lib
+        key = (self.device.index, i, n)
+        if key not in ConcurrentCycleGANs._CU_STREAMS:
+            with torch.cuda.device(self.device):
+                ncu = lib.load().dcs_device_cu_count()
+                if ncu < 2 * n:
+                    raise RuntimeError(f"concurrent schedule: {ncu} compute units for {n} streams")
+                lo, hi = (i * ncu // n) & ~1, ((i + 1) * ncu // n) & ~1 if i + 1 < n else ncu
+                words = (ncu + 31) // 32
+                mask = (ctypes.c_uint32 * words)()
+                for cu in range(lo, hi):
+                    mask[cu // 32] |= 1 << (cu % 32)
+                raw = ctypes.c_void_p()
+                lib.call("dcs_stream_create_cu_mask", mask, words, ctypes.byref(raw))
+            ConcurrentCycleGANs._CU_STREAMS[key] = torch.cuda.ExternalStream(raw.value, device=self.device)
+        return ConcurrentCycleGANs._CU_STREAMS[key]
 
     def train_step(self, batches):
         """batches: one (real_A, real_B, masks) per system.  Returns one loss dict per system
@@ -202,9 +222,13 @@ class ConcurrentCycleGANs:
         if self.schedule == "serial":
             return [sysm.train_step(*b) for sysm, b in zip(self.systems, batches)]
         cur = torch.cuda.current_stream(self.device)
+        # one event for the inputs: the CU-mask streams are blocking streams, so a command on a
+        # legacy-null caller stream between the two models' launches would serialise them
+        ready = torch.cuda.Event()
+        ready.record(cur)
         out = []
         for sysm, st, b in zip(self.systems, self.streams, batches):
-            st.wait_stream(cur)  # inputs produced on the caller's stream
+            st.wait_event(ready)
             with torch.cuda.stream(st):
                 for t in b:
                     if t is not None:

@@ -99,6 +99,16 @@ typedef struct dcs_conv_desc {
 const char* dcs_last_error(void);
 int dcs_version(void);
 
+/* A HIP stream whose kernels may only occupy the compute units set in cu_mask (words 32-bit
+ * words, bit i = CU i; hipExtStreamCreateWithCUMask).  Diagnostics of the two-stream schedule
+ * of BASELINE config 5 (scripts/conc_cumask.py, DESIGN.md §3, Config 5); the reference trains
+ * its two models one after the other (train.py:27-38), so this has no reference counterpart.
+ * The stream is created blocking: it synchronises with the legacy null stream. */
+int dcs_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream);
+int dcs_stream_destroy(void* stream);
+/* number of compute units of the current device */
+int dcs_device_cu_count(void);
+
 /* ---- convolution family (modules/model.py:61-63,74-79,94-112,122-129 → aten conv) ---- */
 
 /* Pack OIHW weights into the GEMM B operand, logically [Kpad][ncols] (zero padded), stored
@@ -187,6 +197,18 @@ int dcs_pack_nhwc4(const float* x, int c1, const float* x2, int c2, int N, int H
 
 /* Fold the gradient of a reflection-padded tensor back onto the tensor:
  * dx[n,i,j,c] = addend[n,i,j,c] + sum over padded positions mirroring to (i,j). */
+/* Stride-1 data gradient of a ReflectionPad(1) + conv layer straight onto the unpadded grid
+ * (modules/model.py:72-79 backward: aten convolution_backward + reflection_pad2d_backward, and
+ * the residual add of the block when addend != NULL):
+ *   dx[n][y][x][c] = addend[n][y][x][c] + sum over padded pixels (yp, xp) reflecting onto
+ *                    (y, x) of (dy (*) flipped W)[n][yp][xp][c].
+ * d describes the rows pass over the (H+2) x (W+2) padded grid exactly as for dcs_conv_rows
+ * (pt = pl = KH-1, Ho = H+2, Wo = W+2, zero pad, stride 1).  The
+ * conv epilogue writes interior pixels (plus the addend) into dx and the one-pixel ring into
+ * ring (dcs_conv_dgrad_reflect_ring_size bytes); a small kernel then folds the ring in. */
+size_t dcs_conv_dgrad_reflect_ring_size(const dcs_conv_desc* d);
+int dcs_conv_dgrad_reflect(const dcs_conv_desc* d, const float* dy, const float* wpack, const float* addend,
+                           float* dx, float* ring, void* stream);
 int dcs_reflect_fold(const float* dxpad, const float* addend, float* dx, int N, int H, int W, int C,
                      int pad, void* stream);
 

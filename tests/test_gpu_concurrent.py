@@ -19,46 +19,40 @@ def _batch(seed, i, n, hw, cin):
     return rA, rB, mk
 
 
-def test_concurrent_schedule_refuses_bf16_modes():
-    """The two-stream schedule runs exact-f32 operands (Config 5)."""
-    from modules.hip import ops
-    from modules.trainer import ConcurrentCycleGANs
-    prev = ops.get_mma()
-    ops.set_mma("bf16x6")
-    try:
-        with pytest.raises(ValueError, match="f32"):
-            ConcurrentCycleGANs([], DEV, schedule="concurrent")
-        ConcurrentCycleGANs([], DEV, schedule="serial")  # the serial schedule runs every mode
-    finally:
-        ops.set_mma(prev)
-
-
-@pytest.mark.parametrize("mode", ["f32"])
-def test_concurrent_equals_sequential(mode):
+# fresh repetitions of the concurrent run: with the two streams sharing compute-unit pairs, 6-45 %
+# of such repetitions left the sequential numbers in bf16x6 (scripts/conc_cumask.py,
+# profiles/r02e_hazard_cumask.md); the CU-partitioned streams of ConcurrentCycleGANs never did
+@pytest.mark.parametrize("mode,reps", [("f32", 1), ("bf16x6", 6)])
+def test_concurrent_equals_sequential(mode, reps):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
     n, hw, nb, steps = 2, 64, 2, 3
     cfg = [(3, 801), (2, 802)]
     prev = ops.get_mma()
     ops.set_mma(mode)
+    side = torch.cuda.Stream()  # the caller's stream: the legacy null stream stays idle
     try:
-        seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
-        want = [[{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)]
-                for m, (c, s) in zip(seq, cfg)]
-        run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV,
-                                  schedule="concurrent")
-        got = [[], []]
-        for i in range(steps):
-            outs = run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])
-            torch.cuda.synchronize()
-            for j, o in enumerate(outs):
-                got[j].append({k: float(v) for k, v in o.items()})
+        with torch.cuda.stream(side):
+            batches = [[_batch(s, i, n, hw, c) for i in range(steps)] for c, s in cfg]
+            seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
+            want = [[{k: float(v) for k, v in m.train_step(*batches[j][i]).items()} for i in range(steps)]
+                    for j, m in enumerate(seq)]
+            for rep in range(reps):
+                run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV,
+                                          schedule="concurrent")
+                torch.cuda.synchronize()
+                got = [[], []]
+                for i in range(steps):
+                    outs = run.train_step([batches[j][i] for j in range(len(cfg))])
+                    torch.cuda.synchronize()
+                    for j, o in enumerate(outs):
+                        got[j].append({k: float(v) for k, v in o.items()})
+                assert got == want, f"repetition {rep}"
+                for a, b in zip(seq, run.systems):
+                    assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)
+                    assert torch.equal(a.optimizer_D_A.flat_p, b.optimizer_D_A.flat_p)
     finally:
         ops.set_mma(prev)
-    assert got == want
-    for a, b in zip(seq, run.systems):
-        assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)
-        assert torch.equal(a.optimizer_D_A.flat_p, b.optimizer_D_A.flat_p)
 
 
 def test_serial_schedule_equals_independent_runs():

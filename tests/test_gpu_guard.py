@@ -3,8 +3,8 @@
 Every tensor the product code allocates through torch.empty / empty_like / zeros / zeros_like /
 ones on the device (kernel outputs, padded dgrad buffers, split-K partial slabs, the per-stream
 workspaces) is carved out of a larger buffer whose 4 KiB on either side is filled with a canary
-byte.  One step of two CycleGANs on two HIP streams (config 5's concurrent schedule, which runs
-the f32 operand mode) and one single-stream bf16x6 step run with every allocation guarded;
+byte.  One step of two CycleGANs on two HIP streams (config 5's concurrent schedule) and one
+single-stream step run with every allocation guarded, in f32 and bf16x6;
 afterwards every guard band must still hold the canary: no kernel stores outside the extent its
 host code allocated for it (the two-stream audit).
 """
@@ -90,7 +90,7 @@ class _Guarded:
         return bad
 
 
-@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("serial", "bf16x6")])
+@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("concurrent", "bf16x6"), ("serial", "bf16x6")])
 def test_no_store_outside_allocations(schedule, mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
