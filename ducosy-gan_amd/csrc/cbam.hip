@@ -4,8 +4,10 @@
 // avgpool(IN(y)) is identically 0 (IN output has zero mean per (n,c)), so the avg branch is
 // evaluated on exact zeros: it contributes fc(0) = 0 forward and exactly 0 gradient.
 // maxpool(IN(y)) = IN(max y) because the IN scale is positive, so the max comes from the
-// statistics pass over y.  Channel reductions use one wave64 per pixel (channels on lanes,
-// float4 per lane, xor-shuffle reductions).
+// statistics pass over y.  Channel reductions run 16 lanes per pixel, 4 pixels per wave (16
+// channels per lane as float4 columns, 4-step xor reductions inside a 16-lane row) for C = 64,
+// 128, 256, and one wave64 per pixel otherwise; the per-(n, c) sums of the backward run as
+// float4 columns with pixel lanes folded through LDS.
 #include "common.hpp"
 
 namespace dcs {
@@ -120,6 +122,159 @@ __global__ __launch_bounds__(256) void sa_apply_kernel(const float* __restrict__
         reinterpret_cast<float4*>(out + p * C)[c4] = o;
     }
 }
+
+// ---- 16-lane-per-pixel forms (C = 64 * NQ, NQ in {1, 2, 4}) -------------------------------
+// A wave holds 4 pixels; lane j of a pixel's 16-lane group owns float4 columns q*16 + j
+// (q < NQ), so every load instruction moves 4 pixels x 256 contiguous bytes, the per-(image,
+// channel) scale / shift / ca stay in registers across the wave's pixels (reloaded only when the
+// image changes), and each reduction over channels is 4 xor steps inside a 16-lane row.
+constexpr int CB_QUADS = 4;  // pixel quads per wave
+
+template <int NQ>
+struct CbRegs {
+    float4 s[NQ], b[NQ], a[NQ];
+    int n = -1;
+    __device__ __forceinline__ void load(const float* sc, const float* sh, const float* ca, int C, int nn, int j) {
+        if (nn == n) return;
+        n = nn;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const long long o = (long long)nn * C + 4 * (q * 16 + j);
+            s[q] = *reinterpret_cast<const float4*>(sc + o);
+            b[q] = *reinterpret_cast<const float4*>(sh + o);
+            a[q] = *reinterpret_cast<const float4*>(ca + o);
+        }
+    }
+};
+
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void sa_reduce16_kernel(const float* __restrict__ y, const float* __restrict__ sc,
+                                                          const float* __restrict__ sh, const float* __restrict__ ca,
+                                                          int HW, int C, long long P, float* __restrict__ sin_,
+                                                          int* __restrict__ sarg) {
+    const int lane = threadIdx.x & 63, j = lane & 15, grp = lane >> 4;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    CbRegs<NQ> r;
+    for (int it = 0; it < CB_QUADS; ++it) {
+        const long long p = (wave * CB_QUADS + it) * 4 + grp;
+        if (p >= P) break;
+        r.load(sc, sh, ca, C, (int)(p / HW), j);
+        const float4* yp = reinterpret_cast<const float4*>(y + p * C);
+        float sum = 0.f, mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 v = yp[q * 16 + j];
+            const int c = 4 * (q * 16 + j);
+            const float z0 = fmaf(v.x, r.s[q].x, r.b[q].x) * r.a[q].x;
+            const float z1 = fmaf(v.y, r.s[q].y, r.b[q].y) * r.a[q].y;
+            const float z2 = fmaf(v.z, r.s[q].z, r.b[q].z) * r.a[q].z;
+            const float z3 = fmaf(v.w, r.s[q].w, r.b[q].w) * r.a[q].w;
+            sum += z0; sum += z1; sum += z2; sum += z3;
+            if (z0 > mx) { mx = z0; am = c; }
+            if (z1 > mx) { mx = z1; am = c + 1; }
+            if (z2 > mx) { mx = z2; am = c + 2; }
+            if (z3 > mx) { mx = z3; am = c + 3; }
+        }
+        sum = row16_sum(sum);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            const float om = __shfl_xor(mx, o, 64);
+            const int oa = __shfl_xor(am, o, 64);
+            if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+        }
+        if (j == 0) {
+            reinterpret_cast<float2*>(sin_)[p] = make_float2(sum / (float)C, mx);
+            sarg[p] = am;
+        }
+    }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void sa_apply16_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                         const float* __restrict__ sc, const float* __restrict__ sh,
+                                                         const float* __restrict__ ca, const float* __restrict__ sin_,
+                                                         const float* __restrict__ wsa, int H, int W, int C, int ksa,
+                                                         long long P, float* __restrict__ sa,
+                                                         float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, j = lane & 15, grp = lane >> 4;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int HW = H * W, r = ksa / 2, taps = ksa * ksa;
+    CbRegs<NQ> rg;
+    for (int it = 0; it < CB_QUADS; ++it) {
+        const long long p = (wave * CB_QUADS + it) * 4 + grp;
+        if (p >= P) break;
+        const int n = (int)(p / HW);
+        const int rem = (int)(p - (long long)n * HW);
+        const int py = rem / W, px = rem - py * W;
+        float pre = 0.f;
+        for (int t = j; t < 2 * taps; t += 16) {
+            const int ch = t / taps, tt = t - ch * taps;
+            const int ty = tt / ksa, tx = tt - ty * ksa;
+            const int yy = py + ty - r, xx = px + tx - r;
+            if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+                pre = fmaf(wsa[t], sin_[((long long)n * HW + yy * W + xx) * 2 + ch], pre);
+        }
+        pre = row16_sum(pre);
+        const float g = sigmoidf_(pre);
+        if (j == 0) sa[p] = g;
+        rg.load(sc, sh, ca, C, n, j);
+        const float4* yp = reinterpret_cast<const float4*>(y + p * C);
+        const float4* xp = reinterpret_cast<const float4*>(x + p * C);
+        float4* op = reinterpret_cast<float4*>(out + p * C);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 v = yp[q * 16 + j], xv = xp[q * 16 + j];
+            float4 o;
+            o.x = xv.x + fmaf(v.x, rg.s[q].x, rg.b[q].x) * rg.a[q].x * g;
+            o.y = xv.y + fmaf(v.y, rg.s[q].y, rg.b[q].y) * rg.a[q].y * g;
+            o.z = xv.z + fmaf(v.z, rg.s[q].z, rg.b[q].z) * rg.a[q].z * g;
+            o.w = xv.w + fmaf(v.w, rg.s[q].w, rg.b[q].w) * rg.a[q].w * g;
+            op[q * 16 + j] = o;
+        }
+    }
+}
+
+// backward b1 (16-lane form): dpre[p] = (sum_c dout*zc) * sa*(1-sa)
+template <int NQ>
+__global__ __launch_bounds__(256) void cb_bwd_dsa16_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                           const float* __restrict__ sc, const float* __restrict__ sh,
+                                                           const float* __restrict__ ca, const float* __restrict__ sa,
+                                                           int HW, int C, long long P, float* __restrict__ dpre) {
+    const int lane = threadIdx.x & 63, j = lane & 15, grp = lane >> 4;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    CbRegs<NQ> r;
+    for (int it = 0; it < CB_QUADS; ++it) {
+        const long long p = (wave * CB_QUADS + it) * 4 + grp;
+        if (p >= P) break;
+        r.load(sc, sh, ca, C, (int)(p / HW), j);
+        const float4* yp = reinterpret_cast<const float4*>(y + p * C);
+        const float4* dp = reinterpret_cast<const float4*>(dout + p * C);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float4 v = yp[q * 16 + j], d = dp[q * 16 + j];
+            acc = fmaf(d.x, fmaf(v.x, r.s[q].x, r.b[q].x) * r.a[q].x, acc);
+            acc = fmaf(d.y, fmaf(v.y, r.s[q].y, r.b[q].y) * r.a[q].y, acc);
+            acc = fmaf(d.z, fmaf(v.z, r.s[q].z, r.b[q].z) * r.a[q].z, acc);
+            acc = fmaf(d.w, fmaf(v.w, r.s[q].w, r.b[q].w) * r.a[q].w, acc);
+        }
+        acc = row16_sum(acc);
+        if (j == 0) {
+            const float g = sa[p];
+            dpre[p] = acc * g * (1.f - g);
+        }
+    }
+}
+
+static inline int cb_nq(int C) { return (C == 64 || C == 128 || C == 256) ? C / 64 : 0; }
+static inline unsigned cb16_blocks(long long P) { return (unsigned)cdiv(P, 4LL * 4 * CB_QUADS); }
 
 // ---- backward ---------------------------------------------------------------------------
 // b1: dpre[p] = (sum_c dout*zc) * sa*(1-sa)
@@ -527,12 +682,20 @@ extern "C" int dcs_cbam_forward(const float* x, const float* y, const float* sca
                        shift, w1, w2, C, Cr, ca);
     int e = check_launch("ca_forward");
     if (e) return e;
-    hipLaunchKernelGGL(sa_reduce_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, y, scale, shift, ca, H * W, C, P,
-                       sin_, sarg);
+    const int nq = cb_nq(C);
+#define DCS_CB16(K, NQ, ...) hipLaunchKernelGGL((K<NQ>), dim3(cb16_blocks(P)), dim3(256), 0, s, __VA_ARGS__)
+    if (nq == 4) DCS_CB16(sa_reduce16_kernel, 4, y, scale, shift, ca, H * W, C, P, sin_, sarg);
+    else if (nq == 2) DCS_CB16(sa_reduce16_kernel, 2, y, scale, shift, ca, H * W, C, P, sin_, sarg);
+    else if (nq == 1) DCS_CB16(sa_reduce16_kernel, 1, y, scale, shift, ca, H * W, C, P, sin_, sarg);
+    else hipLaunchKernelGGL(sa_reduce_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, y, scale, shift, ca, H * W, C,
+                            P, sin_, sarg);
     e = check_launch("sa_reduce");
     if (e) return e;
-    hipLaunchKernelGGL(sa_apply_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, x, y, scale, shift, ca, sin_, wsa,
-                       H, W, C, ksa, P, sa, out);
+    if (nq == 4) DCS_CB16(sa_apply16_kernel, 4, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
+    else if (nq == 2) DCS_CB16(sa_apply16_kernel, 2, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
+    else if (nq == 1) DCS_CB16(sa_apply16_kernel, 1, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
+    else hipLaunchKernelGGL(sa_apply_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, x, y, scale, shift, ca, sin_,
+                            wsa, H, W, C, ksa, P, sa, out);
     return check_launch("sa_apply");
 }
 
@@ -557,8 +720,12 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     hipStream_t s = as_stream(stream);
     const long long P = (long long)N * H * W;
     const int HW = H * W;
-    hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca, sa,
-                       HW, C, P, w.dpre);
+    const int nq = cb_nq(C);
+    if (nq == 4) DCS_CB16(cb_bwd_dsa16_kernel, 4, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
+    else if (nq == 2) DCS_CB16(cb_bwd_dsa16_kernel, 2, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
+    else if (nq == 1) DCS_CB16(cb_bwd_dsa16_kernel, 1, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
+    else hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca,
+                            sa, HW, C, P, w.dpre);
     int e = check_launch("cb_bwd_dsa");
     if (e) return e;
     hipLaunchKernelGGL(cb_bwd_dsin_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, w.dpre, wsa, H, W, ksa, P,
@@ -596,3 +763,4 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     }
     return check_launch("cb_bwd_apply");
 }
+#undef DCS_CB16

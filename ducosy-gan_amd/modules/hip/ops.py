@@ -438,15 +438,17 @@ class ConvGeom:
             p = t
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
-            if _FUSE_FOLD and p == 1 and self.k == 3 and H >= 4 and W >= 4 and not narrow and dy.is_contiguous() \
-                    and not _x6p(d) and ci % 4 == 0:
-                # interior written by the conv epilogue (+ addend), the ring folded in after
+            if _FUSE_FOLD and addend is None and p == 1 and self.k == 3 and H >= 4 and W >= 4 and not narrow \
+                    and dy.is_contiguous() and not _x6p(d) and ci % 4 == 0:
+                # interior written by the conv epilogue, the ring folded in after.  With a residual
+                # addend the padded pass + dcs_reflect_fold stays faster: the addend read in the
+                # epilogue sits after the MFMA loop (+145 us per 16-image launch against +125 us for
+                # the whole fold pass, profiles/r02e_kernel_table.md)
                 ring = lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4
                 buf = torch.empty(N * H * W * ci + ring, device=dev, dtype=torch.float32)
                 out = buf[:N * H * W * ci].view(N, H, W, ci)
                 e0 = PROBE.begin() if _is_res_geom(self) else None
-                lib.call("dcs_conv_dgrad_reflect", ctypes.byref(d), _p(dy), _p(wpack_d),
-                         _p(addend.contiguous()) if addend is not None else None, _p(out),
+                lib.call("dcs_conv_dgrad_reflect", ctypes.byref(d), _p(dy), _p(wpack_d), None, _p(out),
                          ctypes.c_void_p(buf.data_ptr() + N * H * W * ci * 4), _stream())
                 PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
                 return out

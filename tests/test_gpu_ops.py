@@ -261,6 +261,50 @@ def test_reflect_dgrad_direct_and_accumulate(ops, H):
     assert rel(got, want) < 1e-5
 
 
+@pytest.mark.parametrize("H,mode", [(4, "bf16x6"), (9, "bf16x6"), (16, "f32"), (16, "bf16x6")])
+def test_dgrad_reflect_epilogue_fold_matches_fold_pass(ops, H, mode):
+    """dcs_conv_dgrad_reflect (interior pixels stored by the conv epilogue, the one-pixel ring
+    folded in by a second kernel) against the padded-grid pass + dcs_reflect_fold, without and
+    (direct C-ABI call) with the residual addend; only the summation order of the ring pixels
+    differs."""
+    import ctypes
+    from modules.hip import lib
+    prev = ops.get_mma()
+    ops.set_mma(mode)
+    try:
+        g, _ = _geom((256, 256, 3, 1, (1, 1, 1, 1), "reflect", 1, H))
+        w = rnd((256, 256, 3, 3), 41, "w", -0.05, 0.05).cuda()
+        wd = g.pack_dgrad(w)
+        dyn = rnd((2, H, H, 256), 41, "dy").cuda()
+        add = rnd((2, H, H, 256), 41, "add").cuda()
+        fused = g.dgrad(dyn, wd, H, H)
+        ops._FUSE_FOLD = False
+        try:
+            plain = g.dgrad(dyn, wd, H, H)
+            plain_add = g.dgrad(dyn, wd, H, H, addend=add.clone())
+        finally:
+            ops._FUSE_FOLD = True
+        assert rel(fused, plain) < 1e-6
+        d = lib.ConvDesc()
+        d.N, d.Hs, d.Ws, d.Cs = 2, H, H, 256
+        d.s_n, d.s_c, d.s_h, d.s_w = H * H * 256, 1, H * 256, 256
+        d.csplit, d.up, d.pad_mode = 256, 1, lib.DCS_PAD_ZERO
+        d.KH = d.KW = 3
+        d.pt = d.pl = 2
+        d.stride, d.Ho, d.Wo, d.Co = 1, H + 2, H + 2, 256
+        d.ldb, d.mma = wd.shape[1], ops._MMA
+        d.korder = lib.KORDER_SLICE if g.kslice else lib.KORDER_TAP
+        ring = lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4
+        buf = torch.empty(2 * H * H * 256 + ring, device=DEV)
+        lib.call("dcs_conv_dgrad_reflect", ctypes.byref(d), ctypes.c_void_p(dyn.data_ptr()),
+                 ctypes.c_void_p(wd.data_ptr()), ctypes.c_void_p(add.data_ptr()), ctypes.c_void_p(buf.data_ptr()),
+                 ctypes.c_void_p(buf.data_ptr() + 2 * H * H * 256 * 4), None)
+        torch.cuda.synchronize()
+        assert rel(buf[:2 * H * H * 256].view(2, H, H, 256), plain_add) < 1e-6
+    finally:
+        ops.set_mma(prev)
+
+
 @pytest.mark.parametrize("c1,c2,k,stride,pads,mode", [(1, 2, 7, 1, (3, 3, 3, 3), "reflect"),
                                                       (1, 1, 7, 1, (3, 3, 3, 3), "reflect"),
                                                       (1, 0, 7, 1, (3, 3, 3, 3), "reflect"),
