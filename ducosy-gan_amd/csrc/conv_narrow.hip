@@ -12,6 +12,12 @@
 namespace dcs {
 
 constexpr int NT_TH = 16, NT_TW = 64, NT_CC = 8, NT_XT = 4;
+#ifndef DCS_NARROW_TY_UNROLL
+#define DCS_NARROW_TY_UNROLL 1
+#endif
+#ifndef DCS_NARROW_WAVES
+#define DCS_NARROW_WAVES 3  // waves per SIMD the head forward is compiled for (3 blocks of 4 waves per CU)
+#endif
 
 // Halo coordinate -> source coordinate.  Halo pixels that only feed masked outputs (tile
 // overhang past Ho/Wo) can lie more than one reflection away: clamp them into the tensor so
@@ -61,7 +67,7 @@ __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
 }
 
 template <int KH, int KW>
-__global__ __launch_bounds__(256) void narrow_rows_tiled_kernel(const dcs_conv_desc d, const float* __restrict__ src,
+__global__ __launch_bounds__(256, DCS_NARROW_WAVES) void narrow_rows_tiled_kernel(const dcs_conv_desc d, const float* __restrict__ src,
                                                                 const float* __restrict__ wp,
                                                                 const float* __restrict__ bias,
                                                                 const float* __restrict__ psc,
@@ -82,10 +88,12 @@ __global__ __launch_bounds__(256) void narrow_rows_tiled_kernel(const dcs_conv_d
             lw[i] = wp[((long long)t * d.Cs + c0 + c) * d.ldb];
         }
         __syncthreads();
-#pragma unroll
+        // tap rows not unrolled and 3 waves per SIMD (<= 168 VGPRs, was 238): 3 blocks of 50 KB LDS
+        // fit a CU instead of 2
+#pragma unroll DCS_NARROW_TY_UNROLL
         for (int ty = 0; ty < KH; ++ty) {
             const float* row = lin + ((r + ty) * HW_ + cg * NT_XT) * NT_CC;
-#pragma unroll
+#pragma unroll DCS_NARROW_TY_UNROLL
             for (int q = 0; q < 2; ++q) {
                 float4 v[NT_XT + KW - 1];
 #pragma unroll
@@ -368,9 +376,12 @@ bool narrow_wgrad_tiled_ok(const dcs_conv_desc& d, const float* src) {
     return narrow_tiled_ok(d, src) && d.KH == 7 && d.Cs == 64;
 }
 
+#ifndef DCS_NARROW_WGRAD_BLOCKS
+#define DCS_NARROW_WGRAD_BLOCKS 768  // 3 blocks of 53 KB LDS per CU on 256 CUs
+#endif
 int narrow_wgrad_tiled_blocks(const dcs_conv_desc& d) {
     long long tiles = cdiv(d.Wo, NT_TW) * cdiv(d.Ho, NT_TH) * d.N;
-    return (int)(tiles < 512 ? tiles : 512);
+    return (int)(tiles < DCS_NARROW_WGRAD_BLOCKS ? tiles : DCS_NARROW_WGRAD_BLOCKS);
 }
 
 int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const float* src, const float* psc,
