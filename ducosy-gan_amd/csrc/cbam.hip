@@ -241,38 +241,6 @@ __global__ __launch_bounds__(256) void sa_apply16_kernel(const float* __restrict
     }
 }
 
-// backward b1 (16-lane form): dpre[p] = (sum_c dout*zc) * sa*(1-sa)
-template <int NQ>
-__global__ __launch_bounds__(256) void cb_bwd_dsa16_kernel(const float* __restrict__ dout, const float* __restrict__ y,
-                                                           const float* __restrict__ sc, const float* __restrict__ sh,
-                                                           const float* __restrict__ ca, const float* __restrict__ sa,
-                                                           int HW, int C, long long P, float* __restrict__ dpre) {
-    const int lane = threadIdx.x & 63, j = lane & 15, grp = lane >> 4;
-    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    CbRegs<NQ> r;
-    for (int it = 0; it < CB_QUADS; ++it) {
-        const long long p = (wave * CB_QUADS + it) * 4 + grp;
-        if (p >= P) break;
-        r.load(sc, sh, ca, C, (int)(p / HW), j);
-        const float4* yp = reinterpret_cast<const float4*>(y + p * C);
-        const float4* dp = reinterpret_cast<const float4*>(dout + p * C);
-        float acc = 0.f;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const float4 v = yp[q * 16 + j], d = dp[q * 16 + j];
-            acc = fmaf(d.x, fmaf(v.x, r.s[q].x, r.b[q].x) * r.a[q].x, acc);
-            acc = fmaf(d.y, fmaf(v.y, r.s[q].y, r.b[q].y) * r.a[q].y, acc);
-            acc = fmaf(d.z, fmaf(v.z, r.s[q].z, r.b[q].z) * r.a[q].z, acc);
-            acc = fmaf(d.w, fmaf(v.w, r.s[q].w, r.b[q].w) * r.a[q].w, acc);
-        }
-        acc = row16_sum(acc);
-        if (j == 0) {
-            const float g = sa[p];
-            dpre[p] = acc * g * (1.f - g);
-        }
-    }
-}
-
 static inline int cb_nq(int C) { return (C == 64 || C == 128 || C == 256) ? C / 64 : 0; }
 static inline unsigned cb16_blocks(long long P) { return (unsigned)cdiv(P, 4LL * 4 * CB_QUADS); }
 
@@ -720,12 +688,10 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     hipStream_t s = as_stream(stream);
     const long long P = (long long)N * H * W;
     const int HW = H * W;
-    const int nq = cb_nq(C);
-    if (nq == 4) DCS_CB16(cb_bwd_dsa16_kernel, 4, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
-    else if (nq == 2) DCS_CB16(cb_bwd_dsa16_kernel, 2, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
-    else if (nq == 1) DCS_CB16(cb_bwd_dsa16_kernel, 1, dout, y, scale, shift, ca, sa, HW, C, P, w.dpre);
-    else hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca,
-                            sa, HW, C, P, w.dpre);
+    // one wave per pixel: the 16-lane form (4 pixels per wave, 4 quads per wave) measured 104 vs
+    // 96 us per 16-image launch here (a read-only pass wants more loads in flight per wave)
+    hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca, sa,
+                       HW, C, P, w.dpre);
     int e = check_launch("cb_bwd_dsa");
     if (e) return e;
     hipLaunchKernelGGL(cb_bwd_dsin_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, w.dpre, wsa, H, W, ksa, P,
