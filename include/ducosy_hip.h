@@ -100,8 +100,9 @@ const char* dcs_last_error(void);
 int dcs_version(void);
 
 /* A HIP stream whose kernels may only occupy the compute units set in cu_mask (words 32-bit
- * words, bit i = CU i; hipExtStreamCreateWithCUMask).  Diagnostics of the two-stream schedule
- * of BASELINE config 5 (scripts/conc_cumask.py, DESIGN.md §3, Config 5); the reference trains
+ * words, bit i = CU i; hipExtStreamCreateWithCUMask).  The two-stream schedule of BASELINE
+ * config 5 runs each model on its own CU partition (modules/trainer.py ConcurrentCycleGANs;
+ * DESIGN.md §3, Config 5: streams sharing a CU pair gave wrong results); the reference trains
  * its two models one after the other (train.py:27-38), so this has no reference counterpart.
  * The stream is created blocking: it synchronises with the legacy null stream. */
 int dcs_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream);

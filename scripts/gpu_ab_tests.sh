@@ -1,0 +1,7 @@
+# parity tests of the default build, then per-layer (kbench) and whole-step A/B against lib/libducosy_hip_$1.so
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)} && mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_mma.py tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/q_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAILED|^E  " gpurun_out/q_tests.log | head -20; exit 1; }
+tail -1 gpurun_out/q_tests.log
+bash scripts/ab.sh $1 --batch 16 --mma bf16x6 --only down1,down2,up1,up2,d1,d2 > gpurun_out/ab_$1.log 2>&1 || exit 1
+bash scripts/ab_lib.sh $1 || exit 1
