@@ -29,6 +29,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // and bf16x3 (each f32 operand split into hi + lo bf16, three MFMAs hi*hi + hi*lo + lo*hi:
 // ~2^-16 relative per product instead of 2^-24, at 3/16 of the f32-MFMA cycles per FLOP).
 constexpr int MMA_F32 = 0, MMA_BF16 = 1, MMA_BF16X3 = 3, MMA_BF16X6 = 6;
+// internal: DCS_MMA_BF16 on the bf16x6 pipeline with its three LDS planes used as three
+// consecutive 16-k sub-tiles (48 k per barrier, one product each), for the residual convs
+constexpr int MMA_BF16P = 2;
 #ifndef DCS_BF16_BUFGATHER
 #define DCS_BF16_BUFGATHER 1  // branch-free buffer-descriptor gather in the bf16 rows pass
 #endif
@@ -143,6 +146,9 @@ constexpr int NT = 256;
 #endif
 #ifndef DCS_X6_SGB0
 #define DCS_X6_SGB0 0  // ... the same for the other bf16x6 rows kernels
+#endif
+#ifndef DCS_BF16P
+#define DCS_BF16P 1  // half-precision residual convs on the x6 pipeline (48 k per barrier)
 #endif
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
@@ -647,7 +653,8 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     constexpr int BTPR = NTH / BN;                 // B loader threads per row (2 or 4)
     // bf16: 64-deep k-tiles (twice the MFMA work per round of global loads: the bf16 passes are
     // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
-    constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : BK;  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
+    constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : (MMA == MMA_BF16P ? 48 : BK);  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
+    constexpr bool X6L = MMA == MMA_BF16X6 || MMA == MMA_BF16P;  // the x6 LDS planes and pipeline
     constexpr int AKPT = BKT / 2;                  // k per A-loader thread (2 threads per row)
     constexpr int ACH = AKPT / 4;                  // float4 per A-loader thread
     constexpr int BKPT = BKT / BTPR;               // k per B-loader thread
@@ -661,7 +668,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // odd groups of 8 rows, so both the 8-lane ds_write_b128 groups and the 16-lane
     // ds_read_b128 groups hit 64 distinct banks (MI355X_MICROARCH.md LDS table)
     constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK
-                             : MMA == MMA_BF16X6 ? 3 * 2 * (BM + BN) * 16 / 2 : (BM + BN) * LDE;
+                             : X6L ? 3 * 2 * (BM + BN) * 16 / 2 : (BM + BN) * LDE;
 
     // f32: As[2][BM][LDK] | Bs[2][BN][LDK];  bf16 modes: Ah[2][BM][LDE] | Bh[2][BN][LDE]
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
@@ -696,13 +703,14 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
 
-    // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap)
-    const int arow = tid >> 1, akq = (tid & 1) * AKPT;
+    // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap); BF16P:
+    // 8 k of each of the tile's three 16-k sub-tiles
+    const int arow = tid >> 1, akq = (tid & 1) * (MMA == MMA_BF16P ? 8 : AKPT);
     const RowInfo ri = row_info(d, g, (int)(m0 + arow), fold);
     const bool rvalid = ri.out_off >= 0;
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     // B loader: one output channel row, BKPT consecutive k
-    const int brow = tid / BTPR, bkq = (tid % BTPR) * BKPT;
+    const int brow = tid / BTPR, bkq = (tid % BTPR) * (MMA == MMA_BF16P ? 16 / BTPR : BKPT);
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
     const int K = g.ntaps * d.Cs;
@@ -792,6 +800,24 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 }
             }
             aj += BKT / 4;
+        } else if (MMA == MMA_BF16P) {
+            // three 16-k sub-tiles (slice-major: the next tap of the slice each), 8 k per thread
+#pragma unroll
+            for (int sub = 0; sub < 3; ++sub) {
+                const bool kin = aj < g.ntaps && ac < d.Cs;
+                int ady, adx, bt, sy = 0, sx = 0;
+                tap_decode(d, g, kin ? aj : 0, ady, adx, bt);
+                const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                const int off = (kin && rvalid && yok && xok)
+                                    ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4
+                                    : OOB_OFF;
+                dst[2 * sub] = buf_load4(arsrc, off);
+                dst[2 * sub + 1] = buf_load4(arsrc, off + 16);
+                const bool wrap = aj + 1 >= g.ntaps;
+                aj = wrap ? 0 : aj + 1;
+                ac += wrap ? 16 : 0;
+            }
         } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
             // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
             int sy = 0, sx = 0, off = OOB_OFF;
@@ -866,6 +892,16 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     };
     const __amdgpu_buffer_rsrc_t brsrc = src_rsrc(wp);
     auto load_b = [&](int kt, auto& dst) {
+        if constexpr (MMA == MMA_BF16P) {  // slice-major packed B: the tile's 48 k are consecutive
+#pragma unroll
+            for (int sub = 0; sub < 3; ++sub) {
+                const long long col = (long long)kt * BKT + 16 * sub + bkq;
+                const int off = col < d.ldb ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
+                dst[2 * sub] = buf_load4(brsrc, off);
+                dst[2 * sub + 1] = buf_load4(brsrc, off + 16);
+            }
+            return;
+        }
         long long col;
         bool ok = true;
         if (!d.parity && !KSB) {
@@ -910,6 +946,17 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             for (int i = 0; i < ACH; ++i) *reinterpret_cast<float4*>(&As[buf][arow][akq + 4 * i]) = sa[i];
 #pragma unroll
             for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = sb[i];
+        } else if constexpr (MMA == MMA_BF16P) {
+            static_assert(BKT == 48 && ACH == 6 && BCH == 6 && BN == 128, "bf16p tiles: 3 x 16 k, 8 per thread each");
+#pragma unroll
+            for (int sub = 0; sub < 3; ++sub) {
+                const floatx8 fa = {sa[2 * sub].x, sa[2 * sub].y, sa[2 * sub].z, sa[2 * sub].w,
+                                    sa[2 * sub + 1].x, sa[2 * sub + 1].y, sa[2 * sub + 1].z, sa[2 * sub + 1].w};
+                *reinterpret_cast<bf16x8*>(Ah + x6o(sub, buf, arow, akq >> 3)) = __builtin_convertvector(fa, bf16x8);
+                const floatx8 fb = {sb[2 * sub].x, sb[2 * sub].y, sb[2 * sub].z, sb[2 * sub].w,
+                                    sb[2 * sub + 1].x, sb[2 * sub + 1].y, sb[2 * sub + 1].z, sb[2 * sub + 1].w};
+                *reinterpret_cast<bf16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = __builtin_convertvector(fb, bf16x8);
+            }
         } else if constexpr (MMA == MMA_BF16X6) {
             static_assert(BKT == 16 && ACH == 2 && (BCH == 2 || BCH == 1), "x6 tiles: 16 k, 8 / 4 per loader thread");
             bf16x8 hi, mid, lo;
@@ -982,6 +1029,24 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         constexpr int NST = BKT / 16;
         const int kh = (lane >> 5) * 8;
         auto step = [&](int cur, int st) {
+            if constexpr (MMA == MMA_BF16P) {  // three 16-k sub-tiles, one product each, into acc
+#pragma unroll
+                for (int sub = 0; sub < 3; ++sub) {
+                    bf16x8 fa[IM], fb[JN];
+#pragma unroll
+                    for (int i = 0; i < IM; ++i)
+                        fa[i] = *reinterpret_cast<const bf16x8*>(Ah + x6o(sub, cur, wm * WM + i * 32 + l32, kh >> 3));
+#pragma unroll
+                    for (int j = 0; j < JN; ++j)
+                        fb[j] = *reinterpret_cast<const bf16x8*>(Ah + x6o(sub, cur, BM + wn * WN + j * 32 + l32, kh >> 3));
+#pragma unroll
+                    for (int i = 0; i < IM; ++i)
+#pragma unroll
+                        for (int j = 0; j < JN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+                return;
+            }
             bf16x8 ah[IM], bh[JN], al[IM], bl[JN], am[IM], bm[JN];
 #pragma unroll
             for (int i = 0; i < IM; ++i) {
@@ -1030,7 +1095,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 }
         };
         auto fold_t = [&](int kt) {  // close the inner accumulation chain every KT2 k-tiles
-            if (MMA != MMA_BF16 && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
+            if (MMA != MMA_BF16 && MMA != MMA_BF16P && ((kt % KT2) == KT2 - 1 || kt + 1 == nkt)) {
 #pragma unroll
                 for (int i = 0; i < IM; ++i)
 #pragma unroll
@@ -1041,7 +1106,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                     }
             }
         };
-        if constexpr (MMA == MMA_BF16X6 && DCS_X6_PIPE) {
+        if constexpr (X6L && DCS_X6_PIPE) {
             // two register sets: tile kt+2's gather is in flight while tile kt computes, so
             // staging tile kt+1 waits only for loads issued a whole k-tile earlier
             // The loads are issued unconditionally (k-tiles past the end gather zeros from the
@@ -1059,7 +1124,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                     // staging before the chain fold and unconditional (a tile past the end is
                     // zeros into a buffer nobody reads again): one basic block with the MFMAs
                     store_tiles(1, ra, rb, pa1);
-                    x6_interleave<IM * JN * 6, TAG == 1 ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : 6), (TAG == 1 && MMA == MMA_BF16X6) ? DCS_X6_SGB : DCS_X6_SGB0>();
                     fold_t(kt);
                 } else {
                     fold_t(kt);
@@ -1072,7 +1137,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 step(1, 0);
                 if (DCS_X6_STORE_FIRST) {
                     store_tiles(0, ra2, rb2, pa2);
-                    x6_interleave<IM * JN * 6, TAG == 1 ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : 6), (TAG == 1 && MMA == MMA_BF16X6) ? DCS_X6_SGB : DCS_X6_SGB0>();
                     fold_t(kt + 1);
                 } else {
                     fold_t(kt + 1);
@@ -1964,6 +2029,12 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
         return check_launch("conv_rows");
     }
+    if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
+        // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier
+        hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16P>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias,
+                           psc, psh, out, gx, gy, parts, fold);
+        return check_launch("conv_rows");
+    }
     const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \
@@ -2345,8 +2416,9 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool dy_small = (long long)d.N * d.Ho * d.Wo * d.Co * 4 < (long long)OOB_OFF - 64;
     // The bf16 weight-gradient kernel measured slower than the exact f32 one at every layer
-    // (res 2.1-2.5 ms vs 1.75 ms: its 8-pixel walk per thread is VALU bound), so bf16 modes run
-    // the f32 weight gradient unless DCS_WGRAD_MMA16 is defined (kept for the A/B record).
+    // (res 2.1-2.5 ms vs 1.75 ms: its 8-pixel walk per thread is VALU bound), so the bf16 and
+    // bf16x3 modes run the bf16x6 weight gradient (fp32-class and faster than f32) unless
+    // DCS_WGRAD_MMA16 is defined (kept for the A/B record).
 #ifdef DCS_WGRAD_MMA16
     if (d.mma != MMA_F32 && vec && dy_small && p.BM == 128 && p.BN == 128 && !d.parity) {
 #else
@@ -2361,7 +2433,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (d.mma == MMA_BF16X6 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64)) &&
+    } else if (d.mma != MMA_F32 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64)) &&
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
