@@ -150,6 +150,9 @@ constexpr int NT = 256;
 #ifndef DCS_BF16P
 #define DCS_BF16P 1  // half-precision residual convs on the x6 pipeline (48 k per barrier)
 #endif
+#ifndef DCS_BF16P_BM256
+#define DCS_BF16P_BM256 1  // ... on 256-row tiles where they divide the pixels
+#endif
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
@@ -645,7 +648,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts, int fold) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    static_assert(BM == 128 || (BM == 256 && MMA == MMA_BF16X6 && BN == 128 && VEC == 1),
+    static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P) && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
     constexpr int NTH = 2 * BM;                    // threads (two per A row)
     constexpr int WM = 64, WN = BN / 2;            // per-wave tile
@@ -893,12 +896,13 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     const __amdgpu_buffer_rsrc_t brsrc = src_rsrc(wp);
     auto load_b = [&](int kt, auto& dst) {
         if constexpr (MMA == MMA_BF16P) {  // slice-major packed B: the tile's 48 k are consecutive
+            constexpr int BQ = BCH / 3;      // float4 per sub-tile: 2 (256 threads) or 1 (512)
 #pragma unroll
             for (int sub = 0; sub < 3; ++sub) {
                 const long long col = (long long)kt * BKT + 16 * sub + bkq;
                 const int off = col < d.ldb ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
-                dst[2 * sub] = buf_load4(brsrc, off);
-                dst[2 * sub + 1] = buf_load4(brsrc, off + 16);
+#pragma unroll
+                for (int q = 0; q < BQ; ++q) dst[BQ * sub + q] = buf_load4(brsrc, off + 16 * q);
             }
             return;
         }
@@ -947,15 +951,23 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 #pragma unroll
             for (int i = 0; i < BCH; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow][bkq + 4 * i]) = sb[i];
         } else if constexpr (MMA == MMA_BF16P) {
-            static_assert(BKT == 48 && ACH == 6 && BCH == 6 && BN == 128, "bf16p tiles: 3 x 16 k, 8 per thread each");
+            static_assert(BKT == 48 && ACH == 6 && (BCH == 6 || BCH == 3) && BN == 128,
+                          "bf16p tiles: 3 x 16 k, 8 A and 8 / 4 B per thread each");
 #pragma unroll
             for (int sub = 0; sub < 3; ++sub) {
                 const floatx8 fa = {sa[2 * sub].x, sa[2 * sub].y, sa[2 * sub].z, sa[2 * sub].w,
                                     sa[2 * sub + 1].x, sa[2 * sub + 1].y, sa[2 * sub + 1].z, sa[2 * sub + 1].w};
                 *reinterpret_cast<bf16x8*>(Ah + x6o(sub, buf, arow, akq >> 3)) = __builtin_convertvector(fa, bf16x8);
-                const floatx8 fb = {sb[2 * sub].x, sb[2 * sub].y, sb[2 * sub].z, sb[2 * sub].w,
-                                    sb[2 * sub + 1].x, sb[2 * sub + 1].y, sb[2 * sub + 1].z, sb[2 * sub + 1].w};
-                *reinterpret_cast<bf16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = __builtin_convertvector(fb, bf16x8);
+                if constexpr (BCH == 6) {
+                    const floatx8 fb = {sb[2 * sub].x, sb[2 * sub].y, sb[2 * sub].z, sb[2 * sub].w,
+                                        sb[2 * sub + 1].x, sb[2 * sub + 1].y, sb[2 * sub + 1].z, sb[2 * sub + 1].w};
+                    *reinterpret_cast<bf16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = __builtin_convertvector(fb, bf16x8);
+                } else {  // 512 threads: 4 k of B per thread, the 8-byte half of a 16-byte chunk
+                    const float4 v = sb[sub];
+                    const f32x4v f4 = {v.x, v.y, v.z, v.w};
+                    *reinterpret_cast<bf16x4*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3) + 4 * ((bkq >> 2) & 1)) =
+                        __builtin_convertvector(f4, bf16x4);
+                }
             }
         } else if constexpr (MMA == MMA_BF16X6) {
             static_assert(BKT == 16 && ACH == 2 && (BCH == 2 || BCH == 1), "x6 tiles: 16 k, 8 / 4 per loader thread");
@@ -2030,9 +2042,17 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         return check_launch("conv_rows");
     }
     if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
-        // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier
-        hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16P>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias,
-                           psc, psh, out, gx, gy, parts, fold);
+        // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier; 256-row
+        // tiles where they divide the pixels (the forward)
+        if (DCS_BF16P_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
+            const int gx2 = (int)cdiv(Mmax, 256);
+            hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16P>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
+                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts, fold);
+            if (bm_used) *bm_used = 256;
+        } else {
+            hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16P>), grid, dim3(NT), 0, s, d, src, src2, wpack,
+                               bias, psc, psh, out, gx, gy, parts, fold);
+        }
         return check_launch("conv_rows");
     }
     const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
