@@ -2152,12 +2152,15 @@ typedef short shortx4 __attribute__((ext_vector_type(4)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
 
-template <int TAG>
+// MMA == MMA_BF16P (the half-precision mode): the three planes hold three consecutive 16-pixel
+// sub-tiles converted to bf16 (48 pixels per barrier, one product each, one accumulation level).
+template <int TAG, int MMA = MMA_BF16X6>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
     const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws, int kt_per_split,
     int gn, int gm) {
     const dcs_conv_desc d = specialise<TAG>(din);
+    constexpr int NSUB = MMA == MMA_BF16P ? 3 : 1;  // 16-pixel sub-tiles per k-tile
     constexpr int BM = 128, BN = 128, BKP = 16;  // output channels x (tap, ci) columns x pixels per k-tile
     constexpr int WM = BM / 2, WN = BN / 2, IM = WM / 32, JN = WN / 32;
     constexpr int PITCH = 160;                   // bf16 per LDS row
@@ -2179,9 +2182,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const int Ktot = g.ntaps * d.Cs;
     const int m0 = mtile * BM, n0 = ntile * BN;
     const long long nkt_all = (P + BKP - 1) / BKP;
-    const long long kt_beg = (long long)split * kt_per_split;
+    long long kt_beg = (long long)split * kt_per_split;
     long long kt_end = kt_beg + kt_per_split;
     if (kt_end > nkt_all) kt_end = nkt_all;
+    // pixels of this split; BF16P walks them in 48-pixel k-tiles numbered from 0
+    const long long px_beg = kt_beg * BKP;
+    const long long px_end = kt_end * BKP < P ? kt_end * BKP : P;
+    if constexpr (MMA == MMA_BF16P) {
+        kt_end = px_end > px_beg ? (px_end - px_beg + 3 * BKP - 1) / (3 * BKP) : 0;
+        kt_beg = 0;
+    }
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
@@ -2200,7 +2210,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const __amdgpu_buffer_rsrc_t rsrc = src_rsrc(src);
     int pn = 0, pqy = 0, pqx = 0;  // pixel of the next k-tile row this thread loads
     {
-        const long long p = kt_beg * BKP + kr;
+        const long long p = px_beg + kr;
         if (p < P) {
             const int per = g.My * g.Mx;
             pn = (int)(p / per);
@@ -2211,19 +2221,21 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     }
     // Two register sets: the global loads of tile kt+2 are issued while tile kt is multiplied and
     // consumed (split + stored to LDS) only at the end of tile kt+1, two tiles of MFMA work later.
-    float4 ra0[2], rb0[2], ra1[2], rb1[2];
+    float4 ra0[2 * NSUB], rb0[2 * NSUB], ra1[2 * NSUB], rb1[2 * NSUB];
     // Branch-free loads (buffer loads; out-of-range offsets read zeros) so that the wait for one
     // register set never waits for the other; the prologue affine is applied at the store.
     const __amdgpu_buffer_rsrc_t dyrsrc = src_rsrc(dy);
-    int pro0 = -1, pro1 = -1;  // per set: pixel-image channel offset of the prologue, -1 = none
-    auto load = [&](long long kt, float4 (&ra)[2], float4 (&rb)[2], int& pro) {
-        long long p = kt * BKP + kr;
-        const bool pok = p < P;
+    int pro0[NSUB], pro1[NSUB];  // per set and sub-tile: pixel-image channel offset of the prologue, -1 = none
+    auto load = [&](long long kt, float4 (&ra)[2 * NSUB], float4 (&rb)[2 * NSUB], int (&pro)[NSUB]) {
+#pragma unroll
+      for (int sub = 0; sub < NSUB; ++sub) {
+        long long p = MMA == MMA_BF16P ? px_beg + kt * (3 * BKP) + sub * BKP + kr : kt * BKP + kr;
+        const bool pok = p < (MMA == MMA_BF16P ? px_end : P);
         const int co = m0 + cc;
         if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            ra[i] = buf_load4(dyrsrc, (pok && co + 4 * i < d.Co) ? (int)((p * d.Co + co + 4 * i) * 4) : OOB_OFF);
+            ra[2 * sub + i] = buf_load4(dyrsrc, (pok && co + 4 * i < d.Co) ? (int)((p * d.Co + co + 4 * i) * 4) : OOB_OFF);
         // sub-pixel phases: the tap offsets already include the padding
         const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
         const int vx = d.parity == 2 ? pqx + badx : pqx * d.stride - d.pl + badx;
@@ -2233,8 +2245,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         const bool ok = pok && bcol_ok && yok && xok;
         const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) rb[i] = buf_load4(rsrc, off + 16 * i);
-        pro = (d.pro_act != DCS_ACT_NONE && ok) ? pn * d.Cs + bchan : -1;
+        for (int i = 0; i < 2; ++i) rb[2 * sub + i] = buf_load4(rsrc, off + 16 * i);
+        pro[sub] = (d.pro_act != DCS_ACT_NONE && ok) ? pn * d.Cs + bchan : -1;
         // next k-tile: at most one row wrap (the dispatch requires Mx >= BKP), as selects so the
         // tile body stays one basic block
         pqx += BKP;
@@ -2244,17 +2256,36 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         const bool wy = pqy == g.My;
         pqy = wy ? 0 : pqy;
         pn += wy ? 1 : 0;
+      }
     };
-    auto store = [&](int buf, const float4 (&ra)[2], const float4 (&rbl)[2], int pro) {
+    auto store = [&](int buf, const float4 (&ra)[2 * NSUB], const float4 (&rbl)[2 * NSUB], const int (&pro)[NSUB]) {
+        if constexpr (MMA == MMA_BF16P) {
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                const floatx8 fa = {ra[2 * sub].x, ra[2 * sub].y, ra[2 * sub].z, ra[2 * sub].w,
+                                    ra[2 * sub + 1].x, ra[2 * sub + 1].y, ra[2 * sub + 1].z, ra[2 * sub + 1].w};
+                *reinterpret_cast<bf16x8*>(X + xo(0, sub, buf, kr, cc)) = __builtin_convertvector(fa, bf16x8);
+                float4 rb[2] = {rbl[2 * sub], rbl[2 * sub + 1]};
+                if (d.pro_act != DCS_ACT_NONE && pro[sub] >= 0) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        rb[i] = affine_act4(rb[i], psc + pro[sub] + 4 * i, psh + pro[sub] + 4 * i, d.pro_act);
+                }
+                const floatx8 fb = {rb[0].x, rb[0].y, rb[0].z, rb[0].w, rb[1].x, rb[1].y, rb[1].z, rb[1].w};
+                *reinterpret_cast<bf16x8*>(X + xo(1, sub, buf, kr, cc)) = __builtin_convertvector(fb, bf16x8);
+            }
+            return;
+        }
         bf16x8 hi, mid, lo;
         split8x3(ra[0], ra[1], hi, mid, lo);
         *reinterpret_cast<bf16x8*>(X + xo(0, 0, buf, kr, cc)) = hi;
         *reinterpret_cast<bf16x8*>(X + xo(0, 1, buf, kr, cc)) = mid;
         *reinterpret_cast<bf16x8*>(X + xo(0, 2, buf, kr, cc)) = lo;
         float4 rb[2] = {rbl[0], rbl[1]};
-        if (d.pro_act != DCS_ACT_NONE && pro >= 0) {
+        if (d.pro_act != DCS_ACT_NONE && pro[0] >= 0) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) rb[i] = affine_act4(rb[i], psc + pro + 4 * i, psh + pro + 4 * i, d.pro_act);
+            for (int i = 0; i < 2; ++i)
+                rb[i] = affine_act4(rb[i], psc + pro[0] + 4 * i, psh + pro[0] + 4 * i, d.pro_act);
         }
         split8x3(rb[0], rb[1], hi, mid, lo);
         *reinterpret_cast<bf16x8*>(X + xo(1, 0, buf, kr, cc)) = hi;
@@ -2283,9 +2314,28 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    auto tile = [&](long long kt, float4 (&nra)[2], float4 (&nrb)[2], int& npro, const float4 (&ora)[2],
-                    const float4 (&orb)[2], int opro) {
+    auto tile = [&](long long kt, float4 (&nra)[2 * NSUB], float4 (&nrb)[2 * NSUB], int (&npro)[NSUB],
+                    const float4 (&ora)[2 * NSUB], const float4 (&orb)[2 * NSUB], const int (&opro)[NSUB]) {
         const int cur = (int)((kt - kt_beg) & 1);
+        if constexpr (MMA == MMA_BF16P) {
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                bf16x8 fa[IM], fb[JN];
+#pragma unroll
+                for (int i = 0; i < IM; ++i) fa[i] = frag(0, sub, cur, wm * WM + i * 32);
+#pragma unroll
+                for (int j = 0; j < JN; ++j) fb[j] = frag(1, sub, cur, wn * WN + j * 32);
+                if (sub == 0) load(kt + 2, nra, nrb, npro);
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+            store(cur ^ 1, ora, orb, opro);
+            __syncthreads();
+            return;
+        }
         bf16x8 ah[IM], am[IM], al[IM], bh[JN], bm[JN], bl[JN];
 #pragma unroll
         for (int i = 0; i < IM; ++i) {
@@ -2457,7 +2507,10 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
-        if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
+            if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        } else if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
     } else if (p.BM == 128) {
         if (vec && res) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, dy, x, x2, psc, psh, w, p.kt_per_split, gn, gm);
