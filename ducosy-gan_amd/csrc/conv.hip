@@ -150,6 +150,9 @@ constexpr int NT = 256;
 #ifndef DCS_BF16P
 #define DCS_BF16P 1  // half-precision residual convs on the x6 pipeline (48 k per barrier)
 #endif
+#ifndef DCS_BF16P_ROWS
+#define DCS_BF16P_ROWS 1  // the residual rows passes too (else the plain bf16 rows kernel)
+#endif
 #ifndef DCS_BF16P_BM256
 #define DCS_BF16P_BM256 1  // ... on 256-row tiles where they divide the pixels
 #endif
@@ -2041,7 +2044,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
         return check_launch("conv_rows");
     }
-    if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
+    if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && DCS_BF16P_ROWS && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
         // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier; 256-row
         // tiles where they divide the pixels (the forward)
         if (DCS_BF16P_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
