@@ -4,6 +4,13 @@
 // then a fixed-order merge) and therefore deterministic.
 #include "common.hpp"
 
+#ifndef DCS_NORM_BATCH
+#define DCS_NORM_BATCH 1  // IN apply / backward apply: whole-block fast path with every load issued first
+#endif
+#ifndef DCS_NORM_PUNROLL
+#define DCS_NORM_PUNROLL 1  // IN backward partial sums: pixel-loop unroll (4 measured 1.5 % slower)
+#endif
+
 namespace dcs {
 
 // Part (one chunk's statistics of one (n,c)): common.hpp, shared with the conv epilogue
@@ -252,6 +259,25 @@ __global__ __launch_bounds__(256) void in_apply_pow2_kernel(const float4* __rest
     const float* b = sh + (long long)n * (cmask + 1);
     const float4* xs = x + (long long)n * per_n4;
     float4* os = out + (long long)n * per_n4;
+    const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    if (DCS_NORM_BATCH && i0 + 768 < per_n4) {  // whole block in range: the 4 loads issued together
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = xs[i0 + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = ((i0 + 256 * u) * 4) & cmask;
+            const float4 s4 = *reinterpret_cast<const float4*>(s + c);
+            const float4 b4 = *reinterpret_cast<const float4*>(b + c);
+            float4 o;
+            o.x = act_apply(fmaf(v[u].x, s4.x, b4.x), ACT);
+            o.y = act_apply(fmaf(v[u].y, s4.y, b4.y), ACT);
+            o.z = act_apply(fmaf(v[u].z, s4.z, b4.z), ACT);
+            o.w = act_apply(fmaf(v[u].w, s4.w, b4.w), ACT);
+            os[i0 + 256 * u] = o;
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
@@ -330,6 +356,7 @@ __global__ __launch_bounds__(256) void in_bwd_partial_v4_kernel(const float4* __
     const float s[4] = {s4.x, s4.y, s4.z, s4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
     const long long base = (long long)n * HW * cq + c4;
     float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll DCS_NORM_PUNROLL
     for (int p = p0 + plane; p < p1; p += lanes) {
         const float4 g4 = da[base + (long long)p * cq], y4 = y[base + (long long)p * cq];
         const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
@@ -381,6 +408,35 @@ __global__ __launch_bounds__(256) void in_bwd_apply_pow2_kernel(const float4* __
     const int n = blockIdx.y;
     const int C = cmask + 1;
     const long long off = (long long)n * per_n4;
+    const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    if (DCS_NORM_BATCH && i0 + 768 < per_n4) {  // whole block in range: the 8 loads issued together
+        float4 g4u[4], y4u[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            g4u[u] = da[off + i0 + 256 * u];
+            y4u[u] = y[off + i0 + 256 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = ((i0 + 256 * u) * 4) & cmask;
+            const float4 s4 = *reinterpret_cast<const float4*>(sc + n * C + c);
+            const float4 b4 = *reinterpret_cast<const float4*>(sh + n * C + c);
+            const Sum2* k = coef + n * C + c;
+            const float gv[4] = {g4u[u].x, g4u[u].y, g4u[u].z, g4u[u].w};
+            const float yv[4] = {y4u[u].x, y4u[u].y, y4u[u].z, y4u[u].w};
+            const float s[4] = {s4.x, s4.y, s4.z, s4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float xh = fmaf(yv[e], s[e], b[e]);
+                const float g = gv[e] * act_grad(xh, ACT);
+                const Sum2 kk = k[e];
+                o[e] = s[e] * (g - kk.a - xh * kk.b);
+            }
+            dy[off + i0 + 256 * u] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
