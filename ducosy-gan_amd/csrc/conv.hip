@@ -156,6 +156,9 @@ constexpr int NT = 256;
 #ifndef DCS_BF16P_BM256
 #define DCS_BF16P_BM256 1  // ... on 256-row tiles where they divide the pixels
 #endif
+#ifndef DCS_WGRAD_REDUCE_UNROLL
+#define DCS_WGRAD_REDUCE_UNROLL 8
+#endif
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
@@ -1696,6 +1699,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, in
     const int tap = k / Cs, ci = k - tap * Cs;
     float s = 0.f;
     if (ci >= Cw) return;  // zero-padded source channel (no weight)
+    // loads hoisted 8 at a time, the additions kept in split order (bit-identical sums)
+#pragma unroll DCS_WGRAD_REDUCE_UNROLL
     for (int q = 0; q < nsplit; ++q) s += ws[(long long)q * total + idx];
     dw[((long long)co * Cw + ci) * taps + tap] = s;
 }
