@@ -10,6 +10,10 @@
 // float4 columns with pixel lanes folded through LDS.
 #include "common.hpp"
 
+#ifndef DCS_SERIAL_UNROLL
+#define DCS_SERIAL_UNROLL 8  // serial fixed-order reductions: loads hoisted, additions in order
+#endif
+
 namespace dcs {
 
 // ---- channel attention MLP (one block per image) ----------------------------------------
@@ -314,6 +318,7 @@ __global__ __launch_bounds__(256) void cb_bwd_dwsa_partial_kernel(const float* _
     const long long p0 = chunk * per, p1 = min(P, p0 + per);
     const int HW = H * W;
     float acc = 0.f;
+#pragma unroll 4
     for (long long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
         int n = (int)(p / HW);
         int rem = (int)(p - (long long)n * HW);
@@ -330,6 +335,7 @@ __global__ void cb_bwd_dwsa_final_kernel(const float* __restrict__ part, int nt,
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nt) return;
     double s = 0.0;
+#pragma unroll DCS_SERIAL_UNROLL
     for (int k = 0; k < nchunk; ++k) s += part[(long long)k * nt + t];
     dwsa[t] = (float)s;
 }
@@ -469,6 +475,7 @@ __global__ __launch_bounds__(256) void cb_bwd_ca_kernel(const Sum3* __restrict__
     for (int c = tid; c < C; c += blockDim.x) {
         const long long nc = (long long)n * C + c;
         double A = 0.0, B = 0.0, Cc = 0.0;
+#pragma unroll DCS_SERIAL_UNROLL
         for (int k = 0; k < nchunk; ++k) {
             Sum3 p = parts[((long long)n * nchunk + k) * C + c];
             A += p.a; B += p.b; Cc += p.c;
@@ -518,6 +525,7 @@ __global__ void cb_bwd_dw_reduce_kernel(const float* __restrict__ dwpart, int N,
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 2 * CCr) return;
     float s = 0.f;
+#pragma unroll DCS_SERIAL_UNROLL
     for (int n = 0; n < N; ++n) s += dwpart[(long long)n * 2 * CCr + i];
     if (i < CCr) dw1[i] = s;
     else dw2[i - CCr] = s;

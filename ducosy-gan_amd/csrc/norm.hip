@@ -387,6 +387,7 @@ __global__ __launch_bounds__(256) void in_bwd_finalize8_kernel(const Sum2* __res
     const int n = live ? idx / C : 0, c = live ? idx - n * C : 0;
     double a = 0.0, b = 0.0;
     if (live)
+#pragma unroll 4
         for (int k = sub; k < nchunk; k += 8) {
             const Sum2 p = parts[((long long)n * nchunk + k) * C + c];
             a += p.a;
