@@ -314,18 +314,19 @@ __global__ __launch_bounds__(256) void cb_bwd_dwsa_partial_kernel(const float* _
     const int taps = ksa * ksa, r = ksa / 2;
     const int ch = t / taps, tt = t - ch * taps;
     const int ty = tt / ksa, tx = tt - ty * ksa;
-    const long long per = (P + nchunk - 1) / nchunk;
-    const long long p0 = chunk * per, p1 = min(P, p0 + per);
+    // 32-bit pixel index math (the host guarantees P < 2^31)
+    const int per = (int)((P + nchunk - 1) / nchunk);
+    const int p0 = chunk * per, p1 = (int)min(P, (long long)p0 + per);
     const int HW = H * W;
     float acc = 0.f;
 #pragma unroll 4
-    for (long long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        int n = (int)(p / HW);
-        int rem = (int)(p - (long long)n * HW);
-        int py = rem / W, px = rem - py * W;
-        int yy = py + ty - r, xx = px + tx - r;
+    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const int n = p / HW;
+        const int rem = p - n * HW;
+        const int py = rem / W, px = rem - py * W;
+        const int yy = py + ty - r, xx = px + tx - r;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-            acc = fmaf(dpre[p], sin_[((long long)n * HW + yy * W + xx) * 2 + ch], acc);
+            acc = fmaf(dpre[p], sin_[(n * HW + yy * W + xx) * 2 + ch], acc);
     }
     acc = block_sum_256(acc, red);
     if (threadIdx.x == 0) part[(long long)chunk * gridDim.x + t] = acc;
@@ -692,6 +693,8 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
         return fail(DCS_E_INVALID, "cbam_backward: bad dims");
     if (ws_bytes < dcs_cbam_backward_workspace_size(N, H, W, C, Cr, ksa))
         return fail(DCS_E_WORKSPACE, "cbam_backward: workspace too small");
+    if ((long long)N * H * W * 2 >= (1LL << 31))
+        return fail(DCS_E_INVALID, "cbam_backward: N*H*W*2 must fit in 31 bits");
     CbWs w = cb_layout(ws, N, H, W, C, Cr, ksa);
     hipStream_t s = as_stream(stream);
     const long long P = (long long)N * H * W;
