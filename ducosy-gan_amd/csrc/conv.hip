@@ -1815,21 +1815,22 @@ __device__ __forceinline__ int reflect_pre(int i, int H, int pad, int* a) {
 
 __global__ void reflect_fold_kernel(const float* __restrict__ dxp, const float* __restrict__ add,
                                     float* __restrict__ dx, int N, int H, int W, int C4, int pad) {
-    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    long long total = (long long)N * H * W * C4;
+    // 32-bit index math (the host guarantees N*(H+2p)*(W+2p)*C4 < 2^31)
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = N * H * W * C4;
     if (idx >= total) return;
-    int c4 = (int)(idx % C4);
-    long long t = idx / C4;
-    int j = (int)(t % W); t /= W;
-    int i = (int)(t % H);
-    int n = (int)(t / H);
+    const int c4 = idx % C4;
+    int t = idx / C4;
+    const int j = t % W; t /= W;
+    const int i = t % H;
+    const int n = t / H;
     const int Hp = H + 2 * pad, Wp = W + 2 * pad;
     int ay[3], ax[3];
     int ny = reflect_pre(i, H, pad, ay), nx = reflect_pre(j, W, pad, ax);
     float4 s = add ? reinterpret_cast<const float4*>(add)[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = 0; p < ny; ++p)
         for (int q = 0; q < nx; ++q) {
-            float4 v = reinterpret_cast<const float4*>(dxp)[(((long long)n * Hp + ay[p]) * Wp + ax[q]) * C4 + c4];
+            float4 v = reinterpret_cast<const float4*>(dxp)[((n * Hp + ay[p]) * Wp + ax[q]) * C4 + c4];
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
     reinterpret_cast<float4*>(dx)[idx] = s;
@@ -2669,7 +2670,7 @@ extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* 
     if (!dxpad || !dx || N <= 0 || H <= 0 || W <= 0 || C <= 0 || pad < 0 || pad > 3 || pad >= H || pad >= W)
         return fail(DCS_E_INVALID, "reflect_fold: bad arguments");
     hipStream_t s = as_stream(stream);
-    if (C % 4 == 0) {
+    if (C % 4 == 0 && (long long)N * (H + 2 * pad) * (W + 2 * pad) * (C / 4) < (1LL << 31)) {
         long long total = (long long)N * H * W * (C / 4);
         hipLaunchKernelGGL(reflect_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dxpad, addend, dx,
                            N, H, W, C / 4, pad);
