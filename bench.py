@@ -39,11 +39,13 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, den
 BF16_MFMA_PEAK_TFLOPS = 16 * F32_MFMA_PEAK_TFLOPS  # v_mfma_f32_32x32x16_bf16: 16x the f32 rate (~2.5 PF dense)
 # peak per mode for the dominant kernel's algorithmic FLOPs: bf16x3 issues 3 bf16 MFMAs per product
 MODE_PEAK = {"f32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3,
-             "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6}
+             "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6, "f16x3": BF16_MFMA_PEAK_TFLOPS / 3}
 MODE_DTYPE = {"f32": "f32", "bf16": "bf16 (MFMA operands; f32 accumulation and storage)",
               "bf16x3": "f32 via bf16x3 MFMA (hi/lo split, ~2^-16 per product; f32 accumulation and storage)",
-              "bf16x6": "f32 via bf16x6 MFMA (hi/mid/lo split, ~2^-24 per product; f32 accumulation and storage)"}
-MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6}
+              "bf16x6": "f32 via bf16x6 MFMA (hi/mid/lo split, ~2^-24 per product; f32 accumulation and storage)",
+              "f16x3": "f32 via f16x3 MFMA (power-of-two scaled hi/lo fp16 split, 22 significant bits, three "
+                       "products; f32 accumulation and storage)"}
+MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6, "f16x3": 7}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -102,7 +104,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=9)
     ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mma", default="bf16x6", choices=["f32", "bf16", "bf16x3", "bf16x6"],
+    ap.add_argument("--mma", default="bf16x6", choices=["f32", "bf16", "bf16x3", "bf16x6", "f16x3"],
                     help="MFMA operand mode of the conv passes: bf16x6 = three-way split, fp32-class "
                          "(default; error <= the exact-f32 path's, tests/test_gpu_mma.py), f32 = exact "
                          "fp32 MFMA, bf16x3 = hi/lo split, bf16 = plain bf16 operands")
@@ -227,7 +229,7 @@ def main():
             "roofline": {
                 "kernel": (f"256-ch 3x3 residual conv rows pass: forward conv_rows_kernel<256,128,1,1,{MODE_TAG[args.mma]}>, "
                            f"data gradient conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}>"
-                           if args.mma == "bf16x6" else
+                           if args.mma in ("bf16x6", "f16x3") else
                            f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)"),
                 "bound": "mfma",
                 "achieved": round(achieved, 3),

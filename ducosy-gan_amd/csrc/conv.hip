@@ -32,6 +32,9 @@ constexpr int MMA_F32 = 0, MMA_BF16 = 1, MMA_BF16X3 = 3, MMA_BF16X6 = 6;
 // internal: DCS_MMA_BF16 on the bf16x6 pipeline with its three LDS planes used as three
 // consecutive 16-k sub-tiles (48 k per barrier, one product each), for the residual convs
 constexpr int MMA_BF16P = 2;
+// f16x3 (DCS_MMA_F16X3): fp32 operands scaled by a power of two and split into hi + lo fp16,
+// three products on v_mfma_f32_32x32x16_f16 (include/ducosy_hip.h)
+constexpr int MMA_F16X3 = 7;
 #ifndef DCS_BF16_BUFGATHER
 #define DCS_BF16_BUFGATHER 1  // branch-free buffer-descriptor gather in the bf16 rows pass
 #endif
@@ -89,6 +92,37 @@ __device__ __forceinline__ void split8x3(const float4& a, const float4& b, bf16x
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// f16x3 split: v' = v * 2^s (exact), hi = fp16(v'), lo = fp16(v' - hi) (the residual is exact in
+// fp32; |v' - hi - lo| <= 2^-22 |v'| while |v'| < 2^15 and lo is normal, else an absolute
+// 2^-25 floor from the fp16 denormals, far below the tensor's 2^15 top)
+__device__ __forceinline__ void split8h(const float4& a, const float4& b, float sc, f16x8& hi, f16x8& lo) {
+    const floatx8 f = floatx8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w} * sc;
+    hi = __builtin_convertvector(f, f16x8);
+    lo = __builtin_convertvector(f - __builtin_convertvector(hi, floatx8), f16x8);
+}
+__device__ __forceinline__ void split4h(const float4& a, float sc, f16x4& hi, f16x4& lo) {
+    const f32x4v f = f32x4v{a.x, a.y, a.z, a.w} * sc;
+    hi = __builtin_convertvector(f, f16x4);
+    lo = __builtin_convertvector(f - __builtin_convertvector(hi, f32x4v), f16x4);
+}
+
+// f16x3 operand exponent: s with max|operand| * 2^s < 2^15, from the n (<= 1024) partial
+// maxima of the operand's range record (every wave reduces them itself; wave-uniform result)
+__device__ __forceinline__ int f16x3_exp(const float* __restrict__ rng, int n) {
+    const int lane = threadIdx.x & 63;
+    float m = 0.f;
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, rng[i]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    int e = 0;
+    (void)frexpf(m, &e);  // m = f * 2^e, 0.5 <= f < 1 (e = 0 for m = 0)
+    int sh = 15 - e;
+    sh = sh < -100 ? -100 : (sh > 100 ? 100 : sh);
+    return __builtin_amdgcn_readfirstlane(sh);
+}
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x4v unpack4(const bf16x4& h) {
     u32x2v w;
@@ -349,14 +383,10 @@ __device__ __forceinline__ float gather1(const dcs_conv_desc& d, const float* __
 // ---------------------------------------------------------------------------------------
 // weight packing
 // ---------------------------------------------------------------------------------------
-__global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
-                                    int kind, int ci_count, int Kpad, int ncols, int nmajor,
-                                    float* __restrict__ out) {
+__device__ __forceinline__ float pack_value(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
+                                           int kind, int ci_count, int Kpad, int ncols, int nmajor, long long idx) {
     // element (k, col) of the logical [Kpad][ncols] GEMM B matrix; stored N-major
     // ([ncols][Kpad], MFMA rows pass) or K-major ([Kpad][ncols], narrow kernels)
-    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    long long total = (long long)Kpad * ncols;
-    if (idx >= total) return;
     int k, col;
     if (nmajor) { col = (int)(idx / Kpad); k = (int)(idx - (long long)col * Kpad); }
     else { k = (int)(idx / ncols); col = (int)(idx - (long long)k * ncols); }
@@ -428,7 +458,35 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int C
             v = w[(((long long)co * Cin + col) * KH + ty) * KW + tx];
         }
     }
-    out[idx] = v;
+    return v;
+}
+
+__global__ void pack_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
+                                    int kind, int ci_count, int Kpad, int ncols, int nmajor,
+                                    float* __restrict__ out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)Kpad * ncols) return;
+    out[idx] = pack_value(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, idx);
+}
+
+// the same over a DCS_RANGE_PARTS-block grid-stride walk, each block also writing the max
+// |value| it packed (the rng_b range record of an f16x3 rows pass over these weights)
+__global__ __launch_bounds__(256) void pack_weights_r_kernel(const float* __restrict__ w, int Cout, int Cin, int KH,
+                                                             int KW, int kind, int ci_count, int Kpad, int ncols,
+                                                             int nmajor, float* __restrict__ out,
+                                                             float* __restrict__ rng) {
+    const long long total = (long long)Kpad * ncols;
+    float m = 0.f;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const float v = pack_value(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, idx);
+        out[idx] = v;
+        m = fmaxf(m, fabsf(v));
+    }
+    __shared__ float red[4];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) rng[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -635,26 +693,26 @@ __device__ __forceinline__ void rows_in_stats(const dcs_conv_desc& d, const floa
 // bf16x6 rows k-loop body: the fragment reads first, then each MFMA followed by DCS_X6_SGB
 // VALU instructions (the next tile's split and address arithmetic), then the LDS stores, so the
 // split runs in the shadow of the wave's own MFMAs instead of after them (0 = compiler order)
-template <int NMFMA, int NV>
+template <int NMFMA, int NV, int NDSR = 12, int NDSW = 6>
 __device__ __forceinline__ void x6_interleave() {
     if constexpr (NV > 0) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x100, NDSR, 0);  // DS read
 #pragma unroll
         for (int i = 0; i < NMFMA; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
         }
-        __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);  // DS write
+        __builtin_amdgcn_sched_group_barrier(0x200, NDSW, 0);  // DS write
     }
 }
 
 template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
-__global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
+__global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts, int fold) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P) && BN == 128 && VEC == 1),
+    static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P || MMA == MMA_F16X3) && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
     constexpr int NTH = 2 * BM;                    // threads (two per A row)
     constexpr int WM = 64, WN = BN / 2;            // per-wave tile
@@ -662,8 +720,14 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     constexpr int BTPR = NTH / BN;                 // B loader threads per row (2 or 4)
     // bf16: 64-deep k-tiles (twice the MFMA work per round of global loads: the bf16 passes are
     // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
-    constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : (MMA == MMA_BF16P ? 48 : BK);  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
-    constexpr bool X6L = MMA == MMA_BF16X6 || MMA == MMA_BF16P;  // the x6 LDS planes and pipeline
+    // f16x3 (H3): two fp16 planes; the vectorised gathers stage two 16-k sub-tiles per barrier
+    // (32 k: the MFMAs per barrier of the 16-k bf16x6 tile), the 4-channel stem one
+    constexpr bool H3 = MMA == MMA_F16X3;
+    constexpr int NSUB = (H3 && VEC == 1) ? 2 : 1;  // 16-k sub-tiles per k-tile (split-at-store modes)
+    constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : (MMA == MMA_BF16P ? 48 : (H3 ? 16 * NSUB : BK));  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
+    constexpr bool X6L = MMA == MMA_BF16X6 || MMA == MMA_BF16P || H3;  // the x6 LDS planes and pipeline
+    constexpr bool X6F = MMA == MMA_BF16X6 || H3;  // operands split at the LDS store (prologue deferred there)
+    constexpr int NSLOT = H3 ? 2 * NSUB : 3;       // LDS planes per buffer: [plane][sub] (H3), else 3
     constexpr int AKPT = BKT / 2;                  // k per A-loader thread (2 threads per row)
     constexpr int ACH = AKPT / 4;                  // float4 per A-loader thread
     constexpr int BKPT = BKT / BTPR;               // k per B-loader thread
@@ -677,7 +741,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // odd groups of 8 rows, so both the 8-lane ds_write_b128 groups and the 16-lane
     // ds_read_b128 groups hit 64 distinct banks (MI355X_MICROARCH.md LDS table)
     constexpr int LDS_FLOATS = MMA == MMA_F32 ? 2 * (BM + BN) * LDK
-                             : X6L ? 3 * 2 * (BM + BN) * 16 / 2 : (BM + BN) * LDE;
+                             : X6L ? NSLOT * 2 * (BM + BN) * 16 / 2 : (BM + BN) * LDE;
 
     // f32: As[2][BM][LDK] | Bs[2][BN][LDK];  bf16 modes: Ah[2][BM][LDE] | Bh[2][BN][LDE]
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
@@ -693,7 +757,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // bf16x6 prologue (TAG 0): the per-(image, channel) scale / shift of the <= 2 images a tile
     // spans, staged once, so the affine at the LDS store reads LDS instead of issuing global
     // loads that would wait behind the prefetched gathers
-    constexpr bool PRO_LDS = MMA == MMA_BF16X6 && TAG != 1;
+    constexpr bool PRO_LDS = X6F && TAG != 1;
     constexpr int PRO_CMAX = 512;
     __shared__ __attribute__((aligned(16))) float prol[PRO_LDS ? 4 * PRO_CMAX : 4];
 
@@ -714,12 +778,12 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 
     // A loader: one row, 16 consecutive k (VEC: Cs % 16 == 0, so the 16 k share one tap); BF16P:
     // 8 k of each of the tile's three 16-k sub-tiles
-    const int arow = tid >> 1, akq = (tid & 1) * (MMA == MMA_BF16P ? 8 : AKPT);
+    const int arow = tid >> 1, akq = (tid & 1) * ((MMA == MMA_BF16P || NSUB > 1) ? 8 : AKPT);
     const RowInfo ri = row_info(d, g, (int)(m0 + arow), fold);
     const bool rvalid = ri.out_off >= 0;
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
     // B loader: one output channel row, BKPT consecutive k
-    const int brow = tid / BTPR, bkq = (tid % BTPR) * (MMA == MMA_BF16P ? 16 / BTPR : BKPT);
+    const int brow = tid / BTPR, bkq = (tid % BTPR) * ((MMA == MMA_BF16P || NSUB > 1) ? 16 / BTPR : BKPT);
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
     const int K = g.ntaps * d.Cs;
@@ -728,6 +792,15 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     const float* srow = src + ri.n * d.s_n;
     const long long so = (long long)ri.n * d.Cs;
     const __amdgpu_buffer_rsrc_t arsrc = src_rsrc(src);
+    // f16x3 operand scales 2^ea, 2^eb and the exponent that undoes them in the epilogue
+    float asc = 1.f, bsc = 1.f;
+    int eab = 0;
+    if constexpr (H3) {
+        const int ea = f16x3_exp(d.rng_a, d.rng_a_n), eb = f16x3_exp(d.rng_b, d.rng_b_n);
+        asc = __builtin_ldexpf(1.f, ea);
+        bsc = __builtin_ldexpf(1.f, eb);
+        eab = -(ea + eb);
+    }
     bool pro_lds = false;  // block-uniform
     int pro_base = 0;      // n_lo * Cs: psc/psh index of prol[0]
     if constexpr (PRO_LDS) {
@@ -754,7 +827,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
     // L1/L2 instead of after a sweep over all channels (the dispatch requires d.korder == SLICE)
     // TAG 0 bf16x6 kernels with 16-channel-aligned sources walk the same slice-major order over
     // tap-major packed weights (KSB: the B column is rebuilt from (tap, channel) per k-tile)
-    constexpr bool KSB = TAG != 1 && MMA == MMA_BF16X6 && VEC == 1 && DCS_KSLICE_ALL;
+    constexpr bool KSB = TAG != 1 && X6F && VEC == 1 && DCS_KSLICE_ALL;
     constexpr bool KS = TAG == 1 || KSB;
     int aj, ac;
     if constexpr (KS) {
@@ -783,14 +856,25 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             while (c >= d.Cs) { c -= d.Cs; ++j; }
         }
     };
+    // one 16-k sub-tile step (NSUB > 1); equal to advance for 16-k tiles
+    auto advance16 = [&](int& j, int& c) {
+        if constexpr (KS) {
+            j += 1;
+            if (j >= g.ntaps) { j -= g.ntaps; c += 16; }
+        } else {
+            c += 16;
+            while (c >= d.Cs) { c -= d.Cs; ++j; }
+        }
+    };
 
     float4 ra[ACH];
     float4 rb[BCH];
 
     // pa: bf16x6 defers the prologue affine to the LDS store (a load consumed at once would make
     // the next tile's gather wait); it records the channel offset into psc/psh, -1 for none
-    auto load_a = [&](int kt, auto& dst, int& pa) {
-        pa = -1;
+    auto load_a = [&](int kt, auto& dst, int (&pa)[NSUB]) {
+#pragma unroll
+        for (int q = 0; q < NSUB; ++q) pa[q] = -1;
         if (VEC == 2) {  // Cs == 4: taps aj .. aj+ACH-1, one float4 each (no prologue)
 #pragma unroll
             for (int e = 0; e < ACH; ++e) dst[e] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -827,12 +911,30 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 aj = wrap ? 0 : aj + 1;
                 ac += wrap ? 16 : 0;
             }
+        } else if (VEC && NSUB > 1) {
+            // f16x3: NSUB 16-k sub-tiles (the next tap of the slice, or the next 16 channels), 8 k
+            // per thread each, by the branch-free select gather of the bf16x6 tiles below
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                const bool kin = aj < g.ntaps && ac < d.Cs;
+                int ady, adx, bt, sy = 0, sx = 0;
+                tap_decode(d, g, kin ? aj : 0, ady, adx, bt);
+                const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                const int off = (kin && rvalid && yok && xok)
+                                    ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4
+                                    : OOB_OFF;
+                dst[2 * sub] = buf_load4(arsrc, off);
+                dst[2 * sub + 1] = buf_load4(arsrc, off + 16);
+                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[sub] = (int)so + ac;
+                advance16(aj, ac);
+            }
         } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
             // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
             int sy = 0, sx = 0, off = OOB_OFF;
             // past the last k-tile (the x6 pipeline's unconditional prefetch) the walk leaves the
             // range through aj (tap-major) or through ac (slice-major): both must stay in range
-            if constexpr (MMA == MMA_BF16X6 && DCS_X6_SELGATHER) {
+            if constexpr (X6F && DCS_X6_SELGATHER) {
                 // select form (tap 0 stands in for a tap past the end): no exec-mask branch
                 // splits the k-loop body, so the scheduler can spread the next tile's split
                 // arithmetic over this tile's MFMAs
@@ -852,8 +954,8 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             }
 #pragma unroll
             for (int i = 0; i < ACH; ++i) dst[i] = buf_load4(arsrc, off + 16 * i);
-            if constexpr (MMA == MMA_BF16X6) {
-                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa = (int)so + ac;
+            if constexpr (X6F) {
+                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[0] = (int)so + ac;
             } else if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
 #pragma unroll
                 for (int i = 0; i < ACH; ++i) dst[i] = affine_act4(dst[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
@@ -912,6 +1014,27 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             }
             return;
         }
+        if constexpr (NSUB > 1) {  // f16x3 sub-tiles: BKPT / NSUB k of each 16-k sub-tile
+            constexpr int BQ = BCH / NSUB;
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                long long col;
+                bool ok = true;
+                if (!d.parity && !KSB) {
+                    col = (long long)kt * BKT + 16 * sub + bkq;
+                } else {
+                    ok = bj < g.ntaps && bc < d.Cs;
+                    int ady, adx, bt = 0;
+                    if (ok) tap_decode(d, g, bj, ady, adx, bt);
+                    col = (long long)bt * d.Cs + bc;
+                    advance16(bj, bc);
+                }
+                const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
+#pragma unroll
+                for (int q = 0; q < BQ; ++q) dst[BQ * sub + q] = buf_load4(brsrc, off + 16 * q);
+            }
+            return;
+        }
         long long col;
         bool ok = true;
         if (!d.parity && !KSB) {
@@ -923,7 +1046,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             col = (long long)bt * d.Cs + bc;
             advance(bj, bc);
         }
-        if constexpr (MMA == MMA_BF16X6 && DCS_BF16_BUFGATHER) {  // branch-free: k-tiles past the end read zeros
+        if constexpr (X6F && DCS_BF16_BUFGATHER) {  // branch-free: k-tiles past the end read zeros
             const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
 #pragma unroll
             for (int i = 0; i < BCH; ++i) dst[i] = buf_load4(brsrc, off + 16 * i);
@@ -934,20 +1057,26 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    auto store_tiles = [&](int buf, const auto& sa0, const auto& sb, int pa) {
+    auto store_tiles = [&](int buf, const auto& sa0, const auto& sb, const int (&pa)[NSUB]) {
         float4 sa[ACH];
 #pragma unroll
         for (int i = 0; i < ACH; ++i) sa[i] = sa0[i];
-        if constexpr (MMA == MMA_BF16X6) {
-            if (d.pro_act != DCS_ACT_NONE && pa >= 0) {
-                if (pro_lds) {
-                    const int q = pa - pro_base;
+        if constexpr (X6F) {
+            constexpr int AQ = ACH / NSUB;  // float4 of one sub-tile
 #pragma unroll
-                    for (int i = 0; i < ACH; ++i)
-                        sa[i] = affine_act4(sa[i], prol + q + 4 * i, prol + 2 * PRO_CMAX + q + 4 * i, d.pro_act);
-                } else {
+            for (int sub = 0; sub < NSUB; ++sub) {
+                const int pq = pa[sub];
+                if (d.pro_act != DCS_ACT_NONE && pq >= 0) {
+                    if (pro_lds) {
+                        const int q = pq - pro_base;
 #pragma unroll
-                    for (int i = 0; i < ACH; ++i) sa[i] = affine_act4(sa[i], psc + pa + 4 * i, psh + pa + 4 * i, d.pro_act);
+                        for (int i = 0; i < AQ; ++i)
+                            sa[AQ * sub + i] = affine_act4(sa[AQ * sub + i], prol + q + 4 * i, prol + 2 * PRO_CMAX + q + 4 * i, d.pro_act);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < AQ; ++i)
+                            sa[AQ * sub + i] = affine_act4(sa[AQ * sub + i], psc + pq + 4 * i, psh + pq + 4 * i, d.pro_act);
+                    }
                 }
             }
         }
@@ -975,27 +1104,36 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                         __builtin_convertvector(f4, bf16x4);
                 }
             }
+        } else if constexpr (H3) {
+            // planes [hi | lo] x sub-tiles: slot = plane * NSUB + sub
+            static_assert(ACH == 2 * NSUB && (BCH == 2 * NSUB || BCH == NSUB), "f16x3 tiles: 8 A and 8 / 4 B per thread per sub-tile");
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                f16x8 hi, lo;
+                split8h(sa[2 * sub], sa[2 * sub + 1], asc, hi, lo);
+                *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, arow, akq >> 3)) = hi;
+                *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, arow, akq >> 3)) = lo;
+                if constexpr (BCH == 2 * NSUB) {
+                    split8h(sb[2 * sub], sb[2 * sub + 1], bsc, hi, lo);
+                    *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = hi;
+                    *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3)) = lo;
+                } else {  // 4 k of B per thread: the 8-byte half of a 16-byte chunk
+                    f16x4 h4, l4;
+                    split4h(sb[sub], bsc, h4, l4);
+                    const int q = 4 * ((bkq >> 2) & 1);
+                    *reinterpret_cast<f16x4*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3) + q) = h4;
+                    *reinterpret_cast<f16x4*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3) + q) = l4;
+                }
+            }
         } else if constexpr (MMA == MMA_BF16X6) {
             static_assert(BKT == 16 && ACH == 2 && (BCH == 2 || BCH == 1), "x6 tiles: 16 k, 8 / 4 per loader thread");
             bf16x8 hi, mid, lo;
-#ifdef DCS_X6_FAKEA
-            {
-                const floatx8 f = {sa[0].x, sa[0].y, sa[0].z, sa[0].w, sa[1].x, sa[1].y, sa[1].z, sa[1].w};
-                hi = mid = lo = __builtin_convertvector(f, bf16x8);
-            }
-#else
             split8x3(sa[0], sa[1], hi, mid, lo);
-#endif
             *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, arow, akq >> 3)) = hi;
             *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, arow, akq >> 3)) = mid;
             *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, arow, akq >> 3)) = lo;
             if constexpr (BCH == 2) {
-#ifdef DCS_X6_FAKEB  // timing experiment only: B conversion without the split arithmetic
-                const floatx8 f = {sb[0].x, sb[0].y, sb[0].z, sb[0].w, sb[1].x, sb[1].y, sb[1].z, sb[1].w};
-                hi = mid = lo = __builtin_convertvector(f, bf16x8);
-#else
                 split8x3(sb[0], sb[1], hi, mid, lo);
-#endif
                 *reinterpret_cast<bf16x8*>(Ah + x6o(0, buf, BM + brow, bkq >> 3)) = hi;
                 *reinterpret_cast<bf16x8*>(Ah + x6o(1, buf, BM + brow, bkq >> 3)) = mid;
                 *reinterpret_cast<bf16x8*>(Ah + x6o(2, buf, BM + brow, bkq >> 3)) = lo;
@@ -1034,7 +1172,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    int pa0 = -1, pa1 = -1;
+    int pa0[NSUB], pa1[NSUB];
     load_a(0, ra, pa0);
     load_b(0, rb);
     store_tiles(0, ra, rb, pa0);
@@ -1062,6 +1200,33 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
 #pragma unroll
                         for (int j = 0; j < JN; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+                return;
+            }
+            if constexpr (H3) {  // per sub-tile: lo*hi, hi*lo, hi*hi (smallest terms first)
+#pragma unroll
+                for (int sub = 0; sub < NSUB; ++sub) {
+                    f16x8 fah[IM], fal[IM], fbh[JN], fbl[JN];
+#pragma unroll
+                    for (int i = 0; i < IM; ++i) {
+                        const int row = wm * WM + i * 32 + l32;
+                        fah[i] = *reinterpret_cast<const f16x8*>(Ah + x6o(sub, cur, row, kh >> 3));
+                        fal[i] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
+                    }
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        const int row = BM + wn * WN + j * 32 + l32;
+                        fbh[j] = *reinterpret_cast<const f16x8*>(Ah + x6o(sub, cur, row, kh >> 3));
+                        fbl[j] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
+                    }
+#pragma unroll
+                    for (int i = 0; i < IM; ++i)
+#pragma unroll
+                        for (int j = 0; j < JN; ++j) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], t[i][j], 0, 0, 0);
+                        }
                 }
                 return;
             }
@@ -1131,7 +1296,7 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
             // buffer descriptors): a load under a branch makes the compiler's vmcnt bookkeeping
             // assume it may be missing and wait for every load at the next LDS store.
             float4 ra2[ACH], rb2[BCH];
-            int pa2 = -1;
+            int pa2[NSUB];
             load_a(1, ra, pa1);
             load_b(1, rb);
             for (int kt = 0; kt < nkt; kt += 2) {
@@ -1142,7 +1307,8 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                     // staging before the chain fold and unconditional (a tile past the end is
                     // zeros into a buffer nobody reads again): one basic block with the MFMAs
                     store_tiles(1, ra, rb, pa1);
-                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : 6), (TAG == 1 && MMA == MMA_BF16X6) ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? 3 * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
+                                  H3 ? (IM + JN) * 2 * NSUB : 12, H3 ? 4 * NSUB : 6>();
                     fold_t(kt);
                 } else {
                     fold_t(kt);
@@ -1155,7 +1321,8 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
                 step(1, 0);
                 if (DCS_X6_STORE_FIRST) {
                     store_tiles(0, ra2, rb2, pa2);
-                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : 6), (TAG == 1 && MMA == MMA_BF16X6) ? DCS_X6_SGB : DCS_X6_SGB0>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? 3 * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
+                                  H3 ? (IM + JN) * 2 * NSUB : 12, H3 ? 4 * NSUB : 6>();
                     fold_t(kt + 1);
                 } else {
                     fold_t(kt + 1);
@@ -1209,6 +1376,14 @@ __global__ __launch_bounds__(2 * BM, MMA == MMA_BF16X6 ? (BM == 256 ? 2 : DCS_X6
         __syncthreads();
     }
 
+    if constexpr (H3) {  // undo the operand scales (exact powers of two)
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+    }
     // epilogue: + bias, activation, NHWC store; in the reflection-fold data gradient
     // (fold, dcs_conv_dgrad_reflect) src2 carries the residual addend of the interior pixels
     const float* addend = fold ? src2 : nullptr;
@@ -1933,8 +2108,11 @@ static int validate(const dcs_conv_desc* d, bool rows) {
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
     if (d->cw < 0 || d->cw > d->Cs) return fail(DCS_E_INVALID, "conv: bad cw (weight channels)");
-    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3 && d->mma != MMA_BF16X6)
-        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16, DCS_MMA_BF16X3 or DCS_MMA_BF16X6");
+    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3 && d->mma != MMA_BF16X6 && d->mma != MMA_F16X3)
+        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16, DCS_MMA_BF16X3, DCS_MMA_BF16X6 or DCS_MMA_F16X3");
+    if (d->mma == MMA_F16X3 && (!d->rng_a || !d->rng_b || d->rng_a_n <= 0 || d->rng_b_n <= 0 ||
+                                d->rng_a_n > 1024 || d->rng_b_n > 1024))
+        return fail(DCS_E_INVALID, "conv: DCS_MMA_F16X3 needs the operand range records rng_a / rng_b (1..1024 partial maxima)");
     if (!d->parity) {
         // output dims must be those of the forward conv over the virtual input
         int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
@@ -1980,8 +2158,15 @@ int launch_narrow_wgrad_tiled(const dcs_conv_desc& d, const float* dy, const flo
 
 using namespace dcs;
 
+extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                                  int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream);
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                 int Kpad, int ncols, int nmajor, float* out, void* stream) {
+    return dcs_pack_weights_r(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out, nullptr, stream);
+}
+
+extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                                  int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream) {
     if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
         (kind != 5 && ci_count > Cin) || (kind == 5 && ci_count < Cin) || kind < 0 ||
         (kind & 7) > 5 || (kind & ~(7 | DCS_PACK_KSLICE)) ||
@@ -1990,8 +2175,12 @@ extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int K
         return fail(DCS_E_INVALID, "pack_weights: bad arguments");
     if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
     long long total = (long long)Kpad * ncols;
-    hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
-                       Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
+    if (rng)
+        hipLaunchKernelGGL(pack_weights_r_kernel, dim3(DCS_RANGE_PARTS), dim3(256), 0, as_stream(stream), w, Cout, Cin,
+                           KH, KW, kind, ci_count, Kpad, ncols, nmajor, out, rng);
+    else
+        hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
+                           Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
     return check_launch("pack_weights");
 }
 
@@ -2031,25 +2220,36 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
                                    "residual geometry with a vectorisable source");
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
-    if (vec && d.mma == MMA_BF16X6 && (BN == 128 || DCS_X6_BN64) && !DCS_ROWS_F32) {  // x6: 128- or 64-column tiles
+    const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3;  // split-at-store pipelines
+#define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
+    if (d.mma == MMA_F16X3)                                                                                          \
+        hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16X3>), G, dim3(2 * BM_), 0, s, d, src, src2, \
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);                                        \
+    else                                                                                                             \
+        hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_BF16X6>), G, dim3(2 * BM_), 0, s, d, src, src2, \
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);
+    if (vec && x6f && (BN == 128 || DCS_X6_BN64) && !DCS_ROWS_F32) {  // x6 / f16x3: 128- or 64-column tiles
         // 256-row tiles where they divide the pixels evenly (the forward over whole 128 x 128
         // images); the 130 x 130 padded data gradient keeps 128-row tiles (measured: its partial
         // last dispatch round and zero-padded border rows make the big tile 7 % slower there)
+        int gxx = gx;
         if (BN == 128 && res && DCS_X6_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
-            const int gx2 = (int)cdiv(Mmax, 256);
-            hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16X6>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
-                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts, fold);
+            gxx = (int)cdiv(Mmax, 256);
+            const dim3 grid2((unsigned)(gxx * gy));
+            DCS_ROWS_X6F(256, 128, 1, 1, grid2)
             if (bm_used) *bm_used = 256;
-        } else if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        } else if (BN == 128 && res) { DCS_ROWS_X6F(128, 128, 1, 1, grid) }
+        else if (BN == 128) { DCS_ROWS_X6F(128, 128, 1, 0, grid) }
+        else { DCS_ROWS_X6F(128, 64, 1, 0, grid) }
         return check_launch("conv_rows");
     }
-    if (v4 && d.mma == MMA_BF16X6 && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
-        if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0, MMA_BF16X6>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+    if (v4 && x6f && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
+        const int gxx = gx;
+        if (BN == 128) { DCS_ROWS_X6F(128, 128, 2, 0, grid) }
+        else { DCS_ROWS_X6F(128, 64, 2, 0, grid) }
         return check_launch("conv_rows");
     }
+#undef DCS_ROWS_X6F
     if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && DCS_BF16P_ROWS && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
         // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier; 256-row
         // tiles where they divide the pixels (the forward)
@@ -2169,15 +2369,25 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws, int kt_per_split,
     int gn, int gm) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    constexpr int NSUB = MMA == MMA_BF16P ? 3 : 1;  // 16-pixel sub-tiles per k-tile
+    constexpr bool H3 = MMA == MMA_F16X3;
+    constexpr int NSUB = MMA == MMA_BF16P ? 3 : (H3 ? 2 : 1);  // 16-pixel sub-tiles per k-tile
+    constexpr int NSLOT = H3 ? 2 * NSUB : 3;     // LDS planes per operand and buffer (f16x3: [hi|lo][sub])
     constexpr int BM = 128, BN = 128, BKP = 16;  // output channels x (tap, ci) columns x pixels per k-tile
     constexpr int WM = BM / 2, WN = BN / 2, IM = WM / 32, JN = WN / 32;
     constexpr int PITCH = 160;                   // bf16 per LDS row
-    constexpr int KT2 = 8;                       // k-tiles per inner accumulation chain (128 pixels)
-    __shared__ __attribute__((aligned(16))) __bf16 X[2 * 3 * 2 * BKP * PITCH];  // [A|B][plane][buf][pix][col]
+    constexpr int KT2 = 8 / NSUB > 0 ? 8 / NSUB : 1;  // k-tiles per inner accumulation chain (128 pixels)
+    __shared__ __attribute__((aligned(16))) __bf16 X[2 * NSLOT * 2 * BKP * PITCH];  // [A|B][plane][buf][pix][col]
     auto xo = [](int op, int pl, int buf, int pix, int col) {
-        return (((op * 3 + pl) * 2 + buf) * BKP + pix) * PITCH + col;
+        return (((op * NSLOT + pl) * 2 + buf) * BKP + pix) * PITCH + col;
     };
+    float asc = 1.f, bsc = 1.f;  // f16x3 operand scales (dy, source) and the epilogue's exponent
+    int eab = 0;
+    if constexpr (H3) {
+        const int ea = f16x3_exp(d.rng_a, d.rng_a_n), eb = f16x3_exp(d.rng_b, d.rng_b_n);
+        asc = __builtin_ldexpf(1.f, ea);
+        bsc = __builtin_ldexpf(1.f, eb);
+        eab = -(ea + eb);
+    }
 
     // sub-pixel descriptors (parity 2) run one GEMM per phase z, as in conv_wgrad_kernel
     const int ncls = d.parity == 2 ? 4 : 1;
@@ -2194,11 +2404,11 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     long long kt_beg = (long long)split * kt_per_split;
     long long kt_end = kt_beg + kt_per_split;
     if (kt_end > nkt_all) kt_end = nkt_all;
-    // pixels of this split; BF16P walks them in 48-pixel k-tiles numbered from 0
+    // pixels of this split; BF16P / f16x3 walk them in NSUB x 16-pixel k-tiles numbered from 0
     const long long px_beg = kt_beg * BKP;
     const long long px_end = kt_end * BKP < P ? kt_end * BKP : P;
-    if constexpr (MMA == MMA_BF16P) {
-        kt_end = px_end > px_beg ? (px_end - px_beg + 3 * BKP - 1) / (3 * BKP) : 0;
+    if constexpr (NSUB > 1) {
+        kt_end = px_end > px_beg ? (px_end - px_beg + NSUB * BKP - 1) / (NSUB * BKP) : 0;
         kt_beg = 0;
     }
 
@@ -2238,8 +2448,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     auto load = [&](long long kt, float4 (&ra)[2 * NSUB], float4 (&rb)[2 * NSUB], int (&pro)[NSUB]) {
 #pragma unroll
       for (int sub = 0; sub < NSUB; ++sub) {
-        long long p = MMA == MMA_BF16P ? px_beg + kt * (3 * BKP) + sub * BKP + kr : kt * BKP + kr;
-        const bool pok = p < (MMA == MMA_BF16P ? px_end : P);
+        long long p = NSUB > 1 ? px_beg + kt * (NSUB * BKP) + sub * BKP + kr : kt * BKP + kr;
+        const bool pok = p < (NSUB > 1 ? px_end : P);
         const int co = m0 + cc;
         if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
 #pragma unroll
@@ -2268,6 +2478,25 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
       }
     };
     auto store = [&](int buf, const float4 (&ra)[2 * NSUB], const float4 (&rbl)[2 * NSUB], const int (&pro)[NSUB]) {
+        if constexpr (H3) {  // slot = plane * NSUB + sub
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                f16x8 hi, lo;
+                split8h(ra[2 * sub], ra[2 * sub + 1], asc, hi, lo);
+                *reinterpret_cast<f16x8*>(X + xo(0, sub, buf, kr, cc)) = hi;
+                *reinterpret_cast<f16x8*>(X + xo(0, NSUB + sub, buf, kr, cc)) = lo;
+                float4 rb[2] = {rbl[2 * sub], rbl[2 * sub + 1]};
+                if (d.pro_act != DCS_ACT_NONE && pro[sub] >= 0) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        rb[i] = affine_act4(rb[i], psc + pro[sub] + 4 * i, psh + pro[sub] + 4 * i, d.pro_act);
+                }
+                split8h(rb[0], rb[1], bsc, hi, lo);
+                *reinterpret_cast<f16x8*>(X + xo(1, sub, buf, kr, cc)) = hi;
+                *reinterpret_cast<f16x8*>(X + xo(1, NSUB + sub, buf, kr, cc)) = lo;
+            }
+            return;
+        }
         if constexpr (MMA == MMA_BF16P) {
 #pragma unroll
             for (int sub = 0; sub < NSUB; ++sub) {
@@ -2307,13 +2536,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const int g16 = lane >> 4;
     const int rpix = 8 * (g16 >> 1) + ((lane & 15) >> 2);
     const int rcol = 16 * (g16 & 1) + 4 * (lane & 3);
-    auto frag = [&](int op, int pl, int buf, int col0) {
+    auto frag16 = [&](int op, int pl, int buf, int col0) {
         const __bf16* p0 = X + xo(op, pl, buf, rpix, col0 + rcol);
         const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(p0));
         const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)(p0 + 4 * PITCH));
-        const shortx8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-        return __builtin_bit_cast(bf16x8, c);
+        return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
     };
+    auto frag = [&](int op, int pl, int buf, int col0) { return __builtin_bit_cast(bf16x8, frag16(op, pl, buf, col0)); };
+    auto fragh = [&](int op, int pl, int buf, int col0) { return __builtin_bit_cast(f16x8, frag16(op, pl, buf, col0)); };
 
     floatx16 acc[IM][JN], t[IM][JN];
 #pragma unroll
@@ -2326,6 +2556,54 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     auto tile = [&](long long kt, float4 (&nra)[2 * NSUB], float4 (&nrb)[2 * NSUB], int (&npro)[NSUB],
                     const float4 (&ora)[2 * NSUB], const float4 (&orb)[2 * NSUB], const int (&opro)[NSUB]) {
         const int cur = (int)((kt - kt_beg) & 1);
+        if constexpr (H3) {
+#pragma unroll
+            for (int sub = 0; sub < NSUB; ++sub) {
+                f16x8 ah[IM], al[IM], bh[JN], bl[JN];
+#pragma unroll
+                for (int i = 0; i < IM; ++i) {
+                    ah[i] = fragh(0, sub, cur, wm * WM + i * 32);
+                    al[i] = fragh(0, NSUB + sub, cur, wm * WM + i * 32);
+                }
+#pragma unroll
+                for (int j = 0; j < JN; ++j) {
+                    bh[j] = fragh(1, sub, cur, wn * WN + j * 32);
+                    bl[j] = fragh(1, NSUB + sub, cur, wn * WN + j * 32);
+                }
+                if (sub == 0) load(kt + 2, nra, nrb, npro);  // unconditional (see below)
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    }
+            }
+            store(cur ^ 1, ora, orb, opro);
+            if constexpr (DCS_WGRAD_SGB > 0) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2 * (IM + JN) * 2 * NSUB, 0);  // DS read
+#pragma unroll
+                for (int i = 0; i < IM * JN * 3 * NSUB; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, DCS_WGRAD_SGB, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x200, 4 * NSUB, 0);  // DS write
+            }
+            const long long rel = kt - kt_beg;
+            if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
+#pragma unroll
+                for (int i = 0; i < IM; ++i)
+#pragma unroll
+                    for (int j = 0; j < JN; ++j) {
+                        acc[i][j] += t[i][j];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
+            __syncthreads();
+            return;
+        }
         if constexpr (MMA == MMA_BF16P) {
 #pragma unroll
             for (int sub = 0; sub < NSUB; ++sub) {
@@ -2409,6 +2687,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         if (kt + 1 < kt_end) tile(kt + 1, ra1, rb1, pro1, ra0, rb0, pro0);
     }
 
+    if constexpr (H3) {  // undo the operand scales (exact powers of two)
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+    }
     float* slab = ws + ((long long)split * ncls + z) * d.Co * Ktot;
     const int l32 = lane & 31;
 #pragma unroll
@@ -2516,7 +2802,10 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
-        if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
+        if (d.mma == MMA_F16X3) {  // f16x3: two 16-pixel sub-tiles per barrier
+            if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        } else if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);

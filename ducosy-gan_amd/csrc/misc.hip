@@ -38,6 +38,52 @@ __global__ void scale_add_kernel(float* __restrict__ y, const float* __restrict_
 
 using namespace dcs;
 
+
+// ---------------------------------------------------------------------------------------
+// range record of an f16x3 operand (include/ducosy_hip.h dcs_range_parts): block b of
+// DCS_RANGE_PARTS reduces max |act(x * scale + shift)| (or |x|) over its contiguous share of
+// the tensor's float4s; the f16x3 conv kernels reduce the DCS_RANGE_PARTS partials themselves
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void range_parts_kernel(const float* __restrict__ x, long long n4, long long per_img,
+                                                          int C, const float* __restrict__ sc,
+                                                          const float* __restrict__ sh, int act,
+                                                          float* __restrict__ parts) {
+    const long long per_blk = (n4 + gridDim.x - 1) / gridDim.x;
+    const long long beg = (long long)blockIdx.x * per_blk;
+    const long long end = beg + per_blk < n4 ? beg + per_blk : n4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    float m = 0.f;
+    auto fold = [&](float4 v, long long i) {
+        if (sc) {
+            const long long e = i * 4;
+            const long long img = e / per_img;
+            const int c = (int)(e % C);
+            const float4 s = *reinterpret_cast<const float4*>(sc + img * C + c);
+            const float4 h = *reinterpret_cast<const float4*>(sh + img * C + c);
+            v.x = act_apply(fmaf(v.x, s.x, h.x), act);
+            v.y = act_apply(fmaf(v.y, s.y, h.y), act);
+            v.z = act_apply(fmaf(v.z, s.z, h.z), act);
+            v.w = act_apply(fmaf(v.w, s.w, h.w), act);
+        }
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    };
+    long long i = beg + threadIdx.x;
+    for (; i + 3 * 512 < end; i += 4 * 512) {  // four loads in flight per thread
+        const float4 a = x4[i], b = x4[i + 512], c = x4[i + 1024], d = x4[i + 1536];
+        fold(a, i); fold(b, i + 512); fold(c, i + 1024); fold(d, i + 1536);
+    }
+    for (; i < end; i += 512) fold(x4[i], i);
+    __shared__ float red[8];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = red[0];
+        for (int w = 1; w < 8; ++w) r = fmaxf(r, red[w]);
+        parts[blockIdx.x] = r;
+    }
+}
+
 extern "C" const char* dcs_last_error(void) { return g_last_error.c_str(); }
 extern "C" int dcs_version(void) { return 1; }
 
@@ -229,4 +275,16 @@ extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, voi
     hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
                        reinterpret_cast<const float*>(ws), C, nch, out);
     return check_launch("channel_sum_final");
+}
+
+extern "C" int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale, const float* shift,
+                               int act, float* parts, void* stream) {
+    if (!x || !parts || n_img <= 0 || per_img <= 0 || per_img % 4 || (reinterpret_cast<uintptr_t>(x) & 15))
+        return fail(DCS_E_INVALID, "range_parts: bad arguments (per_img % 4 == 0, 16-byte aligned x)");
+    if ((scale != nullptr) != (shift != nullptr) || (scale && (C <= 0 || C % 4 || per_img % C)))
+        return fail(DCS_E_INVALID, "range_parts: the prologue needs scale and shift, C % 4 == 0 and per_img % C == 0");
+    if (!scale && act != DCS_ACT_NONE) return fail(DCS_E_INVALID, "range_parts: act without a prologue");
+    hipLaunchKernelGGL(range_parts_kernel, dim3(DCS_RANGE_PARTS), dim3(512), 0, as_stream(stream), x,
+                       (long long)n_img * per_img / 4, (long long)per_img, C, scale, shift, act, parts);
+    return check_launch("range_parts");
 }

@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("DUCOSY_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libdu
 
 DCS_PAD_ZERO, DCS_PAD_REFLECT = 0, 1
 ACT_NONE, ACT_AFFINE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3, 4
-MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6 = 0, 1, 3, 6
+MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6, MMA_F16X3 = 0, 1, 3, 6, 7
+RANGE_PARTS = 512  # DCS_RANGE_PARTS: partial maxima of an f16x3 operand's range record
 KORDER_TAP, KORDER_SLICE, PACK_KSLICE = 0, 1, 8
 
 
@@ -31,6 +32,7 @@ class ConvDesc(ctypes.Structure):
         ("Ho", c_int32), ("Wo", c_int32), ("Co", c_int32),
         ("ldb", c_int32), ("pro_act", c_int32), ("epi_act", c_int32), ("mma", c_int32),
         ("korder", c_int32),
+        ("rng_a_n", c_int32), ("rng_b_n", c_int32), ("rng_a", c_void_p), ("rng_b", c_void_p),
     ]
 
 
@@ -45,6 +47,8 @@ SIGNATURES = {
     "dcs_stream_destroy": (c_int, [P]),
     "dcs_device_cu_count": (c_int, []),
     "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "dcs_pack_weights_r": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "dcs_range_parts": (c_int, [P, c_int, c_int64, c_int, P, P, c_int, P, P]),
     "dcs_conv_rows": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_rows_in_stats_parts_size": (c_size_t, [DP]),
     "dcs_conv_rows_in_stats": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, P, P]),

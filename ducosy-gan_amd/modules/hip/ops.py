@@ -22,7 +22,8 @@ IN_EPS = 1e-5
 # MFMA operand mode of the MFMA convolution passes (include/ducosy_hip.h DCS_MMA_*): "f32" is
 # exact fp32 (the reference's precision, default); "bf16" rounds the GEMM operands to bf16
 # (BASELINE config 5's half-precision path); "bf16x3" splits each operand into hi + lo bf16.
-_MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3, "bf16x6": lib.MMA_BF16X6}
+_MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3, "bf16x6": lib.MMA_BF16X6,
+              "f16x3": lib.MMA_F16X3}
 # default bf16x6: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
 # tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32) and ~1.3x faster on the 3x3 convs
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
@@ -111,6 +112,41 @@ def _round_up(x, m):
 
 
 # ---------------------------------------------------------------------------------------
+# f16x3 operand range records (include/ducosy_hip.h DCS_MMA_F16X3, dcs_range_parts)
+# ---------------------------------------------------------------------------------------
+def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None) -> torch.Tensor:
+    """DCS_RANGE_PARTS partial maxima of |t| (or of |act(t * scale + shift)| with a per-(image,
+    channel) prologue) for an NHWC tensor: the f16x3 kernels reduce them to the operand's power-of-two
+    scale.  Cached on the tensor object per (version, prologue), so the forward, data-gradient and
+    weight-gradient passes over one activation or gradient compute it once."""
+    cached = getattr(t, "_dcs_rng", None)
+    if cached is not None and cached[0] == t._version and cached[1] is (pro[0] if pro else None) \
+            and cached[2] == (pro[2] if pro else ACT_NONE):
+        return cached[3]
+    parts = torch.empty(lib.RANGE_PARTS, device=t.device, dtype=torch.float32)
+    N, C = t.shape[0], t.shape[-1]
+    lib.call("dcs_range_parts", _p(t), N, t.numel() // N, C, _p(pro[0]) if pro else None,
+             _p(pro[1]) if pro else None, pro[2] if pro else ACT_NONE, _p(parts), _stream())
+    t._dcs_rng = (t._version, pro[0] if pro else None, pro[2] if pro else ACT_NONE, parts)
+    return parts
+
+
+def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[torch.Tensor]) -> None:
+    """Operand mode of one MFMA pass.  f16x3 needs the range records of both operands: ``a`` (the
+    gathered tensor, contiguous, with its prologue) and ``b_rng`` (the packed weights' record, or the
+    wgrad source's); a pass without them (concat or strided sources) runs bf16x6."""
+    d.mma = _MMA
+    if _MMA != lib.MMA_F16X3:
+        return
+    if a is None or b_rng is None or not a.is_contiguous() or a.numel() % 4 or a.data_ptr() % 16:
+        d.mma = lib.MMA_BF16X6
+        return
+    ra = range_rec(a, a_pro)
+    d.rng_a, d.rng_a_n = ra.data_ptr(), ra.numel()
+    d.rng_b, d.rng_b_n = b_rng.data_ptr(), b_rng.numel()
+
+
+# ---------------------------------------------------------------------------------------
 # kernel probe: HIP events around the north-star kernel's launches (bench.py roofline)
 # ---------------------------------------------------------------------------------------
 class KernelProbe:
@@ -191,6 +227,12 @@ class Src:
 
 
 BN_MAX = 128
+
+
+def _wrng(wpack: torch.Tensor) -> Optional[torch.Tensor]:
+    """Range record a packed weight tensor carries (dcs_pack_weights_r), None if packed without."""
+    r = getattr(wpack, "_dcs_rng", None)
+    return r[3] if r is not None and r[0] == wpack._version else None
 
 
 def _bn_for(co: int) -> int:
@@ -283,8 +325,14 @@ class ConvGeom:
         else:
             Kpad, cols, nmajor = _round_up(K, 32), _round_up(ncols, _bn_for(ncols)), 1
             out = torch.empty(cols, Kpad, device=w.device, dtype=torch.float32)
-        lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
-                 cols, nmajor, _p(out), _stream())
+        if nmajor and _MMA == lib.MMA_F16X3:  # f16x3 rows pass: the pack also writes the range record
+            rng = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
+            lib.call("dcs_pack_weights_r", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
+                     cols, nmajor, _p(out), _p(rng), _stream())
+            out._dcs_rng = (out._version, None, ACT_NONE, rng)
+        else:
+            lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
+                     cols, nmajor, _p(out), _stream())
         return out
 
     @staticmethod
@@ -307,7 +355,7 @@ class ConvGeom:
             d.up, d.parity = 1, 2  # phases over the source grid (the upsample is in the weights)
         d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
         d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
-        d.mma = _MMA
+        d.mma = _MMA if _MMA != lib.MMA_F16X3 else lib.MMA_BF16X6  # f16x3: _set_mma with the ranges
         d.korder = lib.KORDER_SLICE if (rows and self.kslice and not self.narrow) else lib.KORDER_TAP
         return d
 
@@ -327,6 +375,8 @@ class ConvGeom:
         Ho, Wo = self.out_hw(s.H, s.W)
         d = self._desc_fwd(s, wpack.shape[1], pro[2] if pro is not None else ACT_NONE, epi_act)
         nb = 0 if (self.narrow or not _FUSE_STATS) else lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d))
+        if nb and not self._x6p_fwd(s, d, bias) and s.t2 is None:
+            _set_mma(d, s.t, pro, _wrng(wpack))
         if nb == 0 or self._x6p_fwd(s, d, bias):
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
@@ -361,6 +411,8 @@ class ConvGeom:
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
         x6p = self._x6p_fwd(s, d, bias)
+        if not self.narrow and not x6p and s.t2 is None:
+            _set_mma(d, s.t, pro, _wrng(wpack))
         if x6p:  # operands split once, k-tiles staged by LDS-DMA (conv_x6p.hip)
             sp, wpp = split_x6(s.t), split_x6(wpack)
         e0 = PROBE.begin() if _is_res_geom(self) else None
@@ -406,7 +458,9 @@ class ConvGeom:
         d.up, d.pad_mode = 1, DCS_PAD_ZERO
         d.KH = d.KW = self.k
         d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
-        d.mma = _MMA
+        d.mma = lib.MMA_BF16X6 if _MMA == lib.MMA_F16X3 else _MMA
+        if not narrow:
+            _set_mma(d, dy, None, _wrng(wpack_d))
         d.korder = lib.KORDER_SLICE if (self.kslice and ci > 4) else lib.KORDER_TAP
         d.Co = ci
         dev = dy.device
@@ -487,6 +541,8 @@ class ConvGeom:
         _check_dev(dy, s.t, s.t2)
         pro_act = pro[2] if pro is not None else ACT_NONE
         d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
+        if not self.narrow and s.t2 is None and _MMA == lib.MMA_F16X3 and s.t.is_contiguous():
+            _set_mma(d, dy, None, range_rec(s.t, pro))
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
             d.cw = self.cin
         assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)

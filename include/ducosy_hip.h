@@ -75,6 +75,12 @@ typedef struct dcs_conv_desc {
     int32_t korder;                 /* GEMM K order of the rows pass (and of its packed    */
                                     /* weights): DCS_KORDER_TAP (tap-major) or            */
                                     /* DCS_KORDER_SLICE (16-channel slices, taps inside)  */
+    int32_t rng_a_n, rng_b_n;       /* DCS_MMA_F16X3: counts of the partial maxima below   */
+    const float* rng_a;             /* F16X3: partial maxima of |gathered operand| (rows:  */
+                                    /* the source after its prologue; wgrad: dy), their   */
+                                    /* max an upper bound of every value (dcs_range_parts) */
+    const float* rng_b;             /* F16X3: the same for the other operand (rows: the   */
+                                    /* packed weights, dcs_pack_weights_r; wgrad: source) */
 } dcs_conv_desc;
 
 /* K order of the rows pass.  TAP: k = tap * Cs + c.  SLICE: k = (c / 16) * taps * 16 + tap * 16 +
@@ -95,6 +101,16 @@ typedef struct dcs_conv_desc {
 /* BF16X6: three-way split (hi + mid + lo bf16), six products, ~2^-24 relative error per
  * product (fp32-class); 128-column tiles only, other shapes run F32. */
 #define DCS_MMA_BF16X6 6
+/* F16X3: each fp32 operand, scaled by a power of two 2^s (max|operand| * 2^s < 2^15, from the
+ * descriptor's rng_a / rng_b partial maxima), is split into hi + lo fp16 (22 significant bits:
+ * |v - hi - lo| <= 2^-22 |v|); three products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16,
+ * fp32 two-level accumulation, the result scaled back by 2^-(s_a + s_b) (exact).  Measured
+ * error against float64 at or below the exact-f32 path's on every layer geometry
+ * (tests/test_gpu_mma.py): fp32-class at half the MFMAs of BF16X6.  Shapes without an F16X3
+ * variant run BF16X6. */
+#define DCS_MMA_F16X3 7
+/* partial maxima the F16X3 kernels reduce (dcs_range_parts writes this many) */
+#define DCS_RANGE_PARTS 512
 
 const char* dcs_last_error(void);
 int dcs_version(void);
@@ -125,6 +141,17 @@ int dcs_device_cu_count(void);
  * ci_count limits the packed input channels (dgrad of a concat input needs only the first). */
 int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                      int Kpad, int ncols, int nmajor, float* out, void* stream);
+/* The same, and DCS_RANGE_PARTS partial maxima of |packed value| into rng (the rng_b of an
+ * F16X3 rows pass over these weights). */
+int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                       int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream);
+
+/* Partial maxima of |act(x * scale[n][c] + shift[n][c])| (or |x| when act == DCS_ACT_NONE and
+ * scale == NULL) over an NHWC tensor of n_img images of `per_img` elements, C channels
+ * innermost: DCS_RANGE_PARTS floats into parts, whose max bounds every value (the rng_a / rng_b
+ * of an F16X3 pass).  per_img % 4 == 0, C % 4 == 0 with a prologue. */
+int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale,
+                    const float* shift, int act, float* parts, void* stream);
 
 /* Forward / data-gradient pass: out = gather(src) x B (+ bias, epilogue act). */
 int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,

@@ -3,6 +3,7 @@ float64 CPU reference of the same convolution, forward and data gradient, on eve
 geometry with a vectorised gather.  Tolerances (max |err| / max |ref|), written per mode:
   f32    exact fp32 MFMA                                  <= 1e-5
   bf16x6 hi/mid/lo bf16 split, six products               <= 1e-5   (~2^-24 per product)
+  f16x3  power-of-two scaled hi/lo fp16 split, 3 products <= 1e-5   (~2^-22 per operand)
   bf16x3 hi/lo bf16 split, three products                 <= 5e-5   (~2^-16 per product)
   bf16   bf16 operands, f32 accumulation (config 5)       <= 2e-2   (~2^-9 per operand)
 """
@@ -14,7 +15,7 @@ from test_gpu_ops import CONV_CASES, _geom, rnd, torch_conv
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL = {"f32": 1e-5, "bf16x6": 1e-5, "bf16x3": 5e-5, "bf16": 2e-2}
+TOL = {"f32": 1e-5, "bf16x6": 1e-5, "f16x3": 1e-5, "bf16x3": 5e-5, "bf16": 2e-2}
 CASES = [c for c in CONV_CASES if c[0] % 16 == 0 and c[1] % 16 == 0]
 
 
@@ -30,7 +31,7 @@ def ops():
     o.set_mma(prev)
 
 
-@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "bf16x6", "f32"])
+@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "bf16x6", "f16x3", "f32"])
 @pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
 def test_conv_modes_vs_fp64(ops, mode, case):
     g, H = _geom(case)
@@ -73,9 +74,10 @@ def _errs(ops, mode, g, H, x, w, R):
 
 @pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
 def test_bf16x6_error_matches_exact_f32(ops, case):
-    """bf16x6 is an fp32-class mode: against a float64 convolution of the SAME fp32 operands,
-    its max error (forward, data and weight gradient) is within 1.5x of the exact-fp32 MFMA path's (both are dominated by the fp32
-    accumulation, not the operand split).  Errors are recorded in gpurun_out/x6_err.jsonl."""
+    """bf16x6 and f16x3 are fp32-class modes: against a float64 convolution of the SAME fp32
+    operands, their max error (forward, data and weight gradient) is within 1.5x of the exact-fp32
+    MFMA path's (all are dominated by the fp32 accumulation, not the operand split).  Errors are
+    recorded in gpurun_out/x6_err.jsonl."""
     import json
     import os
     g, H = _geom(case)
@@ -88,17 +90,40 @@ def test_bf16x6_error_matches_exact_f32(ops, case):
     R = torch.from_numpy(prng.normal(23, "R", tuple(yr.shape))).float().double()
     (yr * R).sum().backward()
     e = {}
-    for mode in ("f32", "bf16x6"):
+    for mode in ("f32", "bf16x6", "f16x3"):
         y, dx, dw = _errs(ops, mode, g, H, x, w, R)
         e[mode] = (_relmax(y, yr.detach()), _relmax(dx, xr.grad), _relmax(dw, wr.grad))
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/x6_err.jsonl", "a") as f:
-        f.write(json.dumps({"case": list(case), "f32": e["f32"], "bf16x6": e["bf16x6"]}) + "\n")
+        f.write(json.dumps({"case": list(case), **e}) + "\n")
     for k in range(3):  # forward, data gradient, weight gradient
         assert e["bf16x6"][k] <= 1.5 * e["f32"][k] + 1e-7, e
+        assert e["f16x3"][k] <= 1.5 * e["f32"][k] + 1e-7, e
 
 
-@pytest.mark.parametrize("mode", ["f32", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("scale", [1e-9, 1e-3, 1e4])
+@pytest.mark.parametrize("case", CASES[:3], ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES[:3]])
+def test_f16x3_scale_invariant(ops, case, scale):
+    """f16x3 scales each operand by a power of two from its range record, so the relative error
+    does not depend on the operands' magnitude (gradients of 1e-9, activations of 1e4; fp16 alone
+    covers 6e-8 .. 65504).  Heavy-tailed data (one in 10^4 values x100) keeps the bar."""
+    g, H = _geom(case)
+    N = 2
+    x = rnd((N, g.cin, H, H + 1), 41, "x").double() * scale
+    x.view(-1)[::9973] *= 100.0
+    w = torch.from_numpy(prng.normal(42, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05)).float().double()
+    xr = x.float().double().clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, g)
+    R = (torch.from_numpy(prng.normal(43, "R", tuple(yr.shape))).double() * scale).float().double()
+    (yr * R).sum().backward()
+    y, dx, dw = _errs(ops, "f16x3", g, H, xr.detach(), w, R)
+    assert _relmax(y, yr.detach()) <= TOL["f16x3"]
+    assert _relmax(dx, xr.grad) <= TOL["f16x3"]
+    assert _relmax(dw, wr.grad) <= TOL["f16x3"]
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16x6", "bf16x3", "f16x3"])
 def test_modes_deterministic(ops, mode):
     """Every MFMA mode is run-to-run deterministic (bit-identical forward and data gradient),
     also with other work in flight on a second stream."""
