@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -57,26 +58,50 @@ def _synthetic(n, img, n_masks, device, seed):
     return a, b, m
 
 
-def cpu_baseline(img, blocks, cin, threads):
-    """Time the oracle's CPU step (the reference algorithm restated) on one slice."""
-    sys.path.insert(0, ROOT)
+def _cpu_steps(img, bs, blocks, cin, warmup, steps):
+    """Median seconds per step of the oracle's CPU train step (the reference algorithm restated,
+    oracle/ref_torch.py, fp32) after ``warmup`` untimed steps."""
     from oracle import prng
     from oracle import ref_torch as orc
-    torch.set_num_threads(threads)
     gs, ds = orc.generator_param_shapes(cin, blocks, True), orc.discriminator_param_shapes(1)
     sd = lambda shapes, s: {k: torch.from_numpy(v) for k, v in prng.init_state_dict(shapes, s).items()}
     m = orc.OracleCycleGAN(sd(gs, 1), sd(gs, 2), sd(ds, 3), sd(ds, 4), blocks)
-    a = torch.from_numpy(prng.uniform(5, "A", (1, 1, img, img), -1, 1))
-    b = torch.from_numpy(prng.uniform(5, "B", (1, 1, img, img), -1, 1))
-    mk = torch.from_numpy(prng.bernoulli(5, "M", (1, cin - 1, img, img), 0.3)) if cin > 1 else None
-    m.step(a, b, mk)  # warm-up: first-call oneDNN primitive setup stays out of the timing
-    t0 = time.perf_counter()
-    m.step(a, b, mk)
-    dt = time.perf_counter() - t0
-    return {"value": round(1.0 / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"1 full step (G+D_A+D_B, all losses, Adam) on 1 slice {img}x{img} after 1 untimed "
-                      f"warm-up step, {blocks} residual blocks, cin {cin}, oracle/ref_torch.py fp32 on CPU "
-                      f"({dt:.2f} s)"}
+    a = torch.from_numpy(prng.uniform(5, "A", (bs, 1, img, img), -1, 1))
+    b = torch.from_numpy(prng.uniform(5, "B", (bs, 1, img, img), -1, 1))
+    mk = torch.from_numpy(prng.bernoulli(5, "M", (bs, cin - 1, img, img), 0.3)) if cin > 1 else None
+    for _ in range(warmup):  # first-call oneDNN primitive setup stays out of the timing
+        m.step(a, b, mk)
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        m.step(a, b, mk)
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def cpu_baseline(img, blocks, cin, threads):
+    """BASELINE.md section 3 on this host's cores: the oracle's CPU step at BASELINE config 1 (128x128,
+    bs 2, 1 residual block) and at the metric's shape (512x512, bs 1, 9 blocks), 3 untimed warm-up
+    steps each, median of the timed steps.  ``value`` is the 512x512 rate (same slice shape as the
+    GPU metric); the 512x512 sample is 3 timed steps to keep the default bench within minutes."""
+    sys.path.insert(0, ROOT)
+    torch.set_num_threads(threads)
+    c1 = _cpu_steps(128, 2, 1, cin, 3, 10)
+    full = _cpu_steps(img, 1, blocks, cin, 3, 3)
+    cpu = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(1.0 / full, 4), "unit": "img/s", "cores": threads, "kind": "port", "cpu": cpu,
+            "config1_img_s": round(2.0 / c1, 3),
+            "sample": f"oracle/ref_torch.py fp32 CPU train step (G+D_A+D_B, all losses, Adam), median after 3 "
+                      f"untimed warm-ups: {img}x{img} bs 1, {blocks} blocks, cin {cin}, 3 timed steps "
+                      f"({full:.2f} s/step) = value; BASELINE config 1 (128x128 bs 2, 1 block) 10 timed steps "
+                      f"({c1 * 1e3:.0f} ms/step) = config1_img_s"}
 
 
 def _pmc_record(mode):
@@ -175,19 +200,36 @@ def main():
         torch.distributed.barrier()
     ops.PROBE.reset()
     ops.PROBE.active = True
+    # per-step GPU time from events at the step boundaries (no extra synchronisation): the
+    # median step next to the whole-loop rate
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for i in range(args.steps):
         step(batches[i % 2])
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     ops.PROBE.active = False
+    step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
+    med_ms = statistics.median(step_ms)
     if world > 1:
-        t = torch.tensor([elapsed], device=device)
+        # slowest rank of the whole job (both groups of --dual-schedule groups: the default group)
+        t = torch.tensor([elapsed, med_ms], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t)
+        elapsed, med_ms = float(t[0]), float(t[1])
     n_launch, ms_launch, flop_launch = ops.PROBE.summary()
+    replicas_ok = None
+    if world > 1:  # every replica of a model must still hold the same parameters
+        from modules import parallel as par
+        sysms = runner.systems if (args.dual and not groups) else ([system] if args.workload == "step" else [])
+        flats = [opt.flat_p for sm in sysms for opt in sm.optimizers]
+        replicas_ok = par.replicas_identical(flats) if flats else None
+        ok = torch.tensor([1 if replicas_ok in (True, None) else 0], device=device)
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+        replicas_ok = bool(ok.item()) if flats else None
 
     if rank == 0:
         value = world * models * args.batch * args.steps / elapsed
@@ -215,9 +257,11 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step_median": round(med_ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "replicas_identical": replicas_ok,
             "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {

@@ -53,13 +53,10 @@ SIGNATURES = {
     "dcs_conv_rows_in_stats_parts_size": (c_size_t, [DP]),
     "dcs_conv_rows_in_stats": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_in_stats_finish": (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P, P]),
-    "dcs_split_x6": (c_int, [P, c_int64, P, P]),
     "dcs_conv_dgrad_c1": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P]),
     "dcs_conv_dgrad_to1_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "dcs_conv_dgrad_to1": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                    P, P, c_size_t, P]),
-    "dcs_conv_rows_x6p_ok": (c_int, [DP]),
-    "dcs_conv_rows_x6p": (c_int, [DP, P, P, P, P]),
     "dcs_conv_wgrad_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
     "dcs_conv_dgrad_reflect_ring_size": (c_size_t, [P]),

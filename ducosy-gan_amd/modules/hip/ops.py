@@ -29,9 +29,6 @@ _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
 
 
-# bf16x6 residual convs on pre-split operands staged by LDS-DMA (csrc/conv_x6p.hip); 0 = the
-# split-in-the-gather rows kernel of conv.hip (A/B switch)
-_X6P = os.environ.get("DUCOSY_X6P", "0") == "1"
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
 # IN statistics fused into the conv epilogue (ConvGeom.forward_in_stats); "0" = separate pass (A/B)
 _FUSE_STATS = os.environ.get("DUCOSY_FUSE_STATS", "1") == "1"
@@ -90,21 +87,6 @@ def workspace(nbytes: int, device) -> torch.Tensor:
     if _WS_POISON:  # debug: every request sees NaN bytes (finds reads of unwritten scratch)
         buf.fill_(0xFF)
     return buf
-
-
-def split_x6(t: torch.Tensor) -> torch.Tensor:
-    """fp32 tensor (contiguous, numel % 8 == 0) -> its bf16x6 operand planes: groups of 8
-    consecutive elements as [hi[8], mid[8], lo[8]] bf16 (held in an int16 tensor, 3 x numel)."""
-    if not t.is_contiguous() or t.numel() % 8:
-        raise ValueError("split_x6: contiguous tensor with numel % 8 == 0 expected")
-    _check_dev(t)
-    out = torch.empty(t.numel() * 3, dtype=torch.int16, device=t.device)
-    lib.call("dcs_split_x6", _p(t), t.numel(), _p(out), _stream())
-    return out
-
-
-def _x6p(d: lib.ConvDesc) -> bool:
-    return _X6P and d.mma == lib.MMA_BF16X6 and bool(lib.query("dcs_conv_rows_x6p_ok", ctypes.byref(d)))
 
 
 def _round_up(x, m):
@@ -255,9 +237,8 @@ class ConvGeom:
         """The residual convs run the slice-major K order (include/ducosy_hip.h
         DCS_KORDER_SLICE: 3.7x fewer L2 misses on the gathered rows, 4 % faster in bf16x6) in the
         bf16 operand modes; their packed weights follow it.  The exact-f32 kernel keeps the
-        tap-major order (its gather decodes the tap once per 8 k-tiles there), as does the
-        pre-split x6p path (conv_x6p.hip)."""
-        return _is_res_geom(self) and _KSLICE and not _X6P and _MMA != lib.MMA_F32
+        tap-major order (its gather decodes the tap once per 8 k-tiles there)."""
+        return _is_res_geom(self) and _KSLICE and _MMA != lib.MMA_F32
 
     def out_hw(self, H, W):
         Hv, Wv = H * self.up, W * self.up
@@ -360,10 +341,6 @@ class ConvGeom:
         return d
 
     # ---- forward -------------------------------------------------------------------
-    def _x6p_fwd(self, s: Src, d, bias) -> bool:
-        return (not self.narrow and bias is None and s.t2 is None and s.t.is_contiguous()
-                and s.strides == (s.H * s.W * s.C, 1, s.W * s.C, s.C) and _x6p(d))
-
     def forward_in_stats(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
                          pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
                          epi_act: int = ACT_NONE, want_max: bool = False):
@@ -375,9 +352,9 @@ class ConvGeom:
         Ho, Wo = self.out_hw(s.H, s.W)
         d = self._desc_fwd(s, wpack.shape[1], pro[2] if pro is not None else ACT_NONE, epi_act)
         nb = 0 if (self.narrow or not _FUSE_STATS) else lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d))
-        if nb and not self._x6p_fwd(s, d, bias) and s.t2 is None:
+        if nb and s.t2 is None:
             _set_mma(d, s.t, pro, _wrng(wpack))
-        if nb == 0 or self._x6p_fwd(s, d, bias):
+        if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
         assert s.C == self.cin or (s.C == 4 and self.cin < 4), (s.C, self.cin)
@@ -410,17 +387,11 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
-        x6p = self._x6p_fwd(s, d, bias)
-        if not self.narrow and not x6p and s.t2 is None:
+        if not self.narrow and s.t2 is None:
             _set_mma(d, s.t, pro, _wrng(wpack))
-        if x6p:  # operands split once, k-tiles staged by LDS-DMA (conv_x6p.hip)
-            sp, wpp = split_x6(s.t), split_x6(wpack)
         e0 = PROBE.begin() if _is_res_geom(self) else None
-        if x6p:
-            lib.call("dcs_conv_rows_x6p", ctypes.byref(d), _p(sp), _p(wpp), _p(out), _stream())
-        else:
-            lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
-                     _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
+        lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
+                 _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
         PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
         return out
 
@@ -493,7 +464,7 @@ class ConvGeom:
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
             if _FUSE_FOLD and addend is None and p == 1 and self.k == 3 and H >= 4 and W >= 4 and not narrow \
-                    and dy.is_contiguous() and not _x6p(d) and ci % 4 == 0:
+                    and dy.is_contiguous() and ci % 4 == 0:
                 # interior written by the conv epilogue, the ring folded in after.  With a residual
                 # addend the padded pass + dcs_reflect_fold stays faster: the addend read in the
                 # epilogue sits after the MFMA loop (+145 us per 16-image launch against +125 us for
@@ -507,15 +478,8 @@ class ConvGeom:
                 PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
                 return out
             dpad = torch.empty(N, d.Ho, d.Wo, ci, device=dev, dtype=torch.float32)
-            x6p = not narrow and dy.is_contiguous() and _x6p(d)
-            if x6p:
-                sp, wpp = split_x6(dy), split_x6(wpack_d)
             e0 = PROBE.begin() if _is_res_geom(self) else None
-            if x6p:
-                lib.call("dcs_conv_rows_x6p", ctypes.byref(d), _p(sp), _p(wpp), _p(dpad), _stream())
-            else:
-                lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad),
-                         _stream())
+            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(dpad), _stream())
             PROBE.end(e0, 2.0 * N * Ho * Wo * self.cout * ci * self.k * self.k)
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
             lib.call("dcs_reflect_fold", _p(dpad), _p(addend), _p(out), N, H, W, ci, p, _stream())

@@ -4,9 +4,13 @@ Replaces the reference's single-process nn.DataParallel (modules/trainer.py:333-
 scatters every G/D call over 8 GPUs, re-broadcasts all parameters per call and reduces
 gradients to cuda:0.  Here each rank owns full replicas of G_A2B, G_B2A, D_A, D_B and its own
 batch shard; per optimizer step the optimizer's flat gradient buffer (FusedAdam.flat_g: 91.6 MB
-for the G pair, 11.05 MB per D at cin 3) is averaged over the replicas.  The G buffer goes out
-in buckets while the G backward is still running (``GradBuckets``); initial weights are
-broadcast from the group's first rank once.
+for the G pair, 11.05 MB per D at cin 3) is averaged over the replicas by ONE stream-ordered
+all-reduce after the backward (``GradBuckets`` with overlap off, the default).  Launching bucket
+all-reduces from inside the backward (``DUCOSY_GRAD_OVERLAP=1``) would put RCCL's kernels on their
+own queue beside the backward's, on shared compute-unit pairs: the condition of the unexplained
+two-queue hazard (Config 5), for at most ~1 ms of a 300+ ms step.  Initial weights
+are broadcast from the group's first rank once; ``replicas_identical`` checks after a run that
+every replica still holds the same parameters (bench.py reports it).
 
 Replica group: by default every rank of the job.  ``set_group`` narrows it to a sub-group, for
 BASELINE config 5 on one node as split GPU groups (soft-tissue model on ranks 0..w/2-1, lung
@@ -127,10 +131,15 @@ def shard(n_total: int, r: int = None, w: int = None):
     return r * per, (r + 1) * per
 
 
+_OVERLAP = os.environ.get("DUCOSY_GRAD_OVERLAP", "0") == "1"
+
+
 class GradBuckets:
-    """All-reduce-mean of one flat gradient buffer in buckets, each launched (async) as soon
-    as the backward has finished accumulating every parameter of the bucket, so the exchange
-    of the early buckets overlaps the rest of the backward.
+    """All-reduce-mean of one flat gradient buffer.  Default (``overlap`` False): ``arm()`` does
+    nothing and ``finish()`` runs one stream-ordered all-reduce of the whole buffer after the
+    backward.  With ``overlap`` (DUCOSY_GRAD_OVERLAP=1, experimental): in buckets, each launched
+    (async) as soon as the backward has finished accumulating every parameter of the bucket, so
+    the exchange of the early buckets overlaps the rest of the backward.
 
     buckets: list of lists of parameters whose ``.grad`` are views of ``flat`` (FusedAdam
     layout); each bucket must be one contiguous span of ``flat``.  Autograd accumulates a leaf
@@ -139,8 +148,9 @@ class GradBuckets:
     backward, ``finish()`` after it (waits for every bucket and applies 1/world); ``early``
     counts the buckets launched from inside the backward.  With one replica both are no-ops."""
 
-    def __init__(self, flat: torch.Tensor, buckets):
+    def __init__(self, flat: torch.Tensor, buckets, overlap: bool = None):
         self.flat = flat
+        self.overlap = _OVERLAP if overlap is None else bool(overlap)
         self.spans, self.members = [], []
         base = flat.data_ptr()
         esz = flat.element_size()
@@ -157,12 +167,18 @@ class GradBuckets:
         self._left = None
         self.early = 0
 
+    def disarm(self):
+        """Remove the hooks of an earlier arm() (also after a backward that raised)."""
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
     def arm(self):
-        if world() == 1:
+        self.disarm()
+        if world() == 1 or not self.overlap:
             return
         self._works = [None] * len(self.spans)
         self._left = [len(b) for b in self.members]
-        self._handles = []
         self.early = 0
         for bi, b in enumerate(self.members):
             for p in b:
@@ -182,9 +198,10 @@ class GradBuckets:
         w = world()
         if w == 1:
             return
-        for h in self._handles:
-            h.remove()
-        self._handles = []
+        if not self.overlap:
+            allreduce_mean_(self.flat)
+            return
+        self.disarm()
         for bi, wk in enumerate(self._works):
             lo, hi = self.spans[bi]
             if wk is None:  # a member received no gradient this step: reduce the bucket now
@@ -192,3 +209,25 @@ class GradBuckets:
             else:
                 wk.wait()
         _scale_(self.flat, 1.0 / w)
+
+
+def replica_checksums(flats) -> torch.Tensor:
+    """[len(flats), 2] float64: sum and index-weighted sum of each flat parameter buffer (any
+    difference between replicas, including a permutation, changes them)."""
+    rows = []
+    for f in flats:
+        d = f.detach().double()
+        w = torch.arange(1, d.numel() + 1, device=d.device, dtype=torch.float64) / d.numel()
+        rows.append(torch.stack([d.sum(), (d * w).sum()]))
+    return torch.stack(rows)
+
+
+def replicas_identical(flats) -> bool:
+    """True when every replica of the group holds bit-for-bit the same checksums (collective: every
+    rank of the group must call it).  A corrupted all-reduce or a diverged replica shows here."""
+    c = replica_checksums(flats)
+    if world() == 1:
+        return True
+    got = [torch.empty_like(c) for _ in range(world())]
+    dist.all_gather(got, c, group=_GROUP)
+    return all(torch.equal(g, got[0]) for g in got)

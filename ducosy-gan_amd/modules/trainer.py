@@ -77,9 +77,10 @@ class CycleGANSystem:
         # identical initial replicas on every rank
         for opt in self.optimizers:
             parallel.broadcast_(opt.flat_p, 0)
-        # G gradient exchange in two buckets: G_B2A's half is final once its one backward call has
-        # run, and goes out while the G_A2B backward of the batched [real_A; real_B] call (the
-        # last of the step, ~40 % of the G backward) is still computing.
+        # G gradient exchange: one all-reduce after the backward by default; with
+        # DUCOSY_GRAD_OVERLAP=1 two buckets (G_B2A's half is final once its one backward call has
+        # run and goes out while the G_A2B backward of the batched [real_A; real_B] call is
+        # still computing)
         self._g_sync = parallel.GradBuckets(self.optimizer_G.flat_g,
                                             [list(self.G_A2B.parameters()), list(self.G_B2A.parameters())])
 
@@ -128,7 +129,10 @@ class CycleGANSystem:
                   + LAMBDA_GRAD * loss_grad_cycle + LAMBDA_GRAD_ID * loss_grad_id + LAMBDA_SSIM * loss_ssim
                   + LAMBDA_CA * loss_ca + LAMBDA_CR * loss_cr + LAMBDA_CE * loss_ce)
         self._g_sync.arm()
-        loss_G.backward()
+        try:
+            loss_G.backward()
+        finally:
+            self._g_sync.disarm()  # no hook outlives a backward that raised
         self._g_sync.finish()  # replica mean of the G gradient
         self.optimizer_G.step()
 

@@ -172,21 +172,6 @@ int dcs_conv_rows_in_stats(const dcs_conv_desc* d, const float* src, const float
                            const float* bias, const float* pro_scale, const float* pro_shift, float* out, void* parts,
                            size_t parts_bytes, int* nchunk, void* stream);
 
-/* bf16x6 operand planes: n fp32 values (n % 8 == 0, 16-byte aligned) -> 3n bf16 in groups of
- * 8 consecutive values as [hi[8], mid[8], lo[8]] (v = hi + mid + lo, each residual exact in
- * fp32).  The pre-split operand format of dcs_conv_rows_x6p. */
-int dcs_split_x6(const float* src, int64_t n, void* dst, void* stream);
-
-/* Forward / stride-1 data-gradient pass of the 3x3 residual convs (modules/model.py:72-80,
- * aten convolution + convolution_backward's grad_input) on pre-split bf16x6 operands staged
- * by LDS-DMA: srcp = dcs_split_x6 of the NHWC fp32 source, wpp = dcs_split_x6 of the N-major
- * packed weights ([ceil(Co/128)*128][ldb]).  Same products, order and fp32 two-level
- * accumulation as dcs_conv_rows with mma = DCS_MMA_BF16X6 (bit-identical results).
- * dcs_conv_rows_x6p_ok: 1 if `d` is a geometry this pass covers (stride 1, regular rows,
- * Cs % 16 == 0, Co % 128 == 0, no prologue / epilogue / bias, split operands < 2 GiB). */
-int dcs_conv_rows_x6p_ok(const dcs_conv_desc* d);
-int dcs_conv_rows_x6p(const dcs_conv_desc* d, const void* srcp, const void* wpp, float* out, void* stream);
-
 /* Weight gradient: dw (OIHW) = sum_pixels dy^T x gather(x).  `d` describes the FORWARD conv
  * (source = x, output = dy).  ws must hold dcs_conv_wgrad_workspace_size(d) bytes. */
 size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* d);

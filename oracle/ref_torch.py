@@ -118,24 +118,34 @@ def residual_block(p: Params, prefix: str, x: torch.Tensor, use_cbam: bool = Tru
     return x + h
 
 
+def generator_stages(p: Params, x: torch.Tensor, num_residual_blocks: int = 9,
+                     use_cbam: bool = True) -> Dict[str, torch.Tensor]:
+    """modules/model.py:90-115 Generator.forward (ResNet-CBAM, output 1 channel, tanh), returning
+    every stage's activation: "stem", "down1", "down2" (conv + IN + ReLU), "res{b}" (each residual
+    block's output), "up1", "up2" and "out"."""
+    st = {}
+    h = F.conv2d(F.pad(x, (3, 3, 3, 3), mode="reflect"), p["model.1.weight"], p["model.1.bias"])
+    h = st["stem"] = F.relu(_inorm(h))
+    for name, idx in (("down1", 4), ("down2", 7)):  # stride-2, zero pad 1 (modules/model.py:96-98)
+        h = F.conv2d(h, p[f"model.{idx}.weight"], p[f"model.{idx}.bias"], stride=2, padding=1)
+        h = st[name] = F.relu(_inorm(h))
+    for b in range(num_residual_blocks):
+        h = st[f"res{b}"] = residual_block(p, f"model.{10 + b}", h, use_cbam)
+    u = 10 + num_residual_blocks
+    for name, idx in (("up1", u + 1), ("up2", u + 5)):  # nearest x2 upsample, conv zero pad 1 (:107-111)
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
+        h = F.conv2d(h, p[f"model.{idx}.weight"], p[f"model.{idx}.bias"], padding=1)
+        h = st[name] = F.relu(_inorm(h))
+    h = F.conv2d(F.pad(h, (3, 3, 3, 3), mode="reflect"),
+                 p[f"model.{u + 9}.weight"], p[f"model.{u + 9}.bias"])
+    st["out"] = torch.tanh(h)
+    return st
+
+
 def generator_forward(p: Params, x: torch.Tensor, num_residual_blocks: int = 9,
                       use_cbam: bool = True) -> torch.Tensor:
     """modules/model.py:90-115 Generator.forward (ResNet-CBAM, output 1 channel, tanh)."""
-    h = F.conv2d(F.pad(x, (3, 3, 3, 3), mode="reflect"), p["model.1.weight"], p["model.1.bias"])
-    h = F.relu(_inorm(h))
-    for idx in (4, 7):  # stride-2, zero pad 1 (modules/model.py:96-98)
-        h = F.conv2d(h, p[f"model.{idx}.weight"], p[f"model.{idx}.bias"], stride=2, padding=1)
-        h = F.relu(_inorm(h))
-    for b in range(num_residual_blocks):
-        h = residual_block(p, f"model.{10 + b}", h, use_cbam)
-    u = 10 + num_residual_blocks
-    for idx in (u + 1, u + 5):  # nearest x2 upsample, conv zero pad 1 (modules/model.py:107-111)
-        h = F.interpolate(h, scale_factor=2, mode="nearest")
-        h = F.conv2d(h, p[f"model.{idx}.weight"], p[f"model.{idx}.bias"], padding=1)
-        h = F.relu(_inorm(h))
-    h = F.conv2d(F.pad(h, (3, 3, 3, 3), mode="reflect"),
-                 p[f"model.{u + 9}.weight"], p[f"model.{u + 9}.bias"])
-    return torch.tanh(h)
+    return generator_stages(p, x, num_residual_blocks, use_cbam)["out"]
 
 
 def discriminator_forward(p: Params, x: torch.Tensor) -> torch.Tensor:

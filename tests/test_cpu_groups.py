@@ -4,10 +4,12 @@
   0-1, lung model on ranks 2-3): inside each group the all-reduce-mean of the shard gradients
   equals that model's full-batch gradient (oracle Generator, per-sample losses), and the
   rank-0 broadcast gives each group its own first rank's weights;
-* world 2: GradBuckets (trainer.py's G exchange, launched from post-accumulate hooks while the
-  backward runs) equals one all-reduce-mean of the whole flat buffer, with a parameter reached
-  by two graph branches (as G_A2B's weights are) and one reached once, and both buckets go out
-  from inside the backward.
+* world 2: GradBuckets (trainer.py's G exchange) equals one all-reduce-mean of the whole flat
+  buffer, with a parameter reached by two graph branches (as G_A2B's weights are) and one
+  reached once: by default after the backward (no bucket goes out from inside it), and with
+  overlap on both buckets go out from inside the backward; a second arm() does not stack hooks;
+* world 2: parallel.replicas_identical (bench.py's "replicas_identical") is True for equal
+  replicas and False when one replica differs by one ulp in one element.
 """
 import os
 import socket
@@ -73,7 +75,7 @@ def _groups_worker(rank, world, port, q):
         raise
 
 
-def _buckets_worker(rank, world, port, q):
+def _buckets_worker(rank, world, port, q, overlap):
     _setup(rank, world, port)
     from modules import parallel
     try:
@@ -82,9 +84,10 @@ def _buckets_worker(rank, world, port, q):
         a = torch.nn.Parameter(torch.arange(4.0))
         b = torch.nn.Parameter(torch.arange(6.0) - 2)
         a.grad, b.grad = flat[:4].view(4), flat[4:].view(6)
-        sync = parallel.GradBuckets(flat, [[a], [b]])
+        sync = parallel.GradBuckets(flat, [[a], [b]], overlap=overlap)
         x = torch.tensor(float(rank + 1))
         sync.arm()
+        sync.arm()  # re-arming replaces the hooks (a stale set would reduce buckets early)
         # a is used by two graph branches that reach it separately (two accumulations)
         la = (a * x).sum()
         lb = (a * a * x).sum() + (b.square() * x).sum()
@@ -102,11 +105,29 @@ def _buckets_worker(rank, world, port, q):
         raise
 
 
-def _run(target, world, n_results):
+def _replica_worker(rank, world, port, q):
+    _setup(rank, world, port)
+    from modules import parallel
+    try:
+        parallel.init_from_env("gloo")
+        f = [torch.linspace(-1, 1, 1000), torch.arange(7.0)]
+        same = parallel.replicas_identical(f)
+        if rank == 1:
+            f[0][123] = torch.nextafter(f[0][123], torch.tensor(2.0))
+        diff = parallel.replicas_identical(f)
+        q.put((rank, same, diff))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:
+        q.put((-1, repr(e), None))
+        raise
+
+
+def _run(target, world, n_results, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *extra)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=280) for _ in range(n_results)]
@@ -124,8 +145,18 @@ def test_split_groups_world4():
 
 
 @pytest.mark.timeout(300)
-def test_grad_buckets_world2():
-    res = _run(_buckets_worker, 2, 2)
+@pytest.mark.parametrize("overlap", [False, True])
+def test_grad_buckets_world2(overlap):
+    res = _run(_buckets_worker, 2, 2, overlap)
     for r in res:
         assert r[0] >= 0, r
-        assert r[1] < 1e-6 and r[2] == 2, r  # both buckets launched from inside the backward
+        # overlap: both buckets launched from inside the backward; default: none (one all-reduce after it)
+        assert r[1] < 1e-6 and r[2] == (2 if overlap else 0), r
+
+
+@pytest.mark.timeout(300)
+def test_replicas_identical_world2():
+    res = _run(_replica_worker, 2, 2)
+    for r in res:
+        assert r[0] >= 0, r
+        assert r[1] is True and r[2] is False, r
