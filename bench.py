@@ -129,10 +129,11 @@ def main():
     ap.add_argument("--blocks", type=int, default=9)
     ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mma", default="bf16x6", choices=["f32", "bf16", "bf16x3", "bf16x6", "f16x3"],
-                    help="MFMA operand mode of the conv passes: bf16x6 = three-way split, fp32-class "
-                         "(default; error <= the exact-f32 path's, tests/test_gpu_mma.py), f32 = exact "
-                         "fp32 MFMA, bf16x3 = hi/lo split, bf16 = plain bf16 operands")
+    ap.add_argument("--mma", default="f16x3", choices=["f32", "bf16", "bf16x3", "bf16x6", "f16x3"],
+                    help="MFMA operand mode of the conv passes: f16x3 = power-of-two scaled hi/lo fp16 split, "
+                         "three products, fp32-class (default; error <= the exact-f32 path's, "
+                         "tests/test_gpu_mma.py), bf16x6 = three-way bf16 split (fp32-class, 6 products), "
+                         "f32 = exact fp32 MFMA, bf16x3 = hi/lo bf16 split, bf16 = plain bf16 operands")
     ap.add_argument("--dual", action="store_true",
                     help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one "
                          "process; value counts the images of both models")

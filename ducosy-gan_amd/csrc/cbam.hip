@@ -91,10 +91,10 @@ __global__ __launch_bounds__(256) void sa_apply_kernel(const float* __restrict__
                                                        const float* __restrict__ ca, const float* __restrict__ sin_,
                                                        const float* __restrict__ wsa, int H, int W, int C, int ksa,
                                                        long long P, float* __restrict__ sa,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, float* __restrict__ rng) {
     const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (p >= P) return;
+    if (p >= P) return;  // wave-uniform
     const int HW = H * W;
     const int n = (int)(p / HW);
     const int rem = (int)(p - (long long)n * HW);
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void sa_apply_kernel(const float* __restrict__
     const float* s = sc + (long long)n * C;
     const float* b = sh + (long long)n * C;
     const float* a = ca + (long long)n * C;
+    float m = 0.f;
     for (int c4 = lane; c4 < C / 4; c4 += 64) {
         float4 v = reinterpret_cast<const float4*>(y + p * C)[c4];
         float4 xv = reinterpret_cast<const float4*>(x + p * C)[c4];
@@ -124,7 +125,9 @@ __global__ __launch_bounds__(256) void sa_apply_kernel(const float* __restrict__
         o.z = xv.z + fmaf(v.z, s[c + 2], b[c + 2]) * a[c + 2] * g;
         o.w = xv.w + fmaf(v.w, s[c + 3], b[c + 3]) * a[c + 3] * g;
         reinterpret_cast<float4*>(out + p * C)[c4] = o;
+        m = fmaxf(m, absmax4(o));
     }
+    range_note(rng, m);
 }
 
 // ---- 16-lane-per-pixel forms (C = 64 * NQ, NQ in {1, 2, 4}) -------------------------------
@@ -206,11 +209,12 @@ __global__ __launch_bounds__(256) void sa_apply16_kernel(const float* __restrict
                                                          const float* __restrict__ ca, const float* __restrict__ sin_,
                                                          const float* __restrict__ wsa, int H, int W, int C, int ksa,
                                                          long long P, float* __restrict__ sa,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out, float* __restrict__ rng) {
     const int lane = threadIdx.x & 63, j = lane & 15, grp = lane >> 4;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int HW = H * W, r = ksa / 2, taps = ksa * ksa;
     CbRegs<NQ> rg;
+    float m = 0.f;
     for (int it = 0; it < CB_QUADS; ++it) {
         const long long p = (wave * CB_QUADS + it) * 4 + grp;
         if (p >= P) break;
@@ -241,8 +245,10 @@ __global__ __launch_bounds__(256) void sa_apply16_kernel(const float* __restrict
             o.z = xv.z + fmaf(v.z, rg.s[q].z, rg.b[q].z) * rg.a[q].z * g;
             o.w = xv.w + fmaf(v.w, rg.s[q].w, rg.b[q].w) * rg.a[q].w * g;
             op[q * 16 + j] = o;
+            m = fmaxf(m, absmax4(o));
         }
     }
+    range_note(rng, m);  // every lane (the pixel loop breaks, never returns)
 }
 
 static inline int cb_nq(int C) { return (C == 64 || C == 128 || C == 256) ? C / 64 : 0; }
@@ -538,9 +544,10 @@ __global__ void cb_bwd_apply_kernel(const float* __restrict__ dout, const float*
                                     const float* __restrict__ ca, const float* __restrict__ sa,
                                     const float* __restrict__ dsin, const int* __restrict__ sarg,
                                     const int* __restrict__ yarg, const Sum3* __restrict__ coef, int HW, int C,
-                                    long long total, float* __restrict__ dy) {
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
+                                    long long total, float* __restrict__ dy, float* __restrict__ rng) {
+    const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i0 < total;
+    const long long i = live ? i0 : total - 1;  // dead lanes recompute the last element, store nothing
     const int c = (int)(i % C);
     const long long pp = i / C;
     const int n = (int)(pp / HW);
@@ -553,7 +560,9 @@ __global__ void cb_bwd_apply_kernel(const float* __restrict__ dout, const float*
     const Sum3 k = coef[nc];
     float dz = dzc * ca[nc];
     if (yarg[nc] == p) dz += k.c;
-    dy[i] = s * (dz - k.a - z * k.b);
+    const float v = s * (dz - k.a - z * k.b);
+    if (live) dy[i] = v;
+    range_note(rng, fabsf(v));  // every lane
 }
 
 // b5, float4 form (C % 4 == 0): one thread per 4 channels of a pixel, 32-bit index math
@@ -562,9 +571,11 @@ __global__ __launch_bounds__(256) void cb_bwd_apply4_kernel(const float* __restr
                                                             const float* __restrict__ ca, const float* __restrict__ sa,
                                                             const float* __restrict__ dsin, const int* __restrict__ sarg,
                                                             const int* __restrict__ yarg, const Sum3* __restrict__ coef,
-                                                            int HW, int C, int total4, float* __restrict__ dy) {
-    const int i4 = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i4 >= total4) return;
+                                                            int HW, int C, int total4, float* __restrict__ dy,
+                                                            float* __restrict__ rng) {
+    const int i40 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i40 < total4;
+    const int i4 = live ? i40 : total4 - 1;  // dead lanes recompute the last float4, store nothing
     const int C4 = C >> 2;
     const int pp = i4 / C4;
     const int c4 = i4 - pp * C4;
@@ -600,7 +611,8 @@ __global__ __launch_bounds__(256) void cb_bwd_apply4_kernel(const float* __restr
     DCS_APPLY_LANE(z, 2, k1.z, k1.w, k2.x)
     DCS_APPLY_LANE(w, 3, k2.y, k2.z, k2.w)
 #undef DCS_APPLY_LANE
-    reinterpret_cast<float4*>(dy)[i4] = o;
+    if (live) reinterpret_cast<float4*>(dy)[i4] = o;
+    range_note(rng, absmax4(o));  // every lane
 }
 
 static inline int cb_chunks(int N, int HW) {
@@ -648,7 +660,7 @@ using namespace dcs;
 extern "C" int dcs_cbam_forward(const float* x, const float* y, const float* scale, const float* shift,
                                 const float* ymax, const float* w1, const float* w2, const float* wsa, int N, int H,
                                 int W, int C, int Cr, int ksa, float* ca, float* sin_, int32_t* sarg, float* sa,
-                                float* out, void* stream) {
+                                float* out, float* rng, void* stream) {
     if (!x || !y || !scale || !shift || !ymax || !w1 || !w2 || !wsa || !ca || !sin_ || !sarg || !sa || !out)
         return fail(DCS_E_INVALID, "cbam_forward: null pointer");
     if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || Cr <= 0 || ksa <= 0 || (ksa & 1) == 0)
@@ -668,11 +680,12 @@ extern "C" int dcs_cbam_forward(const float* x, const float* y, const float* sca
                             P, sin_, sarg);
     e = check_launch("sa_reduce");
     if (e) return e;
-    if (nq == 4) DCS_CB16(sa_apply16_kernel, 4, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
-    else if (nq == 2) DCS_CB16(sa_apply16_kernel, 2, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
-    else if (nq == 1) DCS_CB16(sa_apply16_kernel, 1, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out);
+    if ((e = range_zero(rng, s))) return e;
+    if (nq == 4) DCS_CB16(sa_apply16_kernel, 4, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out, rng);
+    else if (nq == 2) DCS_CB16(sa_apply16_kernel, 2, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out, rng);
+    else if (nq == 1) DCS_CB16(sa_apply16_kernel, 1, x, y, scale, shift, ca, sin_, wsa, H, W, C, ksa, P, sa, out, rng);
     else hipLaunchKernelGGL(sa_apply_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, x, y, scale, shift, ca, sin_,
-                            wsa, H, W, C, ksa, P, sa, out);
+                            wsa, H, W, C, ksa, P, sa, out, rng);
     return check_launch("sa_apply");
 }
 
@@ -685,7 +698,7 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
                                  const float* ymax, const int32_t* yargmax, const float* w1, const float* w2,
                                  const float* wsa, const float* ca, const float* sin_, const int32_t* sarg,
                                  const float* sa, int N, int H, int W, int C, int Cr, int ksa, float* dy, float* dw1,
-                                 float* dw2, float* dwsa, void* ws, size_t ws_bytes, void* stream) {
+                                 float* dw2, float* dwsa, void* ws, size_t ws_bytes, float* rng, void* stream) {
     if (!dout || !y || !scale || !shift || !ymax || !yargmax || !w1 || !w2 || !wsa || !ca || !sin_ || !sarg || !sa ||
         !dy || !dw1 || !dw2 || !dwsa || !ws)
         return fail(DCS_E_INVALID, "cbam_backward: null pointer");
@@ -729,14 +742,15 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     hipLaunchKernelGGL(cb_bwd_dw_reduce_kernel, dim3((unsigned)cdiv(2LL * C * Cr, 256)), dim3(256), 0, s, w.dwpart, N,
                        C * Cr, dw1, dw2);
     if ((e = check_launch("cb_bwd_dw_reduce"))) return e;
+    if ((e = range_zero(rng, s))) return e;
     const long long total = P * C;
     if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31)) {  // C % 4 == 0 checked above
         const int total4 = (int)(total / 4);
         hipLaunchKernelGGL(cb_bwd_apply4_kernel, dim3((unsigned)cdiv(total4, 256)), dim3(256), 0, s, dout, y, scale,
-                           shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total4, dy);
+                           shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total4, dy, rng);
     } else {
         hipLaunchKernelGGL(cb_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, dout, y, scale, shift,
-                           ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy);
+                           ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total, dy, rng);
     }
     return check_launch("cb_bwd_apply");
 }

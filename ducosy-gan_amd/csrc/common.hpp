@@ -30,6 +30,12 @@ inline int check_launch(const char* what) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+// zero an f16x3 range record before its producer's atomic maxima (a no-op for rng == nullptr)
+inline int range_zero(float* rng, hipStream_t s) {
+    if (!rng) return 0;
+    const hipError_t e = hipMemsetAsync(rng, 0, DCS_RANGE_PARTS * sizeof(float), s);
+    return e == hipSuccess ? 0 : fail((int)e, "range record memset failed");
+}
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 constexpr int WAVE = 64;
@@ -59,6 +65,21 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
+}
+
+// f16x3 range record (include/ducosy_hip.h DCS_RANGE_PARTS): a producer kernel folds the max
+// |value| it wrote into rng[block % DCS_RANGE_PARTS] by an atomic max on the float bits
+// (non-negative floats order as unsigned ints); the ABI call zeroed rng first (range_zero).
+// m: this lane's max |value|; every lane of the wave calls it (the reduction shuffles).
+__device__ __forceinline__ void range_note(float* __restrict__ rng, float m) {
+    if (!rng) return;  // kernel argument: wave-uniform
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0)
+        atomicMax(reinterpret_cast<unsigned int*>(rng) + ((blockIdx.x + blockIdx.y * 7919u) & (DCS_RANGE_PARTS - 1)),
+                  __float_as_uint(m));
+}
+__device__ __forceinline__ float absmax4(const float4& v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {

@@ -196,6 +196,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_OCC
 #define DCS_X6_OCC 2  // bf16x6 rows: workgroups per CU the register budget is sized for
 #endif
+#ifndef DCS_H3_NSUB
+#define DCS_H3_NSUB 2  // f16x3 rows, 128-column tiles: 16-k sub-tiles per barrier (64-column tiles: 1)
+#endif
 #ifndef DCS_X6_BM256
 #define DCS_X6_BM256 1  // bf16x6 residual rows: 256 x 128 tiles (512 threads)
 #endif
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
     // f16x3 (H3): two fp16 planes; the vectorised gathers stage two 16-k sub-tiles per barrier
     // (32 k: the MFMAs per barrier of the 16-k bf16x6 tile), the 4-channel stem one
     constexpr bool H3 = MMA == MMA_F16X3;
-    constexpr int NSUB = (H3 && VEC == 1) ? 2 : 1;  // 16-k sub-tiles per k-tile (split-at-store modes)
+    constexpr int NSUB = (H3 && VEC == 1 && BN == 128) ? DCS_H3_NSUB : 1;  // 16-k sub-tiles per k-tile (split-at-store modes)
     constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : (MMA == MMA_BF16P ? 48 : (H3 ? 16 * NSUB : BK));  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
     constexpr bool X6L = MMA == MMA_BF16X6 || MMA == MMA_BF16P || H3;  // the x6 LDS planes and pipeline
     constexpr bool X6F = MMA == MMA_BF16X6 || H3;  // operands split at the LDS store (prologue deferred there)
@@ -2933,24 +2936,27 @@ extern "C" int dcs_conv_wgrad_narrow(const dcs_conv_desc* dp, const float* dy, c
 }
 
 __global__ void pack_nhwc4_kernel(const float* __restrict__ x, int c1, const float* __restrict__ x2, int c2,
-                                  long long HW, long long total, float4* __restrict__ out) {
-    long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel index n*HW + hw
-    if (p >= total) return;
-    const long long n = p / HW, hw = p - n * HW;
+                                  long long HW, long long total, float4* __restrict__ out, float* __restrict__ rng) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel index n*HW + hw
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < c1; ++c) v[c] = x[(n * c1 + c) * HW + hw];
-    for (int c = 0; c < c2; ++c) v[c1 + c] = x2[(n * c2 + c) * HW + hw];
-    out[p] = make_float4(v[0], v[1], v[2], v[3]);
+    if (p < total) {
+        const long long n = p / HW, hw = p - n * HW;
+        for (int c = 0; c < c1; ++c) v[c] = x[(n * c1 + c) * HW + hw];
+        for (int c = 0; c < c2; ++c) v[c1 + c] = x2[(n * c2 + c) * HW + hw];
+        out[p] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    range_note(rng, absmax4(make_float4(v[0], v[1], v[2], v[3])));  // every lane
 }
 
 extern "C" int dcs_pack_nhwc4(const float* x, int c1, const float* x2, int c2, int N, int H, int W, float* out,
-                              void* stream) {
+                              float* rng, void* stream) {
     if (!x || !out || c1 < 1 || c2 < 0 || c1 + c2 > 4 || (c2 > 0 && !x2) || N <= 0 || H <= 0 || W <= 0 ||
         (reinterpret_cast<uintptr_t>(out) & 15))
         return fail(DCS_E_INVALID, "pack_nhwc4: bad arguments");
+    if (int e = range_zero(rng, as_stream(stream))) return e;
     const long long HW = (long long)H * W, total = (long long)N * HW;
     hipLaunchKernelGGL(pack_nhwc4_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), x, c1,
-                       x2, c2, HW, total, reinterpret_cast<float4*>(out));
+                       x2, c2, HW, total, reinterpret_cast<float4*>(out), rng);
     return check_launch("pack_nhwc4");
 }
 

@@ -140,13 +140,17 @@ namespace dcs {
 // dy = da * act'(y) for a = act(y) given the PRE-activation y (relu/lrelu), or given the
 // OUTPUT y for tanh (a = tanh(.), da/dpre = 1 - a^2).
 __global__ void act_backward_kernel(const float* __restrict__ da, const float* __restrict__ y,
-                                    float* __restrict__ dy, long long n, int act) {
+                                    float* __restrict__ dy, long long n, int act, float* __restrict__ rng) {
+    float m = 0.f;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
         float v = y[i];
         float g = act == DCS_ACT_TANH ? (1.f - v * v) : act_grad(v, act);
-        dy[i] = da[i] * g;
+        const float o = da[i] * g;
+        dy[i] = o;
+        m = fmaxf(m, fabsf(o));
     }
+    range_note(rng, m);
 }
 
 // out = x * (*s)   (s a device scalar: loss backward without a host sync)
@@ -225,13 +229,15 @@ static inline int csum_chunks(long long P) {
 
 }  // namespace dcs
 
-extern "C" int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, void* stream) {
+extern "C" int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, float* rng,
+                                void* stream) {
     if (!da || !y || !dy || n < 0) return fail(DCS_E_INVALID, "act_backward: bad arguments");
+    if (int e = range_zero(rng, as_stream(stream))) return e;
     if (n == 0) return DCS_OK;
     long long blocks = cdiv(n, 256);
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(act_backward_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), da, y, dy,
-                       (long long)n, act);
+                       (long long)n, act, rng);
     return check_launch("act_backward");
 }
 

