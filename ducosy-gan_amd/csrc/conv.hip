@@ -18,10 +18,10 @@
 // staged double-buffered LDS ([k][m] layouts, m contiguous, padded by 4 floats), each wave
 // owns (BM/2)x(BN/2) = 2x2 or 2x1 32x32 MFMA accumulators.
 #include "common.hpp"
+#include "conv_common.hpp"
 
 namespace dcs {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // MFMA operand modes (dcs_conv_desc.mma): exact f32 (v_mfma_f32_32x32x2_f32), bf16 operands
@@ -46,7 +46,6 @@ constexpr int lde_bf16() { return MMA == MMA_BF16X3 ? 72 : 40; }
 
 // split 8 floats into hi (round-to-nearest bf16, one v_cvt_pk_bf16_f32 per pair) and, for
 // bf16x3, lo = bf16(v - hi) with hi re-expanded by bit shifts (bf16 -> f32 is exact)
-typedef float floatx8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 template <int MMA>
 __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
@@ -91,38 +90,6 @@ __device__ __forceinline__ void split8x3(const float4& a, const float4& b, bf16x
 }
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-
-// f16x3 split: v' = v * 2^s (exact), hi = fp16(v'), lo = fp16(v' - hi) (the residual is exact in
-// fp32; |v' - hi - lo| <= 2^-22 |v'| while |v'| < 2^15 and lo is normal, else an absolute
-// 2^-25 floor from the fp16 denormals, far below the tensor's 2^15 top)
-__device__ __forceinline__ void split8h(const float4& a, const float4& b, float sc, f16x8& hi, f16x8& lo) {
-    const floatx8 f = floatx8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w} * sc;
-    hi = __builtin_convertvector(f, f16x8);
-    lo = __builtin_convertvector(f - __builtin_convertvector(hi, floatx8), f16x8);
-}
-__device__ __forceinline__ void split4h(const float4& a, float sc, f16x4& hi, f16x4& lo) {
-    const f32x4v f = f32x4v{a.x, a.y, a.z, a.w} * sc;
-    hi = __builtin_convertvector(f, f16x4);
-    lo = __builtin_convertvector(f - __builtin_convertvector(hi, f32x4v), f16x4);
-}
-
-// f16x3 operand exponent: s with max|operand| * 2^s < 2^15, from the n (<= 1024) partial
-// maxima of the operand's range record (every wave reduces them itself; wave-uniform result)
-__device__ __forceinline__ int f16x3_exp(const float* __restrict__ rng, int n) {
-    const int lane = threadIdx.x & 63;
-    float m = 0.f;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, rng[i]);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    int e = 0;
-    (void)frexpf(m, &e);  // m = f * 2^e, 0.5 <= f < 1 (e = 0 for m = 0)
-    int sh = 15 - e;
-    sh = sh < -100 ? -100 : (sh > 100 ? 100 : sh);
-    return __builtin_amdgcn_readfirstlane(sh);
-}
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x4v unpack4(const bf16x4& h) {
     u32x2v w;
@@ -299,10 +266,26 @@ struct RowInfo {
     long long out_off;    // element offset of the output pixel (channel 0), -1 if invalid
 };
 
-// fold (conv_rows_kernel of dcs_conv_dgrad_reflect only): see the fold branch below
+// fold (conv_rows_kernel of dcs_conv_dgrad_reflect only): see the fold branches below
 __device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassGeom& g, int m, int fold = 0) {
     // 32-bit index math: the host guarantees N*My*Mx < 2^31
     RowInfo r;
+    if (fold == 2) {
+        // the one-pixel ring of the (H+2) x (W+2) padded grid only (dcs_conv_dgrad_reflect_win: the
+        // interior comes from the window kernel), rows in the ring buffer's order: top row, bottom
+        // row, then (left, right) of rows 1..H; out_off indexes the ring buffer
+        const int H = d.Ho - 2, ringlen = 2 * d.Wo + 2 * H;
+        if (m >= ringlen * d.N) { r.n = 0; r.by = -100000; r.bx = -100000; r.out_off = -1; return r; }
+        const int n = m / ringlen, idx = m - n * ringlen;
+        int oy, ox;
+        if (idx < 2 * d.Wo) { oy = idx < d.Wo ? 0 : d.Ho - 1; ox = idx < d.Wo ? idx : idx - d.Wo; }
+        else { const int u = idx - 2 * d.Wo; oy = 1 + (u >> 1); ox = (u & 1) ? d.Wo - 1 : 0; }
+        r.n = n;
+        r.by = oy * d.stride - d.pt;
+        r.bx = ox * d.stride - d.pl;
+        r.out_off = ((long long)n * ringlen + idx) * d.Co;
+        return r;
+    }
     const int per = g.My * g.Mx;
     if (m >= per * d.N) { r.n = 0; r.by = -100000; r.bx = -100000; r.out_off = -1; return r; }
     const int n = m / per;
@@ -506,12 +489,6 @@ __global__ __launch_bounds__(256) void pack_weights_r_kernel(const float* __rest
 // ---------------------------------------------------------------------------------------
 constexpr int LDK = BK + 4;  // padded k row (floats)
 
-__device__ __forceinline__ int xcd_remap(int L, int T) {
-    // bijective: blocks L, L+8, ... share an XCD under round-robin dispatch
-    const int xcd = L & 7, q = T >> 3, r = T & 7;
-    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    return base + (L >> 3);
-}
 
 // One k-tile (32 k) of MFMAs.  Two-level fp32 summation: the 16 k-steps of a tile chain into
 // a fresh accumulator that is then added to the running total, so a K-long reduction is a
@@ -771,7 +748,7 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
     const int mtile = rest % gx;
     const int z = rest / gx;
     const ClassGeom g = class_geom(d, z);
-    const long long M = (long long)g.My * g.Mx * d.N;
+    const long long M = fold == 2 ? (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2)) : (long long)g.My * g.Mx * d.N;
     const long long m0 = (long long)mtile * BM;
     if (m0 >= M) return;
     const int n0 = ntile * BN;
@@ -2187,10 +2164,15 @@ extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int
     return check_launch("pack_weights");
 }
 
-namespace {
+namespace dcs {
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
                    const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream,
-                   int fold = 0) {
+                   int fold = 0);
+}  // namespace dcs
+namespace dcs {
+int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
+                   const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream,
+                   int fold) {
     int e = validate(dp, true);
     if (e) return e;
     const dcs_conv_desc& d = *dp;
@@ -2208,6 +2190,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         long long M = (long long)g.My * g.Mx * d.N;
         if (M > Mmax) Mmax = M;
     }
+    if (fold == 2) Mmax = (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2));  // ring rows only
     const int gx = (int)cdiv(Mmax, 128), gy = (int)cdiv(d.Co, BN);
     dim3 grid((unsigned)(gx * gy * ncls));
     if (bm_used) *bm_used = 128;
@@ -2289,7 +2272,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     }
     return check_launch("conv_rows");
 }
-}  // namespace
+}  // namespace dcs
 
 extern "C" int dcs_conv_rows(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack,
                              const float* bias, const float* psc, const float* psh, float* out, void* stream) {
@@ -3002,6 +2985,16 @@ extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, 
                        dx, d.N, H, W, C4);
     return check_launch("reflect_ring_fold");
 }
+
+namespace dcs {
+// fold the padded grid's ring (dcs_conv_dgrad_reflect's ring layout) onto dx's border (H x W interior)
+int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, hipStream_t s) {
+    const int C4 = C / 4;
+    const long long total = (long long)N * (2 * W + 2 * (H - 2)) * C4;
+    hipLaunchKernelGGL(reflect_ring_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, ring, dx, N, H, W, C4);
+    return check_launch("reflect_ring_fold");
+}
+}  // namespace dcs
 
 extern "C" int dcs_upsample2_grad(const float* dup, float* dx, int N, int H, int W, int C, void* stream) {
     if (!dup || !dx || N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0)

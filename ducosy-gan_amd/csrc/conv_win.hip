@@ -1,0 +1,446 @@
+// 3x3 stride-1 'same' convolution over whole image rows on f16x3 operands, the source window of a
+// tile staged once per 16-channel slice (the residual-block convolutions of modules/model.py:72-80:
+// forward with reflection padding, and the interior of the data gradient with zero padding over
+// flipped weights).
+//
+// conv.hip's rows pass gathers A[pixel][(tap, channel)] into LDS per k-tile: every source value is
+// fetched, split into hi/lo fp16 and stored nine times (once per tap).  Here a workgroup owns 256
+// consecutive pixels of one image (R = 256 / W whole rows) x 128 output channels, and per 16-channel
+// slice stages the (R + 2) x (W + 2) source window once (520 pixels at W = 128: 2.0 values per output
+// pixel instead of 9); the nine taps read their MFMA fragments from the window at a per-tap pixel
+// offset.  The weights arrive pre-split (dcs_pack_weights_h3: hi / lo fp16 planes, slice-major K), so
+// their k-tiles are copied to LDS without arithmetic.
+//
+// K loop: 16 slices x 3 kernel rows (ty) = 48 k-tiles of 48 k; a k-tile is three 16-k sub-tiles
+// (tx = 0, 1, 2) of 2 x 2 blocks x 3 products (lo*hi, hi*lo, hi*hi) per wave.  One inner fp32
+// accumulation chain per slice (144 k), added to the running sum (two-level, as conv.hip).
+// 8 waves = 4 (pixels) x 2 (channels) of 64 x 64; one workgroup per CU (115 KB of LDS).
+#include "common.hpp"
+#include "conv_common.hpp"
+
+namespace dcs {
+namespace {
+
+constexpr int WIN_BM = 256, WIN_BN = 128, WIN_NT = 512;
+constexpr int WIN_PIX = 520;             // window pixels for W <= 128: (256 / W + 2) * (W + 2) <= 520
+constexpr int WIN_SLOT = 128 * 16 + 16;  // halves per B plane-slot: 128 rows x 16 k + 16 (bank offset)
+constexpr int WIN_UNITS = (2 * WIN_PIX + WIN_NT - 1) / WIN_NT;  // window (pixel, 8-channel half) units per thread
+
+struct WinArgs {
+    int N, H, W, C, Co;  // source NHWC [N][H][W][C]; output NHWC [N][H][W][Co]
+    int reflect;         // 1: reflection padding (forward), 0: zero padding (data gradient interior)
+    int R, tiles;        // image rows per tile (256 / W), tiles per image (H / R)
+    int gy;              // column tiles (Co / 128)
+    int rng_n;           // partial maxima of the source range record
+};
+
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+
+// half-element offset of (buffer, plane, window pixel, 8-channel half) in the window region:
+// the 16-byte halves of a pixel swap on odd groups of 8 pixels (conflict-free ds_read_b128 for the
+// shifted tap reads and the staging writes alike)
+__device__ __forceinline__ int win_off(int buf, int pl, int wpix, int h) {
+    return ((buf * 2 + pl) * WIN_PIX + wpix) * 16 + 8 * (h ^ ((wpix >> 3) & 1));
+}
+// B: (buffer, plane, tx, output-channel row, half)
+__device__ __forceinline__ int wb_off(int buf, int pl, int tx, int row, int h) {
+    return (buf * 6 + pl * 3 + tx) * WIN_SLOT + row * 16 + 8 * (h ^ ((row >> 3) & 1));
+}
+
+// IN statistics of the tile (as conv.hip rows_in_stats, BM 256 x BN 128): per column the tile's
+// count / mean / M2 / max / first argmax, merged over the four pixel waves in a fixed order
+__device__ __forceinline__ void win_stats(const floatx16 (&acc)[2][2], int p0, int n0, int Co, int wm, int wn,
+                                          int lane, int tid, float* lds, Part* __restrict__ parts, long long chunk) {
+    Part* sp = reinterpret_cast<Part*>(lds);  // [4][128]
+    const int hi = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int colL = wn * 64 + j * 32 + (lane & 31);
+        float s = 0.f, mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = acc[i][j][r];
+                s += v;
+                if (v > mx) { mx = v; am = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi; }
+            }
+        const float mean = s * (1.f / 32.f);
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float dv = acc[i][j][r] - mean;
+                m2 = fmaf(dv, dv, m2);
+            }
+        const float mb = __shfl_xor(mean, 32, 64), m2b = __shfl_xor(m2, 32, 64), mxb = __shfl_xor(mx, 32, 64);
+        const int amb = __shfl_xor(am, 32, 64);
+        if (hi == 0) {
+            const float dl = mb - mean;
+            Part p;
+            p.cnt = 64.f;
+            p.mean = mean + 0.5f * dl;
+            p.m2 = m2 + m2b + dl * dl * 16.f;
+            p.mx = mx;
+            p.amax = am;
+            if (mxb > mx || (mxb == mx && amb < am)) { p.mx = mxb; p.amax = amb; }
+            p.pad[0] = p.pad[1] = p.pad[2] = 0;
+            sp[wm * WIN_BN + colL] = p;
+        }
+    }
+    __syncthreads();
+    if (tid < WIN_BN && n0 + tid < Co) {
+        Part a = sp[tid];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            const Part b = sp[w * WIN_BN + tid];
+            const float tot = a.cnt + b.cnt, dl = b.mean - a.mean;
+            a.mean += dl * (b.cnt / tot);
+            a.m2 += b.m2 + dl * dl * (a.cnt * b.cnt / tot);
+            a.cnt = tot;
+            if (b.mx > a.mx || (b.mx == a.mx && b.amax < a.amax)) { a.mx = b.mx; a.amax = b.amax; }
+        }
+        parts[chunk * Co + n0 + tid] = a;
+    }
+}
+
+__global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
+                                                                 const _Float16* __restrict__ wh,
+                                                                 const _Float16* __restrict__ wl,
+                                                                 const float* __restrict__ rng,
+                                                                 const int* __restrict__ wexp,
+                                                                 const float* __restrict__ addend,
+                                                                 float* __restrict__ out, Part* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT];
+    _Float16* const Wn = smem;                               // [2][2][WIN_PIX][16]
+    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;        // [2][6][WIN_SLOT]
+
+    const int T = gridDim.x;
+    const int L = xcd_remap(blockIdx.x, T);
+    const int ntile = L % a.gy, mt = L / a.gy;
+    const int n = mt / a.tiles, tile = mt - n * a.tiles;
+    const int n0 = ntile * WIN_BN;
+    const int y0 = tile * a.R;                 // first image row of the tile
+    const int W = a.W, WP = a.W + 2, C = a.C;
+    const int K = 9 * C;                       // packed K (slice-major: (c/16)*144 + tap*16 + c%16)
+    const int nslice = C / 16;
+    const int npix = (a.R + 2) * WP;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int l32 = lane & 31, kh = lane >> 5;
+
+    const int ea = f16x3_exp(rng, a.rng_n);
+    const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
+    const float asc = __builtin_ldexpf(1.f, ea);
+
+    // window staging units of this thread: (pixel, 8-channel half); the byte offset of the unit's
+    // source channel 0 (OOB_OFF-style sentinel -1 for zero padding / past the window)
+    int uoff[WIN_UNITS];
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        const int u = tid + q * WIN_NT;
+        const int wpix = u >> 1, h = u & 1;
+        uoff[q] = -1;
+        if (wpix < npix) {
+            const int wr = wpix / WP, wc = wpix - (wpix / WP) * WP;
+            int sy = y0 - 1 + wr, sx = wc - 1;
+            bool ok = true;
+            if (a.reflect) {
+                sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
+                sx = sx < 0 ? -sx : (sx >= W ? 2 * W - 2 - sx : sx);
+            } else {
+                ok = sy >= 0 && sy < a.H && sx >= 0 && sx < W;
+            }
+            if (ok) uoff[q] = (((n * a.H + sy) * W + sx) * C + 8 * h) * 4;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    float4 wr_[WIN_UNITS][2];
+    auto win_load = [&](int s) {
+#pragma unroll
+        for (int q = 0; q < WIN_UNITS; ++q) {
+            const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+            __builtin_memcpy(&wr_[q][0], &v0, 16);
+            __builtin_memcpy(&wr_[q][1], &v1, 16);
+        }
+    };
+    auto win_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < WIN_UNITS; ++q) {
+            const int u = tid + q * WIN_NT;
+            const int wpix = u >> 1, h = u & 1;
+            if (wpix < npix) {
+                f16x8 hi, lo;
+                split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
+                *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
+                *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
+            }
+        }
+    };
+    // B k-tile (slice s, kernel row ty): 2 planes x 128 rows x 48 k = 1536 16-byte chunks, 3 per
+    // thread; chunk q -> (plane, row, tx, half) with (tx, half) fastest (96 contiguous bytes of a row)
+    // per-thread chunk geometry, fixed for the whole loop: global element offset (minus the k-tile's
+    // k base) and LDS offset (minus the buffer's)
+    int bg[3], bl[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int q = tid + i * WIN_NT;
+        const int pl = q / 768, rem = q - pl * 768;
+        const int row = rem / 6, c6 = rem - (rem / 6) * 6;
+        bg[i] = pl * 0x40000000 + (n0 + row) * K + c6 * 8;  // bit 30: the lo plane
+        bl[i] = wb_off(0, pl, c6 >> 1, row, c6 & 1);
+    }
+    uint4 br0, br1, br2;  // named (an array here was promoted to LDS)
+    auto b_ld = [&](int i, int kb) {
+        const int g = bg[i] & 0x3fffffff;
+        const _Float16* w = (bg[i] >> 30) ? wl : wh;
+        return *reinterpret_cast<const uint4*>(w + g + kb);
+    };
+    auto b_load = [&](int t) {
+        const int s = t / 3, ty = t - 3 * (t / 3);
+        const int kb = s * 144 + ty * 48;
+        br0 = b_ld(0, kb);
+        br1 = b_ld(1, kb);
+        br2 = b_ld(2, kb);
+    };
+    auto b_store = [&](int buf) {
+        const int boff = buf * 6 * WIN_SLOT;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[0]) = br0;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[1]) = br1;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[2]) = br2;
+    };
+
+    // window pixel of this lane's output row in each 32-row block (tap (0, 0) = the window's top-left)
+    int wb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = wm * 64 + i * 32 + l32;
+        wb[i] = (q / W) * WP + (q - (q / W) * W);
+    }
+
+    floatx16 acc[2][2], t[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
+
+    // prologue: window of slice 0, B tile 0; B tile 1 in flight
+    win_load(0);
+    b_load(0);
+    win_store(0);
+    b_store(0);
+    __syncthreads();
+    b_load(1);
+
+    for (int s = 0; s < nslice; ++s) {
+        const int wbuf = s & 1;
+        if (s + 1 < nslice) win_load(s + 1);
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) {
+            const int tt = 3 * s + ty, bbuf = tt & 1;
+#pragma unroll
+            for (int tx = 0; tx < 3; ++tx) {
+                f16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int wpix = wb[i] + ty * WP + tx;
+                    ah[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
+                    al[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int row = wn * 64 + j * 32 + l32;
+                    bh[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 0, tx, row, kh));
+                    bl[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 1, tx, row, kh));
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    }
+            }
+            // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2
+            if (tt + 1 < 3 * nslice) b_store(bbuf ^ 1);
+            if (tt + 2 < 3 * nslice) b_load(tt + 2);
+            if (ty == 2 && s + 1 < nslice) win_store(wbuf ^ 1);
+            __syncthreads();
+        }
+        // close the slice's accumulation chain (144 k)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] += t[i][j];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+            }
+    }
+
+    // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
+    const int eab = -(ea + eb);
+    const int p0 = y0 * W;  // the tile's first pixel within the image
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const long long off = ((long long)n * a.H * W + pix) * a.Co + col;
+                float v = acc[i][j][r];
+                if (addend) v += addend[off];
+                out[off] = v;
+            }
+    }
+    if (parts) win_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(smem), parts,
+                         (long long)n * a.tiles + tile);
+}
+
+// pre-split weight pack (dcs_pack_weights_h3): the range of the raw weights first, then every block
+// derives the same exponent and writes hi / lo fp16 planes of the slice-major B
+__global__ __launch_bounds__(256) void wrange_kernel(const float* __restrict__ w, long long n, float* __restrict__ parts) {
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+        m = fmaxf(m, fabsf(w[i]));
+    __shared__ float red[4];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ w, int Cout, int Cin, int flip,
+                                                      int ncols, const float* __restrict__ parts, int nparts,
+                                                      _Float16* __restrict__ oh, _Float16* __restrict__ ol,
+                                                      int* __restrict__ wexp) {
+    const int e = f16x3_exp(parts, nparts);  // every wave derives the same exponent
+    const float sc = __builtin_ldexpf(1.f, e);
+    if (blockIdx.x == 0 && threadIdx.x == 0) wexp[0] = e;
+    const int C = flip ? Cout : Cin;  // reduction channels per tap
+    const int K = 9 * C;
+    const long long total = (long long)ncols * K;
+    for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const int col = (int)(idx / K), k = (int)(idx - (long long)col * K);
+        const int slice = k / 144, rem = k - slice * 144;
+        const int tap = rem >> 4, c = slice * 16 + (rem & 15);
+        int ty = tap / 3, tx = tap - 3 * (tap / 3);
+        float v = 0.f;
+        if (!flip) {  // forward: B[k][co] = W[co][c][ty][tx]
+            if (col < Cout) v = w[(((long long)col * Cin + c) * 3 + ty) * 3 + tx];
+        } else {      // data gradient: B[k][ci] = W[c][ci][2-ty][2-tx] (c = output channel of the forward)
+            if (col < Cin) v = w[(((long long)c * Cin + col) * 3 + (2 - ty)) * 3 + (2 - tx)];
+        }
+        const float f = v * sc;
+        const _Float16 h = (_Float16)f;
+        oh[idx] = h;
+        ol[idx] = (_Float16)(f - (float)h);
+    }
+}
+
+int win_check(const dcs_conv_desc& d, bool fwd) {
+    const bool geom = d.KH == 3 && d.KW == 3 && d.stride == 1 && d.up == 1 && !d.parity && d.Cs % 16 == 0 &&
+                      d.Co % WIN_BN == 0 && d.Ws <= 128 && 256 % d.Ws == 0 && d.Hs % (256 / d.Ws) == 0 &&
+                      d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+                      d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                      d.epi_act == DCS_ACT_NONE && d.mma == DCS_MMA_F16X3 && d.rng_a && d.rng_a_n > 0 &&
+                      d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL;
+    if (!geom) return 0;
+    if (fwd) return d.Ho == d.Hs && d.Wo == d.Ws && d.pt == 1 && d.pl == 1;
+    return d.Ho == d.Hs + 2 && d.Wo == d.Ws + 2 && d.pt == 2 && d.pl == 2 && d.pad_mode == DCS_PAD_ZERO;
+}
+
+int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* src, const void* wh, const void* wl,
+               const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s) {
+    WinArgs a;
+    a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
+    a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
+    const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
+    hipLaunchKernelGGL(conv3_win_h3_kernel, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
+                       reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
+                       addend, out, parts);
+    return check_launch("conv3_win");
+}
+
+}  // namespace
+
+// conv.hip: the generic rows pass (ring rows of the padded data gradient) and the ring fold
+int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
+                   const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream, int fold);
+int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, hipStream_t s);
+
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" size_t dcs_pack_weights_h3_scratch_size(void) { return DCS_RANGE_PARTS * sizeof(float); }
+
+extern "C" int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, int ncols, void* out_hi, void* out_lo,
+                                   float* scratch, int* wexp, void* stream) {
+    if (!w || !out_hi || !out_lo || !scratch || !wexp || Cout <= 0 || Cin <= 0 || ncols <= 0 ||
+        (flip ? Cout : Cin) % 16 != 0 || ncols < (flip ? Cin : Cout))
+        return fail(DCS_E_INVALID, "pack_weights_h3: bad arguments (3x3, reduction channels % 16 == 0)");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(wrange_kernel, dim3(DCS_RANGE_PARTS), dim3(256), 0, s, w, (long long)Cout * Cin * 9, scratch);
+    int e = check_launch("pack_weights_h3 range");
+    if (e) return e;
+    hipLaunchKernelGGL(pack_h3_kernel, dim3(256), dim3(256), 0, s, w, Cout, Cin, flip, ncols, scratch,
+                       (int)DCS_RANGE_PARTS, reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo),
+                       wexp);
+    return check_launch("pack_weights_h3");
+}
+
+extern "C" int dcs_conv3_win_ok(const dcs_conv_desc* dp, int dgrad) { return dp ? win_check(*dp, !dgrad) : 0; }
+
+extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
+                                      const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk,
+                                      void* stream) {
+    if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "conv3_win: null pointer");
+    const dcs_conv_desc& d = *dp;
+    if (!win_check(d, true))
+        return fail(DCS_E_INVALID, "conv3_win: needs a 3x3 stride-1 'same' f16x3 conv over contiguous NHWC rows "
+                                   "(W <= 128, 256 % W == 0, H % (256 / W) == 0, Cs % 16 == 0, Co % 128 == 0)");
+    const int tiles = d.Hs / (256 / d.Ws);
+    if (parts) {
+        if (!nchunk || parts_bytes < (size_t)d.N * tiles * d.Co * sizeof(Part))
+            return fail(DCS_E_WORKSPACE, "conv3_win: parts buffer too small");
+        *nchunk = tiles;
+    }
+    return launch_win(d, d.Hs, d.Ws, d.pad_mode == DCS_PAD_REFLECT, src, w_hi, w_lo, wexp, nullptr, out,
+                      reinterpret_cast<Part*>(parts), as_stream(stream));
+}
+
+extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* dy, const float* wpack,
+                                          const void* w_hi, const void* w_lo, const int* wexp, const float* addend,
+                                          float* dx, float* ring, void* stream) {
+    if (!dp || !dy || !wpack || !w_hi || !w_lo || !wexp || !dx || !ring)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect_win: null pointer");
+    const dcs_conv_desc& d = *dp;
+    if (!win_check(d, false) || d.Co % 4 != 0 || d.Hs < 4 || d.Ws < 4)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect_win: the padded-grid data gradient of a 3x3 reflect-pad-1 conv "
+                                   "(dcs_conv_dgrad_reflect's descriptor) with an f16x3 window geometry expected");
+    hipStream_t s = as_stream(stream);
+    // interior: a 'same' zero-pad conv of dy over the flipped weights, straight into dx (+ addend)
+    int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, addend, dx, nullptr, s);
+    if (e) return e;
+    // the padded grid's one-pixel ring by the generic rows pass, then folded onto the border
+    if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
+    return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, s);
+}

@@ -36,6 +36,8 @@ _KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
 # reflection fold of the stride-1 pad-1 data gradient in the conv epilogue (dcs_conv_dgrad_reflect);
 # "0" = padded-grid rows pass + dcs_reflect_fold (A/B)
 _FUSE_FOLD = os.environ.get("DUCOSY_FUSE_FOLD", "1") == "1"
+# f16x3 residual convs on the window kernel (csrc/conv_win.hip); "0" = the rows pass (A/B)
+_WIN = os.environ.get("DUCOSY_WIN", "1") == "1"
 
 
 def set_mma(mode: str) -> None:
@@ -136,7 +138,7 @@ def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[
     d.mma = _MMA
     if _MMA != lib.MMA_F16X3:
         return
-    if a is None or b_rng is None or not a.is_contiguous() or a.numel() % 4 or a.data_ptr() % 16:
+    if a is None or b_rng is None or not a.is_contiguous() or (a.numel() // a.shape[0]) % 4 or a.data_ptr() % 16:
         d.mma = lib.MMA_BF16X6
         return
     ra = range_rec(a, a_pro)
@@ -274,6 +276,25 @@ class ConvGeom:
                 and self.pads == (1, 1, 1, 1) and self.cout > 4 and self.cin % 16 == 0)
 
     # ---- weight packing ------------------------------------------------------------
+    @property
+    def win(self) -> bool:
+        """f16x3 window kernel for this geometry (3x3 stride-1 pad-1, csrc/conv_win.hip): the packs
+        also carry the pre-split fp16 planes (``_dcs_h3``); used where the call's image fits."""
+        return (_WIN and _MMA == lib.MMA_F16X3 and self.k == 3 and self.stride == 1 and self.up == 1
+                and self.pads == (1, 1, 1, 1) and self.cin % 16 == 0 and self.cout % 128 == 0)
+
+    def _attach_h3(self, wpack: torch.Tensor, w: torch.Tensor, flip: int) -> torch.Tensor:
+        ncols = self.cin if flip else self.cout
+        K = 9 * (self.cout if flip else self.cin)
+        hi = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
+        lo = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
+        wexp = torch.empty(1, device=w.device, dtype=torch.int32)
+        scratch = workspace(lib.query("dcs_pack_weights_h3_scratch_size"), w.device)
+        lib.call("dcs_pack_weights_h3", _p(w), self.cout, self.cin, flip, ncols, _p(hi), _p(lo), _p(scratch),
+                 _p(wexp), _stream())
+        wpack._dcs_h3 = (hi, lo, wexp)
+        return wpack
+
     def pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
         """B operand of the forward GEMM: N-major [Np][Kpad] for the MFMA rows pass (ldb =
         Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns).  ``cin_pad``: the
@@ -283,7 +304,8 @@ class ConvGeom:
         if self.subpixel:
             return self._pack(w, 3, self.cin, 16 * self.cin, self.cout)
         K = self.k * self.k * self.cin
-        return self._pack(w, 0, self.cin, K, self.cout)
+        out = self._pack(w, 0, self.cin, K, self.cout)
+        return self._attach_h3(out, w, 0) if self.win else out
 
     @property
     def c1_dgrad(self) -> bool:
@@ -311,7 +333,8 @@ class ConvGeom:
             return self._pack(w, 4, ci, 16 * self.cout, ci)
         kind = 2 if self.stride == 2 else 1
         K = self.k * self.k * self.cout
-        return self._pack(w, kind, ci, K, ci)
+        out = self._pack(w, kind, ci, K, ci)
+        return self._attach_h3(out, w, 1) if (self.win and ci == self.cin) else out
 
     def _pack(self, w, kind, ci_count, K, ncols):
         if kind in (0, 1) and ncols > 4 and self.kslice:
@@ -370,6 +393,9 @@ class ConvGeom:
         nb = 0 if (self.narrow or not _FUSE_STATS) else lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d))
         if nb and s.t2 is None:
             _set_mma(d, s.t, pro, _wrng(wpack))
+        h3 = getattr(wpack, "_dcs_h3", None)
+        if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
+            return self._win_in_stats(s, d, h3, nb, want_max)
         if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
@@ -393,6 +419,26 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
+    def _win_in_stats(self, s: Src, d, h3, nb, want_max):
+        """Forward + IN statistics on the f16x3 window kernel (csrc/conv_win.hip)."""
+        dev = s.t.device
+        Ho, Wo = self.out_hw(s.H, s.W)
+        out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
+        parts = workspace(nb, dev)
+        nchunk = ctypes.c_int(0)
+        e0 = PROBE.begin() if _is_res_geom(self) else None
+        lib.call("dcs_conv3_win_in_stats", ctypes.byref(d), _p(s.t), _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out),
+                 _p(parts), parts.numel(), ctypes.byref(nchunk), _stream())
+        PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
+        C = self.cout
+        scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        shift = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        xmax = torch.empty(s.N, C, device=dev, dtype=torch.float32) if want_max else None
+        xam = torch.empty(s.N, C, device=dev, dtype=torch.int32) if want_max else None
+        lib.call("dcs_in_stats_finish", _p(parts), s.N, C, nchunk.value, IN_EPS, _p(scale), _p(shift), _p(xmax),
+                 _p(xam), _stream())
+        return out, INStats(scale, shift, xmax, xam)
+
     def forward(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
                 epi_act: int = ACT_NONE) -> torch.Tensor:
@@ -405,9 +451,14 @@ class ConvGeom:
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
         if not self.narrow and s.t2 is None:
             _set_mma(d, s.t, pro, _wrng(wpack))
+        h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
-        lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
-                 _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
+        if h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
+            lib.call("dcs_conv3_win_in_stats", ctypes.byref(d), _p(s.t), _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out),
+                     None, 0, None, _stream())
+        else:
+            lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
+                     _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())
         PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
         return out
 
@@ -479,6 +530,17 @@ class ConvGeom:
             p = t
             d.pt = d.pl = self.k - 1
             d.Ho, d.Wo = Hv + 2 * p, Wv + 2 * p
+            h3 = getattr(wpack_d, "_dcs_h3", None)
+            if h3 is not None and not narrow and dy.is_contiguous() and \
+                    lib.query("dcs_conv3_win_ok", ctypes.byref(d), 1):
+                out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
+                ring = torch.empty(lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4,
+                                   device=dev, dtype=torch.float32)
+                e0 = PROBE.begin() if _is_res_geom(self) else None
+                lib.call("dcs_conv_dgrad_reflect_win", ctypes.byref(d), _p(dy), _p(wpack_d), _p(h3[0]), _p(h3[1]),
+                         _p(h3[2]), _p(addend), _p(out), _p(ring), _stream())
+                PROBE.end(e0, 2.0 * N * H * W * self.cout * ci * self.k * self.k)
+                return out
             if _FUSE_FOLD and addend is None and p == 1 and self.k == 3 and H >= 4 and W >= 4 and not narrow \
                     and dy.is_contiguous() and ci % 4 == 0:
                 # interior written by the conv epilogue, the ring folded in after.  With a residual

@@ -157,6 +157,37 @@ int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int ki
 int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale,
                     const float* shift, int act, float* parts, void* stream);
 
+/* ---- f16x3 window convolution: the residual-block 3x3 convs (modules/model.py:72-80) ----
+ * A workgroup owns 256 consecutive pixels of one image (256 / W whole rows) x 128 output channels
+ * and stages the (rows + 2) x (W + 2) source window once per 16-channel slice, split into hi / lo
+ * fp16; the nine taps read MFMA fragments from it at a per-tap offset (csrc/conv_win.hip).
+ *
+ * dcs_pack_weights_h3: pre-split weights of a 3x3 conv, hi / lo fp16 planes [ncols][9 * C] in the
+ * slice-major K order (k = (c / 16) * 144 + tap * 16 + c % 16), C = Cin for the forward (flip = 0) or
+ * Cout for the data gradient over flipped taps (flip = 1); the values are scaled by 2^wexp[0]
+ * (max |w| * 2^wexp < 2^15), written to *wexp on the device.  scratch: DCS_RANGE_PARTS floats
+ * (dcs_pack_weights_h3_scratch_size bytes).
+ * dcs_conv3_win_ok(d, dgrad): 1 if d is a geometry these passes cover: dgrad = 0, the forward of a
+ * 3x3 stride-1 pad-1 conv (d as for dcs_conv_rows_in_stats); dgrad = 1, the padded-grid data gradient
+ * (d as for dcs_conv_dgrad_reflect); both with mma = DCS_MMA_F16X3 and rng_a set, contiguous NHWC,
+ * W <= 128, 256 % W == 0, H % (256 / W) == 0, Cs % 16 == 0, Co % 128 == 0.
+ * dcs_conv3_win_in_stats: forward + IN statistics partials (as dcs_conv_rows_in_stats; parts = NULL
+ * for none; *nchunk = H * W / 256).
+ * dcs_conv_dgrad_reflect_win: the data gradient of a ReflectionPad2d(1) + 3x3 conv
+ * (dcs_conv_dgrad_reflect's contract, plus the pre-split flipped weights): the interior by the
+ * window pass (+ addend), the padded grid's ring by the rows pass over wpack (fp32 kind 1 |
+ * DCS_PACK_KSLICE with its range record) into ring (dcs_conv_dgrad_reflect_ring_size bytes, any
+ * allocation), folded onto dx's border. */
+size_t dcs_pack_weights_h3_scratch_size(void);
+int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, int ncols, void* out_hi, void* out_lo,
+                        float* scratch, int* wexp, void* stream);
+int dcs_conv3_win_ok(const dcs_conv_desc* d, int dgrad);
+int dcs_conv3_win_in_stats(const dcs_conv_desc* d, const float* src, const void* w_hi, const void* w_lo,
+                           const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream);
+int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* d, const float* dy, const float* wpack, const void* w_hi,
+                               const void* w_lo, const int* wexp, const float* addend, float* dx, float* ring,
+                               void* stream);
+
 /* Forward / data-gradient pass: out = gather(src) x B (+ bias, epilogue act). */
 int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,
                   const float* bias, const float* pro_scale, const float* pro_shift, float* out,

@@ -277,14 +277,15 @@ def test_dgrad_reflect_epilogue_fold_matches_fold_pass(ops, H, mode):
         wd = g.pack_dgrad(w)
         dyn = rnd((2, H, H, 256), 41, "dy").cuda()
         add = rnd((2, H, H, 256), 41, "add").cuda()
-        fused = g.dgrad(dyn, wd, H, H)
-        ops._FUSE_FOLD = False
+        fused = g.dgrad(dyn, wd, H, H)  # f16x3 at H = 16: the window pass (csrc/conv_win.hip)
+        ops._FUSE_FOLD, ops._WIN = False, False
         try:
             plain = g.dgrad(dyn, wd, H, H)
             plain_add = g.dgrad(dyn, wd, H, H, addend=add.clone())
         finally:
-            ops._FUSE_FOLD = True
-        assert rel(fused, plain) < 1e-6
+            ops._FUSE_FOLD, ops._WIN = True, True
+        # the window pass sums in another order (one chain per 16-channel slice)
+        assert rel(fused, plain) < (2e-6 if g.win else 1e-6)
         d = lib.ConvDesc()
         d.N, d.Hs, d.Ws, d.Cs = 2, H, H, 256
         d.s_n, d.s_c, d.s_h, d.s_w = H * H * 256, 1, H * 256, 256
@@ -292,7 +293,8 @@ def test_dgrad_reflect_epilogue_fold_matches_fold_pass(ops, H, mode):
         d.KH = d.KW = 3
         d.pt = d.pl = 2
         d.stride, d.Ho, d.Wo, d.Co = 1, H + 2, H + 2, 256
-        d.ldb, d.mma = wd.shape[1], ops._MMA
+        d.ldb = wd.shape[1]
+        ops._set_mma(d, dyn, None, ops._wrng(wd))  # f16x3: the operands' range records
         d.korder = lib.KORDER_SLICE if g.kslice else lib.KORDER_TAP
         ring = lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4
         buf = torch.empty(2 * H * H * 256 + ring, device=DEV)

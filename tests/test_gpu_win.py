@@ -1,0 +1,120 @@
+"""The f16x3 window kernel of the residual-block convolutions (csrc/conv_win.hip;
+modules/model.py:72-80) against float64 references of the same fp32 operands:
+  * forward (reflection pad 1) + the InstanceNorm statistics of its output (scale / shift / max /
+    argmax from the epilogue partials) at W = 16, 32, 64, 128;
+  * the data gradient onto the reflection-padded input (interior by the window pass, the padded
+    grid's ring by the rows pass, folded onto the border), with and without the residual addend;
+  * equality of bar with the rows pass it replaces: the same fp32-class bound (max error / max |ref|
+    <= 1e-5) and within 1.5x of the exact-f32 MFMA path's error.
+Tolerances written per check below."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import prng
+from test_gpu_ops import rnd
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _relmax(a, b):
+    return float((a.double().cpu() - b).abs().max() / b.abs().max())
+
+
+@pytest.fixture
+def ops():
+    from modules.hip import ops as o
+    prev, prev_win = o.get_mma(), o._WIN
+    yield o
+    o.set_mma(prev)
+    o._WIN = prev_win
+
+
+def _geom(ops, cin=256, cout=256):
+    from modules.hip.lib import DCS_PAD_REFLECT
+    return ops.ConvGeom(cin, cout, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 32, 32), (2, 16, 64), (1, 8, 128)])
+def test_win_forward_and_stats_vs_fp64(ops, N, H, W):
+    ops.set_mma("f16x3")
+    g = _geom(ops)
+    assert g.win
+    x = rnd((N, 256, H, W), 51, "x").double()
+    w = torch.from_numpy(prng.normal(52, "w", (256, 256, 3, 3), 0, 0.05)).float().double()
+    ref = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    mean = ref.mean(dim=(2, 3))
+    var = ref.var(dim=(2, 3), unbiased=False)
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wp = g.pack_fwd(w.float().to(DEV))
+    assert getattr(wp, "_dcs_h3", None) is not None
+    ops.PROBE.reset()
+    y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
+    assert _relmax(y.permute(0, 3, 1, 2), ref) <= 1e-5
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    assert _relmax(st.scale, rstd) <= 1e-5
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= 1e-5 * float((mean * rstd).abs().max() + 1)
+    mx = ref.flatten(2).max(dim=2)
+    assert _relmax(st.xmax, mx.values) <= 1e-5
+    # argmax: the first maximum; where two values tie to within rounding either index is right
+    am = st.xargmax.cpu().long()
+    got_at = ref.flatten(2).gather(2, am[..., None])[..., 0]
+    assert float((got_at - mx.values).abs().max()) <= 1e-5 * float(mx.values.abs().max())
+
+
+@pytest.mark.parametrize("addend", [False, True])
+@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128)])
+def test_win_dgrad_reflect_vs_fp64(ops, N, H, W, addend):
+    ops.set_mma("f16x3")
+    g = _geom(ops)
+    x = rnd((N, 256, H, W), 61, "x").double().requires_grad_(True)
+    w = torch.from_numpy(prng.normal(62, "w", (256, 256, 3, 3), 0, 0.05)).float().double()
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    R = torch.from_numpy(prng.normal(63, "R", tuple(y.shape))).float().double()
+    A = rnd((N, 256, H, W), 64, "A").double() if addend else None
+    (y * R).sum().backward()
+    ref = x.grad + (A if addend else 0)
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Ad = A.float().to(DEV).permute(0, 2, 3, 1).contiguous() if addend else None
+    wd = g.pack_dgrad(w.float().to(DEV))
+    assert getattr(wd, "_dcs_h3", None) is not None
+    dx = g.dgrad(Rd, wd, H, W, addend=Ad)
+    assert _relmax(dx.permute(0, 3, 1, 2), ref) <= 1e-5
+
+
+def test_win_matches_rows_pass_error(ops):
+    """The window pass and the rows pass it replaces (both f16x3) against the exact-f32 path's error
+    vs float64: within 1.5x (fp32-class), forward and data gradient."""
+    N, H, W = 2, 32, 32
+    g = _geom(ops)
+    x = rnd((N, 256, H, W), 71, "x").double().requires_grad_(True)
+    w = torch.from_numpy(prng.normal(72, "w", (256, 256, 3, 3), 0, 0.05)).float().double()
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    R = torch.from_numpy(prng.normal(73, "R", tuple(y.shape))).float().double()
+    (y * R).sum().backward()
+    xd = x.detach().float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    err = {}
+    for tag, mode, win in (("f32", "f32", False), ("rows", "f16x3", False), ("win", "f16x3", True)):
+        ops.set_mma(mode)
+        ops._WIN = win
+        wd = w.float().to(DEV)
+        yy, _ = g.forward_in_stats(ops.Src.nhwc(xd), g.pack_fwd(wd))
+        dx = g.dgrad(Rd, g.pack_dgrad(wd), H, W)
+        err[tag] = (_relmax(yy.permute(0, 3, 1, 2), y.detach()), _relmax(dx.permute(0, 3, 1, 2), x.grad))
+    for k in range(2):
+        assert err["win"][k] <= 1.5 * err["f32"][k] + 1e-7, err
+        assert err["rows"][k] <= 1.5 * err["f32"][k] + 1e-7, err
+
+
+def test_win_ok_rejects_other_geometries(ops):
+    from modules.hip import lib
+    ops.set_mma("f16x3")
+    g = _geom(ops)
+    x = torch.zeros(1, 9, 9, 256, device=DEV)  # 256 % 9 != 0: the rows pass keeps these
+    d = g._desc_fwd(ops.Src.nhwc(x), 2304, 0, 0)
+    ops._set_mma(d, x, None, torch.zeros(512, device=DEV))
+    assert lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0) == 0
