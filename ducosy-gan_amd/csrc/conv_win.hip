@@ -23,7 +23,9 @@ namespace {
 
 constexpr int WIN_BM = 256, WIN_BN = 128, WIN_NT = 512;
 constexpr int WIN_PIX = 520;             // window pixels for W <= 128: (256 / W + 2) * (W + 2) <= 520
-constexpr int WIN_SLOT = 128 * 16 + 16;  // halves per B plane-slot: 128 rows x 16 k + 16 (bank offset)
+// halves per B plane-slot: 128 rows x 16 k + 48 (96 B: the three tx slots of a row, written by
+// neighbouring lanes, land on distinct banks)
+constexpr int WIN_SLOT = 128 * 16 + 48;
 constexpr int WIN_UNITS = (2 * WIN_PIX + WIN_NT - 1) / WIN_NT;  // window (pixel, 8-channel half) units per thread
 
 struct WinArgs {
@@ -240,9 +242,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     __syncthreads();
     b_load(1);
 
+    // every global load below is unconditional (indices clamped at the end): a load under a branch
+    // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer, which here
+    // would expose the window loads' HBM latency at every k-tile's B store
+    const int last = 3 * nslice - 1;
     for (int s = 0; s < nslice; ++s) {
         const int wbuf = s & 1;
-        if (s + 1 < nslice) win_load(s + 1);
+        win_load(s + 1 < nslice ? s + 1 : s);
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) {
             const int tt = 3 * s + ty, bbuf = tt & 1;
@@ -270,10 +276,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                         t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
                     }
             }
-            // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2
-            if (tt + 1 < 3 * nslice) b_store(bbuf ^ 1);
-            if (tt + 2 < 3 * nslice) b_load(tt + 2);
-            if (ty == 2 && s + 1 < nslice) win_store(wbuf ^ 1);
+            // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2 (past the end:
+            // a repeat into a buffer nobody reads again)
+            b_store(bbuf ^ 1);
+            b_load(tt + 2 < last ? tt + 2 : last);
+            if (ty == 2) win_store(wbuf ^ 1);
             __syncthreads();
         }
         // close the slice's accumulation chain (144 k)
@@ -296,19 +303,32 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int col = n0 + wn * 64 + j * 32 + l32;
+    const long long obase = (long long)n * a.H * W * a.Co;
+    auto ooff = [&](int i, int j, int r) {
+        const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 32 + l32;
+    };
+    if (addend) {  // wave-uniform: all 64 addend loads issued before the first use
+        floatx16 ad[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                const long long off = ((long long)n * a.H * W + pix) * a.Co + col;
-                float v = acc[i][j][r];
-                if (addend) v += addend[off];
-                out[off] = v;
-            }
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ad[i][j][r] = addend[ooff(i, j, r)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r] + ad[i][j][r];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r];
     }
     if (parts) win_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(smem), parts,
                          (long long)n * a.tiles + tile);
