@@ -272,9 +272,13 @@ def main():
                 "parallelism": f"2 groups x dp{world // 2}" if groups else f"dp{world}",
             },
             "roofline": {
-                "kernel": (f"256-ch 3x3 residual conv rows pass: forward conv_rows_kernel<256,128,1,1,{MODE_TAG[args.mma]}>, "
+                "kernel": ("256-ch 3x3 residual conv on the f16x3 window kernel conv3_win_h3_kernel: forward, and the "
+                           "data gradient's interior (+ its padded-grid ring on conv_rows_kernel<128,128,1,1,7> and the "
+                           "ring fold, inside the timed launch)"
+                           if args.mma == "f16x3" else
+                           f"256-ch 3x3 residual conv rows pass: forward conv_rows_kernel<256,128,1,1,{MODE_TAG[args.mma]}>, "
                            f"data gradient conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}>"
-                           if args.mma in ("bf16x6", "f16x3") else
+                           if args.mma == "bf16x6" else
                            f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> (256-ch 3x3 residual conv, fwd+dgrad)"),
                 "bound": "mfma",
                 "achieved": round(achieved, 3),
