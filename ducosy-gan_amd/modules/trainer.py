@@ -175,16 +175,18 @@ class ConcurrentCycleGANs:
     (cin 3) and lung (cin 2) models; the reference trains them one after the other,
     train.py:27-38).
 
-    schedule "serial" (default): the systems step one after the other on the caller's stream.
-    schedule "concurrent": one HIP stream per system, each confined to its own contiguous,
+    schedule "serial" (default, the recommended one): the systems step one after the other on the
+    caller's stream.
+    schedule "concurrent" (EXPERIMENTAL; warns on construction): one HIP stream per system, each confined to its own contiguous,
     pair-aligned share of the compute units (dcs_stream_create_cu_mask); the kernels of one model
     fill the gaps of the other (small normalisation / loss / Adam launches, split-K reductions,
     launch latency).  Workspaces are per stream (ops.workspace).  The CU partition is what makes
     it exact: when the two streams share compute-unit pairs, a model's numbers sometimes leave
-    its sequential run (Config 5: 7/20 repetitions on shared CUs, 9/20 with the
-    models on alternating CUs, 0/54 on disjoint halves, 0/32 on interleaved 8-CU blocks).  With
+    its sequential run (Config 5: 30/74 repetitions on shared CUs, 10/32 with the
+    models on alternating CUs, 0/74 on disjoint halves, 0/32 on interleaved 8-CU blocks).  With
     the partition each model equals its own sequential run bit for bit in every operand mode
-    (tests/test_gpu_concurrent.py).  On 8 GPUs the config-5 schedule is "groups" (bench.py
+    (tests/test_gpu_concurrent.py), but the partition avoids a hazard whose mechanism is
+    inferred, not proven, so the schedule stays experimental.  On 8 GPUs the config-5 schedule is "groups" (bench.py
     --dual-schedule groups, modules/parallel.py): each model on its own half of the ranks."""
 
     def __init__(self, systems, device, schedule="serial"):
@@ -193,6 +195,11 @@ class ConcurrentCycleGANs:
         self.systems = list(systems)
         self.device = torch.device(device)
         self.schedule = schedule
+        if schedule == "concurrent":
+            import warnings
+            warnings.warn("ConcurrentCycleGANs(schedule='concurrent') is experimental: it relies on CU-partitioned "
+                          "streams to avoid a cross-stream hazard (DESIGN.md §3); 'serial' is the recommended "
+                          "schedule", RuntimeWarning, stacklevel=2)
         self.streams = [self._cu_stream(i, len(self.systems)) for i in range(len(self.systems))] \
             if schedule == "concurrent" else []
 
