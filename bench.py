@@ -9,16 +9,18 @@ its Adam, D_A step, D_B step) on the fused HIP path, over one synthetic batch of
 GPU that is already resident in HBM.  Data parallel: one process per GPU, each with its own
 shard; one RCCL all-reduce per optimizer (weak scaling).  Rank 0 prints ONE JSON line.
 
-MFMA operand mode (--mma): bf16x6 by default, an fp32-class split (each fp32 operand = hi + mid
-+ lo bf16, six bf16 MFMAs per product, fp32 accumulation and storage; its measured error
-against float64 is at or below the exact-f32 MFMA path's on every layer, tests/test_gpu_mma.py);
---mma f32 runs the exact v_mfma_f32_32x32x2_f32 path.
+MFMA operand mode (--mma): f16x3 by default, an fp32-class split (each fp32 operand, scaled by a
+power of two from its range record, = hi + lo fp16; three fp16 MFMAs per product, fp32
+accumulation and storage; its measured error against float64 is at or below the exact-f32 MFMA
+path's on every layer, tests/test_gpu_mma.py); --mma f32 runs the exact v_mfma_f32_32x32x2_f32
+path; --mma f16 is BASELINE config 5's fp16 MFMA path (one product of the scaled fp16 operands).
 
-roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (implicit GEMM,
-conv_rows_kernel<128,128,1,1,MODE>, forward + data-gradient launches).  Its per-launch
-duration is measured live with HIP events on the launch stream over the timed steps; FLOPs
-are algorithmic (2*pixels*256*256*9 per launch).  Peak: 157.3 TFLOP/s for f32 (gfx950 f32
-MFMA, dense); for bf16x6 the dense bf16 MFMA peak / 6 = 419.5 TFLOP/s of fp32 work.
+roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (forward + data-gradient
+launches; in the fp16 modes the window kernel conv3_win_h3_kernel).  Its per-launch duration is
+measured live with HIP events on the launch stream over the timed steps; FLOPs are algorithmic
+(2*pixels*256*256*9 per launch).  Peak: 157.3 TFLOP/s for f32 (gfx950 f32 MFMA, dense); the dense
+fp16/bf16 MFMA peak (2.5 PF) divided by the products per fragment pair in the split modes (f16x3:
+3 -> 838.9 TFLOP/s of fp32 work; bf16x6: 6 -> 419.5).
 cpu_baseline: the oracle (oracle/ref_torch.py, the CPU restatement of the reference step)
 timed on this host on a bounded sample (one 512x512 slice, 9 blocks, one step).
 """
@@ -40,13 +42,14 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, den
 BF16_MFMA_PEAK_TFLOPS = 16 * F32_MFMA_PEAK_TFLOPS  # v_mfma_f32_32x32x16_bf16: 16x the f32 rate (~2.5 PF dense)
 # peak per mode for the dominant kernel's algorithmic FLOPs: bf16x3 issues 3 bf16 MFMAs per product
 MODE_PEAK = {"f32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3,
-             "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6, "f16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+             "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6, "f16x3": BF16_MFMA_PEAK_TFLOPS / 3, "f16": BF16_MFMA_PEAK_TFLOPS}
 MODE_DTYPE = {"f32": "f32", "bf16": "bf16 (MFMA operands; f32 accumulation and storage)",
               "bf16x3": "f32 via bf16x3 MFMA (hi/lo split, ~2^-16 per product; f32 accumulation and storage)",
               "bf16x6": "f32 via bf16x6 MFMA (hi/mid/lo split, ~2^-24 per product; f32 accumulation and storage)",
               "f16x3": "f32 via f16x3 MFMA (power-of-two scaled hi/lo fp16 split, 22 significant bits, three "
-                       "products; f32 accumulation and storage)"}
-MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6, "f16x3": 7}
+                       "products; f32 accumulation and storage)",
+              "f16": "f16 (MFMA operands: power-of-two scaled fp16, one product; f32 accumulation and storage)"}
+MODE_TAG = {"f32": 0, "bf16": 1, "bf16x3": 3, "bf16x6": 6, "f16x3": 7, "f16": 8}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -129,11 +132,12 @@ def main():
     ap.add_argument("--blocks", type=int, default=9)
     ap.add_argument("--cin", type=int, default=3, help="1 + masks (soft tissue: 3, lung: 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mma", default="f16x3", choices=["f32", "bf16", "bf16x3", "bf16x6", "f16x3"],
+    ap.add_argument("--mma", default="f16x3", choices=["f32", "bf16", "bf16x3", "bf16x6", "f16x3", "f16"],
                     help="MFMA operand mode of the conv passes: f16x3 = power-of-two scaled hi/lo fp16 split, "
                          "three products, fp32-class (default; error <= the exact-f32 path's, "
                          "tests/test_gpu_mma.py), bf16x6 = three-way bf16 split (fp32-class, 6 products), "
-                         "f32 = exact fp32 MFMA, bf16x3 = hi/lo bf16 split, bf16 = plain bf16 operands")
+                         "f32 = exact fp32 MFMA, bf16x3 = hi/lo bf16 split, bf16 = plain bf16 operands, "
+                         "f16 = scaled fp16 operands, one product (BASELINE config 5's fp16 MFMA path)")
     ap.add_argument("--dual", action="store_true",
                     help="BASELINE config 5: soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one "
                          "process; value counts the images of both models")
@@ -272,10 +276,10 @@ def main():
                 "parallelism": f"2 groups x dp{world // 2}" if groups else f"dp{world}",
             },
             "roofline": {
-                "kernel": ("256-ch 3x3 residual conv on the f16x3 window kernel conv3_win_h3_kernel: forward, and the "
-                           "data gradient's interior (+ its padded-grid ring on conv_rows_kernel<128,128,1,1,7> and the "
-                           "ring fold, inside the timed launch)"
-                           if args.mma == "f16x3" else
+                "kernel": (f"256-ch 3x3 residual conv on the window kernel conv3_win_h3_kernel<{3 if args.mma == 'f16x3' else 1}>: "
+                           "forward, and the data gradient's interior (+ its padded-grid ring on "
+                           f"conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}> and the ring fold, inside the timed launch)"
+                           if args.mma in ("f16x3", "f16") else
                            f"256-ch 3x3 residual conv rows pass: forward conv_rows_kernel<256,128,1,1,{MODE_TAG[args.mma]}>, "
                            f"data gradient conv_rows_kernel<128,128,1,1,{MODE_TAG[args.mma]}>"
                            if args.mma == "bf16x6" else

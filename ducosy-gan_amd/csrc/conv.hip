@@ -35,6 +35,8 @@ constexpr int MMA_BF16P = 2;
 // f16x3 (DCS_MMA_F16X3): fp32 operands scaled by a power of two and split into hi + lo fp16,
 // three products on v_mfma_f32_32x32x16_f16 (include/ducosy_hip.h)
 constexpr int MMA_F16X3 = 7;
+// f16 (DCS_MMA_F16): the f16x3 staging with the hi planes only, one product (hi*hi) per fragment
+constexpr int MMA_F16 = 8;
 #ifndef DCS_BF16_BUFGATHER
 #define DCS_BF16_BUFGATHER 1  // branch-free buffer-descriptor gather in the bf16 rows pass
 #endif
@@ -110,6 +112,9 @@ constexpr int BK = 32;
 constexpr int NT = 256;
 #ifndef DCS_X6_BK
 #define DCS_X6_BK 16
+#endif
+#ifndef DCS_WGRAD_WIN
+#define DCS_WGRAD_WIN 1  // f16x3 residual weight gradient on the rolling-window kernel (conv_win.hip)
 #endif
 #ifndef DCS_WGRAD_X6
 #define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
@@ -687,12 +692,12 @@ __device__ __forceinline__ void x6_interleave() {
 }
 
 template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
-__global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
+__global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || MMA == MMA_F16) ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
     const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts, int fold) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P || MMA == MMA_F16X3) && BN == 128 && VEC == 1),
+    static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P || MMA == MMA_F16X3 || MMA == MMA_F16) && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
     constexpr int NTH = 2 * BM;                    // threads (two per A row)
     constexpr int WM = 64, WN = BN / 2;            // per-wave tile
@@ -702,7 +707,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
     // load-latency bound at 32); f32 and bf16x3 (LDS budget) keep 32
     // f16x3 (H3): two fp16 planes; the vectorised gathers stage two 16-k sub-tiles per barrier
     // (32 k: the MFMAs per barrier of the 16-k bf16x6 tile), the 4-channel stem one
-    constexpr bool H3 = MMA == MMA_F16X3;
+    constexpr bool H3 = MMA == MMA_F16X3 || MMA == MMA_F16;
+    constexpr bool F1 = MMA == MMA_F16;  // f16: hi planes only, one product
     constexpr int NSUB = (H3 && VEC == 1 && BN == 128) ? DCS_H3_NSUB : 1;  // 16-k sub-tiles per k-tile (split-at-store modes)
     constexpr int BKT = MMA == MMA_BF16X6 ? DCS_X6_BK : (MMA == MMA_BF16P ? 48 : (H3 ? 16 * NSUB : BK));  // x6: 3 LDS planes, 16-deep tiles keep 2 blocks/CU
     constexpr bool X6L = MMA == MMA_BF16X6 || MMA == MMA_BF16P || H3;  // the x6 LDS planes and pipeline
@@ -1092,17 +1098,17 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
                 f16x8 hi, lo;
                 split8h(sa[2 * sub], sa[2 * sub + 1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, arow, akq >> 3)) = hi;
-                *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, arow, akq >> 3)) = lo;
+                if constexpr (!F1) *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, arow, akq >> 3)) = lo;
                 if constexpr (BCH == 2 * NSUB) {
                     split8h(sb[2 * sub], sb[2 * sub + 1], bsc, hi, lo);
                     *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = hi;
-                    *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3)) = lo;
+                    if constexpr (!F1) *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3)) = lo;
                 } else {  // 4 k of B per thread: the 8-byte half of a 16-byte chunk
                     f16x4 h4, l4;
                     split4h(sb[sub], bsc, h4, l4);
                     const int q = 4 * ((bkq >> 2) & 1);
                     *reinterpret_cast<f16x4*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3) + q) = h4;
-                    *reinterpret_cast<f16x4*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3) + q) = l4;
+                    if constexpr (!F1) *reinterpret_cast<f16x4*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3) + q) = l4;
                 }
             }
         } else if constexpr (MMA == MMA_BF16X6) {
@@ -1191,20 +1197,22 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
                     for (int i = 0; i < IM; ++i) {
                         const int row = wm * WM + i * 32 + l32;
                         fah[i] = *reinterpret_cast<const f16x8*>(Ah + x6o(sub, cur, row, kh >> 3));
-                        fal[i] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
+                        if constexpr (!F1) fal[i] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
                     }
 #pragma unroll
                     for (int j = 0; j < JN; ++j) {
                         const int row = BM + wn * WN + j * 32 + l32;
                         fbh[j] = *reinterpret_cast<const f16x8*>(Ah + x6o(sub, cur, row, kh >> 3));
-                        fbl[j] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
+                        if constexpr (!F1) fbl[j] = *reinterpret_cast<const f16x8*>(Ah + x6o(NSUB + sub, cur, row, kh >> 3));
                     }
 #pragma unroll
                     for (int i = 0; i < IM; ++i)
 #pragma unroll
                         for (int j = 0; j < JN; ++j) {
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], t[i][j], 0, 0, 0);
+                            if constexpr (!F1) {
+                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], t[i][j], 0, 0, 0);
+                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], t[i][j], 0, 0, 0);
+                            }
                             t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], t[i][j], 0, 0, 0);
                         }
                 }
@@ -1287,8 +1295,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
                     // staging before the chain fold and unconditional (a tile past the end is
                     // zeros into a buffer nobody reads again): one basic block with the MFMAs
                     store_tiles(1, ra, rb, pa1);
-                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? 3 * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
-                                  H3 ? (IM + JN) * 2 * NSUB : 12, H3 ? 4 * NSUB : 6>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? (F1 ? 1 : 3) * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
+                                  H3 ? (IM + JN) * (F1 ? 1 : 2) * NSUB : 12, H3 ? (F1 ? 2 : 4) * NSUB : 6>();
                     fold_t(kt);
                 } else {
                     fold_t(kt);
@@ -1301,8 +1309,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3) ? (
                 step(1, 0);
                 if (DCS_X6_STORE_FIRST) {
                     store_tiles(0, ra2, rb2, pa2);
-                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? 3 * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
-                                  H3 ? (IM + JN) * 2 * NSUB : 12, H3 ? 4 * NSUB : 6>();
+                    x6_interleave<IM * JN * (MMA == MMA_BF16P ? 3 : (H3 ? (F1 ? 1 : 3) * NSUB : 6)), (TAG == 1 && X6F) ? DCS_X6_SGB : DCS_X6_SGB0,
+                                  H3 ? (IM + JN) * (F1 ? 1 : 2) * NSUB : 12, H3 ? (F1 ? 2 : 4) * NSUB : 6>();
                     fold_t(kt + 1);
                 } else {
                     fold_t(kt + 1);
@@ -2088,11 +2096,12 @@ static int validate(const dcs_conv_desc* d, bool rows) {
         return fail(DCS_E_INVALID, "conv: reflect pad larger than the input");
     if (d->csplit < 0 || d->csplit > d->Cs) return fail(DCS_E_INVALID, "conv: bad csplit");
     if (d->cw < 0 || d->cw > d->Cs) return fail(DCS_E_INVALID, "conv: bad cw (weight channels)");
-    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3 && d->mma != MMA_BF16X6 && d->mma != MMA_F16X3)
-        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16, DCS_MMA_BF16X3, DCS_MMA_BF16X6 or DCS_MMA_F16X3");
-    if (d->mma == MMA_F16X3 && (!d->rng_a || !d->rng_b || d->rng_a_n <= 0 || d->rng_b_n <= 0 ||
+    if (d->mma != MMA_F32 && d->mma != MMA_BF16 && d->mma != MMA_BF16X3 && d->mma != MMA_BF16X6 && d->mma != MMA_F16X3 &&
+        d->mma != MMA_F16)
+        return fail(DCS_E_INVALID, "conv: mma must be DCS_MMA_F32, DCS_MMA_BF16, DCS_MMA_BF16X3, DCS_MMA_BF16X6, DCS_MMA_F16X3 or DCS_MMA_F16");
+    if ((d->mma == MMA_F16X3 || d->mma == MMA_F16) && (!d->rng_a || !d->rng_b || d->rng_a_n <= 0 || d->rng_b_n <= 0 ||
                                 d->rng_a_n > 1024 || d->rng_b_n > 1024))
-        return fail(DCS_E_INVALID, "conv: DCS_MMA_F16X3 needs the operand range records rng_a / rng_b (1..1024 partial maxima)");
+        return fail(DCS_E_INVALID, "conv: DCS_MMA_F16X3 / DCS_MMA_F16 need the operand range records rng_a / rng_b (1..1024 partial maxima)");
     if (!d->parity) {
         // output dims must be those of the forward conv over the virtual input
         int Hv = d->Hs * d->up, Wv = d->Ws * d->up;
@@ -2206,10 +2215,13 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
                                    "residual geometry with a vectorisable source");
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
-    const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3;  // split-at-store pipelines
+    const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3 || d.mma == MMA_F16;  // split-at-store pipelines
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16X3>), G, dim3(2 * BM_), 0, s, d, src, src2, \
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);                                        \
+    else if (d.mma == MMA_F16)                                                                                       \
+        hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16>), G, dim3(2 * BM_), 0, s, d, src, src2,   \
                            wpack, bias, psc, psh, out, gxx, gy, parts, fold);                                        \
     else                                                                                                             \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_BF16X6>), G, dim3(2 * BM_), 0, s, d, src, src2, \
@@ -2355,7 +2367,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws, int kt_per_split,
     int gn, int gm) {
     const dcs_conv_desc d = specialise<TAG>(din);
-    constexpr bool H3 = MMA == MMA_F16X3;
+    constexpr bool H3 = MMA == MMA_F16X3 || MMA == MMA_F16;
+    constexpr bool F1 = MMA == MMA_F16;  // f16: hi planes only, one product
     constexpr int NSUB = MMA == MMA_BF16P ? 3 : (H3 ? 2 : 1);  // 16-pixel sub-tiles per k-tile
     constexpr int NSLOT = H3 ? 2 * NSUB : 3;     // LDS planes per operand and buffer (f16x3: [hi|lo][sub])
     constexpr int BM = 128, BN = 128, BKP = 16;  // output channels x (tap, ci) columns x pixels per k-tile
@@ -2470,7 +2483,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
                 f16x8 hi, lo;
                 split8h(ra[2 * sub], ra[2 * sub + 1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(X + xo(0, sub, buf, kr, cc)) = hi;
-                *reinterpret_cast<f16x8*>(X + xo(0, NSUB + sub, buf, kr, cc)) = lo;
+                if constexpr (!F1) *reinterpret_cast<f16x8*>(X + xo(0, NSUB + sub, buf, kr, cc)) = lo;
                 float4 rb[2] = {rbl[2 * sub], rbl[2 * sub + 1]};
                 if (d.pro_act != DCS_ACT_NONE && pro[sub] >= 0) {
 #pragma unroll
@@ -2479,7 +2492,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
                 }
                 split8h(rb[0], rb[1], bsc, hi, lo);
                 *reinterpret_cast<f16x8*>(X + xo(1, sub, buf, kr, cc)) = hi;
-                *reinterpret_cast<f16x8*>(X + xo(1, NSUB + sub, buf, kr, cc)) = lo;
+                if constexpr (!F1) *reinterpret_cast<f16x8*>(X + xo(1, NSUB + sub, buf, kr, cc)) = lo;
             }
             return;
         }
@@ -2549,32 +2562,34 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
 #pragma unroll
                 for (int i = 0; i < IM; ++i) {
                     ah[i] = fragh(0, sub, cur, wm * WM + i * 32);
-                    al[i] = fragh(0, NSUB + sub, cur, wm * WM + i * 32);
+                    if constexpr (!F1) al[i] = fragh(0, NSUB + sub, cur, wm * WM + i * 32);
                 }
 #pragma unroll
                 for (int j = 0; j < JN; ++j) {
                     bh[j] = fragh(1, sub, cur, wn * WN + j * 32);
-                    bl[j] = fragh(1, NSUB + sub, cur, wn * WN + j * 32);
+                    if constexpr (!F1) bl[j] = fragh(1, NSUB + sub, cur, wn * WN + j * 32);
                 }
                 if (sub == 0) load(kt + 2, nra, nrb, npro);  // unconditional (see below)
 #pragma unroll
                 for (int i = 0; i < IM; ++i)
 #pragma unroll
                     for (int j = 0; j < JN; ++j) {
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        if constexpr (!F1) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        }
                         t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
                     }
             }
             store(cur ^ 1, ora, orb, opro);
             if constexpr (DCS_WGRAD_SGB > 0) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2 * (IM + JN) * 2 * NSUB, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x100, 2 * (IM + JN) * (F1 ? 1 : 2) * NSUB, 0);  // DS read
 #pragma unroll
-                for (int i = 0; i < IM * JN * 3 * NSUB; ++i) {
+                for (int i = 0; i < IM * JN * (F1 ? 1 : 3) * NSUB; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, DCS_WGRAD_SGB, 0);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x200, 4 * NSUB, 0);  // DS write
+                __builtin_amdgcn_sched_group_barrier(0x200, (F1 ? 2 : 4) * NSUB, 0);  // DS write
             }
             const long long rel = kt - kt_beg;
             if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
@@ -2738,10 +2753,22 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
 }
 }  // namespace
 
+// conv_win.hip: the f16x3 window weight gradient of the residual 3x3 convs
+namespace dcs {
+bool wgrad_win_check(const dcs_conv_desc& d);
+size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
+}  // namespace dcs
+
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
     if (!dp) return 0;
     WgradPlan p = wgrad_plan(*dp);
-    return (size_t)p.nsplit * (dp->parity == 2 ? 4 : 1) * dp->Co * p.Ktot * sizeof(float);
+    size_t n = (size_t)p.nsplit * (dp->parity == 2 ? 4 : 1) * dp->Co * p.Ktot * sizeof(float);
+    if (DCS_WGRAD_WIN && wgrad_win_check(*dp)) {
+        const size_t nw = wgrad_win_workspace_size(*dp);
+        n = nw > n ? nw : n;
+    }
+    return n;
 }
 
 extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const float* x, const float* x2,
@@ -2762,6 +2789,14 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     if (d.parity == 2 && !vec) return fail(DCS_E_INVALID, "conv_wgrad: sub-pixel rows need a vectorisable source");
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
+    if (DCS_WGRAD_WIN && wgrad_win_check(d)) {  // f16x3 residual geometry: the rolling-window kernel
+        const int ns = wgrad_win_launch(d, dy, x, w, s);
+        if (ns < 0) return -ns;
+        const long long total = (long long)d.Co * 9 * d.Cs;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
+                           3, 3, d.Cs, dw);
+        return check_launch("conv_wgrad_reduce");
+    }
     const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity &&
                      d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
     const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
@@ -2791,6 +2826,9 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         if (d.mma == MMA_F16X3) {  // f16x3: two 16-pixel sub-tiles per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        } else if (d.mma == MMA_F16) {  // f16: the same pipeline, one product
+            if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);

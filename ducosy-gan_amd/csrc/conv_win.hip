@@ -108,6 +108,8 @@ __device__ __forceinline__ void win_stats(const floatx16 (&acc)[2][2], int p0, i
     }
 }
 
+// NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only)
+template <int NP>
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
                                                                  const _Float16* __restrict__ wh,
                                                                  const _Float16* __restrict__ wl,
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 f16x8 hi, lo;
                 split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
-                *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
             }
         }
     };
@@ -259,20 +261,22 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 for (int i = 0; i < 2; ++i) {
                     const int wpix = wb[i] + ty * WP + tx;
                     ah[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
-                    al[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
+                    if constexpr (NP == 3) al[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
                 }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int row = wn * 64 + j * 32 + l32;
                     bh[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 0, tx, row, kh));
-                    bl[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 1, tx, row, kh));
+                    if constexpr (NP == 3) bl[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 1, tx, row, kh));
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        if constexpr (NP == 3) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
+                        }
                         t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
                     }
             }
@@ -375,12 +379,317 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight gradient of the residual 3x3 convs on a rolling source window (f16x3):
+//   dW[co][ci][ty][tx] = sum_p dy[p][co] * xpad[p + (ty - 1, tx - 1)][ci]
+// conv.hip's conv_wgrad_x6_kernel owns a 128 (co) x 128 ((tap, ci)) tile and gathers the source at
+// each tap's offset: every source value is fetched, split and staged once per tap column group
+// (nine times).  Here a workgroup owns 64 co x 64 ci x all nine taps and walks one 64-pixel-wide
+// strip of an image row by row: per row it stages the dy row segment (64 px x 64 co) and ONE new
+// source row segment (66 px with the halo x 64 ci) into a ring of four rows, split into hi / lo fp16
+// once; the nine taps read their fragments from the ring at a per-tap (row slot, pixel) offset.
+// MFMA shape: M = co (32), N = ci (32), K = 16 pixels of the row; both operands pixel-major in LDS,
+// fragments by ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).  4 waves, one per
+// SIMD: wave w owns co block (w & 1) x ci block (w >> 1) x 9 taps = nine 32 x 32 accumulators
+// (two-level: a chain of two rows = 128 pixels, then added to the running sum).  Per row and wave:
+// 4 pixel sub-tiles x 9 taps x 3 products = 108 MFMAs between barriers.
+// LDS (halves): ring [4 slots][2 planes][66 px][64 ch], dy [2 buffers][2 planes][64 px][64 ch];
+// 16-byte channel units swizzled by bit 1 of the pixel index (unit ^ 4), so the four consecutive
+// pixels of a transposed read land on the four 64-byte quarters of the banks at any tap offset.
+// Partial sums per (image, strip, row chunk) go to slabs [split][co][tap * C + ci] (the layout of
+// conv.hip's split-K weight gradient), summed by its reduce kernel.
+constexpr int WW_NT = 256, WW_SW = 64, WW_WP = WW_SW + 2;
+constexpr int WW_XROW = 2 * WW_WP * 64;  // halves per ring slot
+constexpr int WW_DROW = 2 * WW_SW * 64;  // halves per dy buffer
+constexpr int WW_XU = (WW_WP * 8 + WW_NT - 1) / WW_NT;  // source-row (pixel, 8-channel unit)s per thread: 3
+
+struct WWArgs {
+    int N, H, W, C, Co;  // source NHWC [N][H][W][C]; dy NHWC [N][H][W][Co]
+    int reflect;         // 1: reflection padding, 0: zero padding
+    int strips, rchunks, rows_per;  // 64-pixel strips per row, row chunks per strip, rows per chunk
+    int gco, gci;        // 64-channel tiles of co / ci
+    int rng_a_n, rng_b_n;
+};
+
+__device__ __forceinline__ int ww_swz(int pix) { return ((pix >> 1) & 1) << 2; }
+
+typedef short wshortx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wshortx4 lds_wshortx4;
+
+__device__ __forceinline__ f16x8 ww_frag(const _Float16* p) {
+    const wshortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wshortx4*)(p));
+    const wshortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wshortx4*)(p + 4 * 64));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int NP>  // as conv3_win_h3_kernel
+__global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const float* __restrict__ dy,
+                                                                 const float* __restrict__ src,
+                                                                 const float* __restrict__ rnga,
+                                                                 const float* __restrict__ rngb,
+                                                                 float* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
+    _Float16* const Xr = smem;                 // [4][2][66][64]
+    _Float16* const Dy = smem + 4 * WW_XROW;   // [2][2][64][64]
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = a.gco * a.gci;
+    const int tile = L % ntile, split = L / ntile;
+    const int co0 = (tile % a.gco) * 64, ci0 = (tile / a.gco) * 64;
+    const int rc = split % a.rchunks, rest = split / a.rchunks;
+    const int strip = rest % a.strips, n = rest / a.strips;
+    const int x0 = strip * WW_SW;
+    const int H = a.H, W = a.W, C = a.C, Co = a.Co;
+    const int y_beg = rc * a.rows_per;
+    const int y_end = y_beg + a.rows_per < H ? y_beg + a.rows_per : H;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int cob = wid & 1, cib = wid >> 1;
+
+    const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
+    const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int OOB = 0x7fffffbf;
+
+    // dy row segment: 64 px x 8 units, two per thread; byte offset within the row
+    int doff[2], dls[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int u = tid + q * WW_NT, pix = u >> 3, cu = u & 7;
+        doff[q] = ((x0 + pix) * Co + co0 + 8 * cu) * 4;
+        dls[q] = pix * 64 + 8 * (cu ^ ww_swz(pix));
+    }
+    // source row segment: 66 px (halo included) x 8 units; byte offset within the row (-1: none)
+    int xoff[WW_XU], xls[WW_XU];
+#pragma unroll
+    for (int q = 0; q < WW_XU; ++q) {
+        const int u = tid + q * WW_NT, wc = u >> 3, cu = u & 7;
+        xoff[q] = -1;
+        xls[q] = -1;
+        if (wc < WW_WP) {
+            int sx = x0 - 1 + wc;
+            bool ok = true;
+            if (a.reflect) sx = sx < 0 ? -sx : (sx >= W ? 2 * W - 2 - sx : sx);
+            else ok = sx >= 0 && sx < W;
+            if (ok) xoff[q] = (sx * C + ci0 + 8 * cu) * 4;
+            xls[q] = wc * 64 + 8 * (cu ^ ww_swz(wc));
+        }
+    }
+    float4 dr[2][2], xr[WW_XU][2];
+    auto ld_dy = [&](int y) {
+        const int rb = ((n * H + y) * W) * Co * 4;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q], 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q] + 16, 0, 0);
+            __builtin_memcpy(&dr[q][0], &v0, 16);
+            __builtin_memcpy(&dr[q][1], &v1, 16);
+        }
+    };
+    auto ld_x = [&](int r) {  // logical source row r in [-1, H]
+        int sy = r;
+        bool ok = true;
+        if (a.reflect) sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
+        else ok = sy >= 0 && sy < H;
+        const int rb = ((n * H + sy) * W) * C * 4;
+#pragma unroll
+        for (int q = 0; q < WW_XU; ++q) {
+            const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
+            __builtin_memcpy(&xr[q][0], &v0, 16);
+            __builtin_memcpy(&xr[q][1], &v1, 16);
+        }
+    };
+    auto st_dy = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            f16x8 hi, lo;
+            split8h(dr[q][0], dr[q][1], asc, hi, lo);
+            *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls[q]) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls[q]) = lo;
+        }
+    };
+    auto st_x = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < WW_XU; ++q) {
+            if (xls[q] >= 0) {
+                f16x8 hi, lo;
+                split8h(xr[q][0], xr[q][1], bsc, hi, lo);
+                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
+            }
+        }
+    };
+
+    // transposed-read lane offsets (halves): lane (r, h) of a fragment gets pixels 8h .. 8h+7 of
+    // channel r of its 32-channel block; in a 16-lane group lane 4q+p reads pixel row q (+4: second
+    // read), channels 4p .. 4p+3
+    const int g16 = lane >> 4;
+    const int rpix = 8 * (g16 >> 1) + ((lane & 15) >> 2);
+    const int rcol = 16 * (g16 & 1) + 4 * (lane & 3);
+    int aoff, boff[3];
+    {
+        const int c = 32 * cob + rcol;
+        aoff = rpix * 64 + 8 * ((c >> 3) ^ ww_swz(rpix)) + (c & 7);
+        const int cb = 32 * cib + rcol;
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+            const int p = rpix + tx;
+            boff[tx] = p * 64 + 8 * ((cb >> 3) ^ ww_swz(p)) + (cb & 7);
+        }
+    }
+
+    floatx16 acc[9], t[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
+
+    // prologue: source rows y_beg-1 .. y_beg+1 into their ring slots, dy row y_beg into buffer 0
+#pragma unroll 1
+    for (int r = y_beg - 1; r <= y_beg + 1; ++r) {
+        ld_x(r);
+        st_x(r & 3);
+    }
+    ld_dy(y_beg);
+    st_dy(y_beg & 1);
+    __syncthreads();
+
+#pragma unroll 1
+    for (int y = y_beg; y < y_end; ++y) {
+        // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
+        ld_dy(y + 1 < y_end ? y + 1 : y);
+        ld_x(y + 2 <= H ? y + 2 : H);
+        const _Float16* const Db = Dy + (y & 1) * WW_DROW;
+        const _Float16* Xs[3];
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + 3 + ty) & 3) * WW_XROW;  // row y - 1 + ty
+        // 36 (pixel sub-tile k, tap) steps; the fragments of step j + 1 are read before the MFMAs of
+        // step j, so their LDS latency hides behind three MFMAs
+        auto rdA = [&](int k, f16x8& h, f16x8& l) {
+            h = ww_frag(Db + aoff + k * 16 * 64);
+            if constexpr (NP == 3) l = ww_frag(Db + WW_SW * 64 + aoff + k * 16 * 64);
+        };
+        auto rdB = [&](int j, f16x8& h, f16x8& l) {
+            const int k = j / 9, tap = j % 9, ty = tap / 3, tx = tap % 3;
+            h = ww_frag(Xs[ty] + boff[tx] + k * 16 * 64);
+            if constexpr (NP == 3) l = ww_frag(Xs[ty] + WW_WP * 64 + boff[tx] + k * 16 * 64);
+        };
+        f16x8 ah, al, bh, bl, nah, nal, nbh, nbl;
+        rdA(0, ah, al);
+        rdB(0, bh, bl);
+#pragma unroll
+        for (int j = 0; j < 36; ++j) {
+            if (j + 1 < 36) {
+                if ((j + 1) % 9 == 0) rdA((j + 1) / 9, nah, nal);
+                rdB(j + 1, nbh, nbl);
+            }
+            floatx16& tt = t[j % 9];
+            if constexpr (NP == 3) {
+                tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tt, 0, 0, 0);
+                tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
+            }
+            tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tt, 0, 0, 0);
+            if (j == 17) {  // stage the rows loaded above into the buffers this row does not read
+                st_dy((y + 1) & 1);
+                st_x((y + 2) & 3);
+            }
+            bh = nbh;
+            bl = nbl;
+            if ((j + 1) % 9 == 0) {
+                ah = nah;
+                al = nal;
+            }
+        }
+        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                acc[i] += t[i];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t[i][r] = 0.f;
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: undo the operand scales, slab [split][co][tap * C + ci]
+    const int eab = -(ea + eb);
+    float* const slab = ws + (long long)split * Co * 9 * C;
+    const int col = ci0 + 32 * cib + (lane & 31);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = co0 + 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            slab[(long long)row * 9 * C + tap * C + col] = __builtin_ldexpf(acc[tap][r], eab);
+        }
+}
+
+struct WWPlan {
+    int strips, rchunks, rows_per, nsplit;
+};
+WWPlan ww_plan(const dcs_conv_desc& d) {
+    WWPlan p;
+    p.strips = d.Ws / WW_SW;
+    const long long base = (long long)d.N * p.strips * (d.Co / 64) * (d.Cs / 64);
+    int rch = (int)cdiv(256, base);  // at least one workgroup per CU
+    const int maxch = d.Hs / 8 > 0 ? d.Hs / 8 : 1;  // >= 8 rows per chunk
+    rch = rch < 1 ? 1 : (rch > maxch ? maxch : rch);
+    p.rows_per = (int)cdiv(d.Hs, rch);
+    p.rchunks = (int)cdiv(d.Hs, p.rows_per);
+    p.nsplit = d.N * p.strips * p.rchunks;
+    return p;
+}
+
+}  // namespace
+
+// d describes the FORWARD conv (source x, output dy)
+bool wgrad_win_check(const dcs_conv_desc& d) {
+    return (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.KH == 3 && d.KW == 3 && d.stride == 1 && d.up == 1 &&
+           d.parity == 0 &&
+           d.pt == 1 && d.pl == 1 && d.Ho == d.Hs && d.Wo == d.Ws && d.Cs % 64 == 0 && d.Co % 64 == 0 &&
+           d.Ws % WW_SW == 0 && d.Hs >= 2 && d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+           d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) &&
+           d.pro_act == DCS_ACT_NONE && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 &&
+           d.rng_b_n > 0 && d.rng_b_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+           (long long)d.N * d.Hs * d.Ws * d.Co * 4 < 0x7fffff00LL - 64;
+}
+
+size_t wgrad_win_workspace_size(const dcs_conv_desc& d) {
+    const WWPlan p = ww_plan(d);
+    return (size_t)p.nsplit * d.Co * 9 * d.Cs * sizeof(float);
+}
+
+// partial slabs into ws (wgrad_win_workspace_size bytes); returns the split count (< 0: error)
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s) {
+    const WWPlan p = ww_plan(d);
+    WWArgs a;
+    a.N = d.N; a.H = d.Hs; a.W = d.Ws; a.C = d.Cs; a.Co = d.Co;
+    a.reflect = d.pad_mode == DCS_PAD_REFLECT;
+    a.strips = p.strips; a.rchunks = p.rchunks; a.rows_per = p.rows_per;
+    a.gco = d.Co / 64; a.gci = d.Cs / 64;
+    a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n;
+    const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
+    if (d.mma == DCS_MMA_F16)
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    else
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    const int e = check_launch("wgrad3_win");
+    return e ? -e : p.nsplit;
+}
+
+namespace {
+
 int win_check(const dcs_conv_desc& d, bool fwd) {
     const bool geom = d.KH == 3 && d.KW == 3 && d.stride == 1 && d.up == 1 && !d.parity && d.Cs % 16 == 0 &&
                       d.Co % WIN_BN == 0 && d.Ws <= 128 && 256 % d.Ws == 0 && d.Hs % (256 / d.Ws) == 0 &&
                       d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
                       d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
-                      d.epi_act == DCS_ACT_NONE && d.mma == DCS_MMA_F16X3 && d.rng_a && d.rng_a_n > 0 &&
+                      d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_a_n > 0 &&
                       d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL;
     if (!geom) return 0;
     if (fwd) return d.Ho == d.Hs && d.Wo == d.Ws && d.pt == 1 && d.pl == 1;
@@ -393,9 +702,14 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
     a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
-    hipLaunchKernelGGL(conv3_win_h3_kernel, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
-                       reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
-                       addend, out, parts);
+    if (d.mma == DCS_MMA_F16)
+        hipLaunchKernelGGL(conv3_win_h3_kernel<1>, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
+                           reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
+                           addend, out, parts);
+    else
+        hipLaunchKernelGGL(conv3_win_h3_kernel<3>, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
+                           reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
+                           addend, out, parts);
     return check_launch("conv3_win");
 }
 

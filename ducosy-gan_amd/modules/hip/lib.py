@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("DUCOSY_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libdu
 
 DCS_PAD_ZERO, DCS_PAD_REFLECT = 0, 1
 ACT_NONE, ACT_AFFINE, ACT_RELU, ACT_LRELU, ACT_TANH = 0, 1, 2, 3, 4
-MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6, MMA_F16X3 = 0, 1, 3, 6, 7
+MMA_F32, MMA_BF16, MMA_BF16X3, MMA_BF16X6, MMA_F16X3, MMA_F16 = 0, 1, 3, 6, 7, 8
 RANGE_PARTS = 512  # DCS_RANGE_PARTS: partial maxima of an f16x3 operand's range record
 KORDER_TAP, KORDER_SLICE, PACK_KSLICE = 0, 1, 8
 

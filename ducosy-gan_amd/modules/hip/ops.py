@@ -20,10 +20,11 @@ from .lib import ACT_AFFINE, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_TANH, DCS_PAD_RE
 IN_EPS = 1e-5
 
 # MFMA operand mode of the MFMA convolution passes (include/ducosy_hip.h DCS_MMA_*): "f32" is
-# exact fp32 (the reference's precision, default); "bf16" rounds the GEMM operands to bf16
+# exact fp32 (the reference's precision); "f16x3" / "bf16x6" split each fp32 operand into fp16 / bf16
+# parts (fp32-class); "f16" rounds the power-of-two scaled operands to fp16 and "bf16" to bf16
 # (BASELINE config 5's half-precision path); "bf16x3" splits each operand into hi + lo bf16.
 _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3, "bf16x6": lib.MMA_BF16X6,
-              "f16x3": lib.MMA_F16X3}
+              "f16x3": lib.MMA_F16X3, "f16": lib.MMA_F16}
 # default f16x3: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
 # tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32, also for bf16x6) at half of bf16x6's MFMAs
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
@@ -38,6 +39,17 @@ _KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
 _FUSE_FOLD = os.environ.get("DUCOSY_FUSE_FOLD", "1") == "1"
 # f16x3 residual convs on the window kernel (csrc/conv_win.hip); "0" = the rows pass (A/B)
 _WIN = os.environ.get("DUCOSY_WIN", "1") == "1"
+
+
+def _h3() -> bool:
+    """f16x3 or f16: the power-of-two scaled fp16 operand modes (range records, window kernels)."""
+    return _MMA in (lib.MMA_F16X3, lib.MMA_F16)
+
+
+def _fallback() -> int:
+    """Mode of a pass the fp16 kernels do not cover (no range record: concat or strided sources):
+    bf16x6 under f16x3 (fp32-class), plain bf16 under f16 (half precision)."""
+    return lib.MMA_BF16 if _MMA == lib.MMA_F16 else lib.MMA_BF16X6
 
 
 def set_mma(mode: str) -> None:
@@ -118,7 +130,7 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
 def _out_rng(out: torch.Tensor):
     """Range record for a producer kernel to fill while it writes ``out`` (f16x3 mode only): the
     kernel zeroes it and folds max |value| in; attached to ``out`` like range_rec's cache."""
-    if _MMA != lib.MMA_F16X3:
+    if not _h3():
         return None
     rng = torch.empty(lib.RANGE_PARTS, device=out.device, dtype=torch.float32)
     out._dcs_rng = (out._version, None, ACT_NONE, rng)
@@ -136,10 +148,10 @@ def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[
     gathered tensor, contiguous, with its prologue) and ``b_rng`` (the packed weights' record, or the
     wgrad source's); a pass without them (concat or strided sources) runs bf16x6."""
     d.mma = _MMA
-    if _MMA != lib.MMA_F16X3:
+    if not _h3():
         return
     if a is None or b_rng is None or not a.is_contiguous() or (a.numel() // a.shape[0]) % 4 or a.data_ptr() % 16:
-        d.mma = lib.MMA_BF16X6
+        d.mma = _fallback()
         return
     ra = range_rec(a, a_pro)
     d.rng_a, d.rng_a_n = ra.data_ptr(), ra.numel()
@@ -280,7 +292,7 @@ class ConvGeom:
     def win(self) -> bool:
         """f16x3 window kernel for this geometry (3x3 stride-1 pad-1, csrc/conv_win.hip): the packs
         also carry the pre-split fp16 planes (``_dcs_h3``); used where the call's image fits."""
-        return (_WIN and _MMA == lib.MMA_F16X3 and self.k == 3 and self.stride == 1 and self.up == 1
+        return (_WIN and _h3() and self.k == 3 and self.stride == 1 and self.up == 1
                 and self.pads == (1, 1, 1, 1) and self.cin % 16 == 0 and self.cout % 128 == 0)
 
     def _attach_h3(self, wpack: torch.Tensor, w: torch.Tensor, flip: int) -> torch.Tensor:
@@ -345,7 +357,7 @@ class ConvGeom:
         else:
             Kpad, cols, nmajor = _round_up(K, 32), _round_up(ncols, _bn_for(ncols)), 1
             out = torch.empty(cols, Kpad, device=w.device, dtype=torch.float32)
-        if nmajor and _MMA == lib.MMA_F16X3:  # f16x3 rows pass: the pack also writes the range record
+        if nmajor and _h3():  # f16x3 rows pass: the pack also writes the range record
             rng = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
             lib.call("dcs_pack_weights_r", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
                      cols, nmajor, _p(out), _p(rng), _stream())
@@ -375,7 +387,7 @@ class ConvGeom:
             d.up, d.parity = 1, 2  # phases over the source grid (the upsample is in the weights)
         d.Ho, d.Wo, d.Co = Ho, Wo, self.cout
         d.ldb, d.pro_act, d.epi_act = ldb, pro_act, epi_act
-        d.mma = _MMA if _MMA != lib.MMA_F16X3 else lib.MMA_BF16X6  # f16x3: _set_mma with the ranges
+        d.mma = _MMA if not _h3() else _fallback()  # f16x3 / f16: _set_mma with the ranges
         d.korder = lib.KORDER_SLICE if (rows and self.kslice and not self.narrow) else lib.KORDER_TAP
         return d
 
@@ -496,7 +508,7 @@ class ConvGeom:
         d.up, d.pad_mode = 1, DCS_PAD_ZERO
         d.KH = d.KW = self.k
         d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
-        d.mma = lib.MMA_BF16X6 if _MMA == lib.MMA_F16X3 else _MMA
+        d.mma = _fallback() if _h3() else _MMA
         if not narrow:
             _set_mma(d, dy, None, _wrng(wpack_d))
         d.korder = lib.KORDER_SLICE if (self.kslice and ci > 4) else lib.KORDER_TAP
@@ -583,7 +595,7 @@ class ConvGeom:
         _check_dev(dy, s.t, s.t2)
         pro_act = pro[2] if pro is not None else ACT_NONE
         d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
-        if not self.narrow and s.t2 is None and _MMA == lib.MMA_F16X3 and s.t.is_contiguous():
+        if not self.narrow and s.t2 is None and _h3() and s.t.is_contiguous():
             _set_mma(d, dy, None, range_rec(s.t, pro))
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
             d.cw = self.cin

@@ -109,6 +109,11 @@ typedef struct dcs_conv_desc {
  * (tests/test_gpu_mma.py): fp32-class at half the MFMAs of BF16X6.  Shapes without an F16X3
  * variant run BF16X6. */
 #define DCS_MMA_F16X3 7
+/* F16: BASELINE config 5's fp16 MFMA path.  Each fp32 operand, scaled by the same power of two as
+ * F16X3 (from rng_a / rng_b), is rounded to fp16 (11 significant bits, no overflow or underflow
+ * from the scale); one product per fragment pair on v_mfma_f32_32x32x16_f16, fp32 accumulation and
+ * storage, the result scaled back exactly.  Shapes without an F16 variant run BF16X6. */
+#define DCS_MMA_F16 8
 /* partial maxima the F16X3 kernels reduce (dcs_range_parts writes this many).  The producers of
  * conv operands (dcs_in_apply, dcs_in_act_backward, dcs_cbam_forward, dcs_cbam_backward,
  * dcs_act_backward, dcs_pack_nhwc4) take an optional `rng` (DCS_RANGE_PARTS floats, or NULL):

@@ -5,6 +5,7 @@ geometry with a vectorised gather.  Tolerances (max |err| / max |ref|), written 
   bf16x6 hi/mid/lo bf16 split, six products               <= 1e-5   (~2^-24 per product)
   f16x3  power-of-two scaled hi/lo fp16 split, 3 products <= 1e-5   (~2^-22 per operand)
   bf16x3 hi/lo bf16 split, three products                 <= 5e-5   (~2^-16 per product)
+  f16    power-of-two scaled fp16 operands, one product   <= 3e-3   (~2^-11 per operand)
   bf16   bf16 operands, f32 accumulation (config 5)       <= 2e-2   (~2^-9 per operand)
 """
 import pytest
@@ -15,7 +16,7 @@ from test_gpu_ops import CONV_CASES, _geom, rnd, torch_conv
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOL = {"f32": 1e-5, "bf16x6": 1e-5, "f16x3": 1e-5, "bf16x3": 5e-5, "bf16": 2e-2}
+TOL = {"f32": 1e-5, "bf16x6": 1e-5, "f16x3": 1e-5, "bf16x3": 5e-5, "f16": 3e-3, "bf16": 2e-2}
 CASES = [c for c in CONV_CASES if c[0] % 16 == 0 and c[1] % 16 == 0]
 
 
@@ -31,7 +32,7 @@ def ops():
     o.set_mma(prev)
 
 
-@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "bf16x6", "f16x3", "f32"])
+@pytest.mark.parametrize("mode", ["bf16", "bf16x3", "bf16x6", "f16x3", "f16", "f32"])
 @pytest.mark.parametrize("case", CASES, ids=[f"c{c[0]}-{c[1]}k{c[2]}s{c[3]}u{c[6]}H{c[7]}" for c in CASES])
 def test_conv_modes_vs_fp64(ops, mode, case):
     g, H = _geom(case)

@@ -118,3 +118,54 @@ def test_win_ok_rejects_other_geometries(ops):
     d = g._desc_fwd(ops.Src.nhwc(x), 2304, 0, 0)
     ops._set_mma(d, x, None, torch.zeros(512, device=DEV))
     assert lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0) == 0
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 16, 64), (1, 20, 64), (1, 8, 128), (1, 32, 128)])
+def test_win_wgrad_vs_fp64(ops, N, H, W):
+    """The rolling-window weight gradient (csrc/conv_win.hip wgrad3_win_h3_kernel: 64-pixel strips,
+    row chunks of 8..H rows, reflection halo) against float64: max error / max |ref| <= 1e-5, and
+    within 1.5x of the exact-f32 MFMA path's error (fp32-class), bit-identical on a second run."""
+    from modules.hip import lib
+    g = _geom(ops)
+    x = rnd((N, 256, H, W), 81, "x").double()
+    w = torch.from_numpy(prng.normal(82, "w", (256, 256, 3, 3), 0, 0.05)).float().double().requires_grad_(True)
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    R = torch.from_numpy(prng.normal(83, "R", tuple(y.shape))).float().double()
+    (y * R).sum().backward()
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    ops.set_mma("f16x3")
+    d = g._desc_fwd(ops.Src.nhwc(xd), 0, 0, 0)
+    ops._set_mma(d, Rd, None, ops.range_rec(xd))
+    assert lib.query("dcs_conv_wgrad_workspace_size", ctypes.byref(d)) >= N * (W // 64) * 256 * 2304 * 4
+    dw = g.wgrad(Rd, ops.Src.nhwc(xd))
+    e_win = _relmax(dw, w.grad)
+    assert e_win <= 1e-5, e_win
+    assert torch.equal(dw, g.wgrad(Rd, ops.Src.nhwc(xd)))
+    ops.set_mma("f32")
+    e_f32 = _relmax(g.wgrad(Rd, ops.Src.nhwc(xd)), w.grad)
+    assert e_win <= 1.5 * e_f32 + 1e-7, (e_win, e_f32)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 16, 64), (1, 16, 128)])
+def test_win_f16_mode_vs_fp64(ops, N, H, W):
+    """BASELINE config 5's fp16 MFMA path (DCS_MMA_F16: the window kernels with the hi planes only,
+    one product): forward, data gradient and weight gradient within 3e-3 of float64 (fp16 operands:
+    2^-11 per operand), and the f16x3 result within 1e-5 on the same operands."""
+    g = _geom(ops)
+    x = rnd((N, 256, H, W), 91, "x").double().requires_grad_(True)
+    w = torch.from_numpy(prng.normal(92, "w", (256, 256, 3, 3), 0, 0.05)).float().double().requires_grad_(True)
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    R = torch.from_numpy(prng.normal(93, "R", tuple(y.shape))).float().double()
+    (y * R).sum().backward()
+    xd = x.detach().float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    for mode, tol in (("f16", 3e-3), ("f16x3", 1e-5)):
+        ops.set_mma(mode)
+        wd = w.detach().float().to(DEV)
+        yy, _ = g.forward_in_stats(ops.Src.nhwc(xd), g.pack_fwd(wd))
+        dx = g.dgrad(Rd, g.pack_dgrad(wd), H, W)
+        dw = g.wgrad(Rd, ops.Src.nhwc(xd))
+        errs = (_relmax(yy.permute(0, 3, 1, 2), y.detach()), _relmax(dx.permute(0, 3, 1, 2), x.grad),
+                _relmax(dw, w.grad))
+        assert max(errs) <= tol, (mode, errs)
