@@ -120,8 +120,8 @@ constexpr int NT = 256;
 #define DCS_WGRAD_X6 1  // bf16x6 weight-gradient kernel in the bf16x6 mode
 #endif
 #ifndef DCS_WGRAD_X6_CO64
-#define DCS_WGRAD_X6_CO64 0  // ... also for 64 output channels (128-row tile, half masked): measured
-                             // 3.49 ms vs 2.58 ms f32 on up2 at bs 16, off
+#define DCS_WGRAD_X6_CO64 1  // ... also for 64 output channels in the fp16 modes (128-row tile, half masked): f16x3 up2 at bs 16
+                             // 2.15 ms vs 2.48 ms f32 (bf16x6 was 3.49 ms: off there), profiles/r03d
 #endif
 #ifndef DCS_X6_BN64
 #define DCS_X6_BN64 1  // bf16x6 rows also for 64-column tiles
@@ -2819,7 +2819,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (d.mma != MMA_F32 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64)) &&
+    } else if (d.mma != MMA_F32 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64 && (d.mma == MMA_F16X3 || d.mma == MMA_F16))) &&
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)

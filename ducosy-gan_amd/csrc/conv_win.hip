@@ -17,6 +17,7 @@
 // 8 waves = 4 (pixels) x 2 (channels) of 64 x 64; one workgroup per CU (115 KB of LDS).
 #include "common.hpp"
 #include "conv_common.hpp"
+#include <type_traits>
 
 namespace dcs {
 namespace {
@@ -389,19 +390,22 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
 // source row segment (66 px with the halo x 64 ci) into a ring of four rows, split into hi / lo fp16
 // once; the nine taps read their fragments from the ring at a per-tap (row slot, pixel) offset.
 // MFMA shape: M = co (32), N = ci (32), K = 16 pixels of the row; both operands pixel-major in LDS,
-// fragments by ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).  4 waves, one per
-// SIMD: wave w owns co block (w & 1) x ci block (w >> 1) x 9 taps = nine 32 x 32 accumulators
-// (two-level: a chain of two rows = 128 pixels, then added to the running sum).  Per row and wave:
-// 4 pixel sub-tiles x 9 taps x 3 products = 108 MFMAs between barriers.
+// fragments by ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).  8 waves, two per
+// SIMD: waves w and w + 4 (same SIMD) own co block (w & 1) x ci block ((w >> 1) & 1), wave w taps
+// 0..4 and wave w + 4 taps 5..8, so each SIMD carries all nine taps of one 32 x 32 (co, ci) block and
+// each wave at most five accumulators (two-level: a chain of two rows = 128 pixels, then added to
+// the running sum), leaving registers for fragment reads ahead and a second wave to cover LDS
+// latency.  Per row and SIMD: 4 pixel sub-tiles x 9 taps x 3 products = 108 MFMAs between barriers.
 // LDS (halves): ring [4 slots][2 planes][66 px][64 ch], dy [2 buffers][2 planes][64 px][64 ch];
 // 16-byte channel units swizzled by bit 1 of the pixel index (unit ^ 4), so the four consecutive
 // pixels of a transposed read land on the four 64-byte quarters of the banks at any tap offset.
 // Partial sums per (image, strip, row chunk) go to slabs [split][co][tap * C + ci] (the layout of
 // conv.hip's split-K weight gradient), summed by its reduce kernel.
-constexpr int WW_NT = 256, WW_SW = 64, WW_WP = WW_SW + 2;
+constexpr int WW_NT = 512, WW_SW = 64, WW_WP = WW_SW + 2;
 constexpr int WW_XROW = 2 * WW_WP * 64;  // halves per ring slot
 constexpr int WW_DROW = 2 * WW_SW * 64;  // halves per dy buffer
-constexpr int WW_XU = (WW_WP * 8 + WW_NT - 1) / WW_NT;  // source-row (pixel, 8-channel unit)s per thread: 3
+constexpr int WW_XU = (WW_WP * 8 + WW_NT - 1) / WW_NT;  // source-row (pixel, 8-channel unit)s per thread: 2
+constexpr int WW_TPW = 5;                                // taps per wave (5 + 4)
 
 struct WWArgs {
     int N, H, W, C, Co;  // source NHWC [N][H][W][C]; dy NHWC [N][H][W][Co]
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     const int y_end = y_beg + a.rows_per < H ? y_beg + a.rows_per : H;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int cob = wid & 1, cib = wid >> 1;
+    const int cob = wid & 1, cib = (wid >> 1) & 1, half = wid >> 2;
 
     const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
     const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
@@ -454,13 +458,12 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     constexpr int OOB = 0x7fffffbf;
 
-    // dy row segment: 64 px x 8 units, two per thread; byte offset within the row
-    int doff[2], dls[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int u = tid + q * WW_NT, pix = u >> 3, cu = u & 7;
-        doff[q] = ((x0 + pix) * Co + co0 + 8 * cu) * 4;
-        dls[q] = pix * 64 + 8 * (cu ^ ww_swz(pix));
+    // dy row segment: 64 px x 8 units, one per thread; byte offset within the row
+    int doff, dls;
+    {
+        const int pix = tid >> 3, cu = tid & 7;
+        doff = ((x0 + pix) * Co + co0 + 8 * cu) * 4;
+        dls = pix * 64 + 8 * (cu ^ ww_swz(pix));
     }
     // source row segment: 66 px (halo included) x 8 units; byte offset within the row (-1: none)
     int xoff[WW_XU], xls[WW_XU];
@@ -478,16 +481,13 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             xls[q] = wc * 64 + 8 * (cu ^ ww_swz(wc));
         }
     }
-    float4 dr[2][2], xr[WW_XU][2];
+    float4 dr[2], xr[WW_XU][2];
     auto ld_dy = [&](int y) {
         const int rb = ((n * H + y) * W) * Co * 4;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q], 0, 0);
-            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q] + 16, 0, 0);
-            __builtin_memcpy(&dr[q][0], &v0, 16);
-            __builtin_memcpy(&dr[q][1], &v1, 16);
-        }
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff + 16, 0, 0);
+        __builtin_memcpy(&dr[0], &v0, 16);
+        __builtin_memcpy(&dr[1], &v1, 16);
     };
     auto ld_x = [&](int r) {  // logical source row r in [-1, H]
         int sy = r;
@@ -505,13 +505,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         }
     };
     auto st_dy = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            f16x8 hi, lo;
-            split8h(dr[q][0], dr[q][1], asc, hi, lo);
-            *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls[q]) = hi;
-            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls[q]) = lo;
-        }
+        f16x8 hi, lo;
+        split8h(dr[0], dr[1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls) = lo;
     };
     auto st_x = [&](int slot) {
 #pragma unroll
@@ -543,9 +540,9 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         }
     }
 
-    floatx16 acc[9], t[9];
+    floatx16 acc[WW_TPW], t[WW_TPW];
 #pragma unroll
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < WW_TPW; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
 
@@ -559,23 +556,22 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     st_dy(y_beg & 1);
     __syncthreads();
 
-#pragma unroll 1
-    for (int y = y_beg; y < y_end; ++y) {
-        // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
-        ld_dy(y + 1 < y_end ? y + 1 : y);
-        ld_x(y + 2 <= H ? y + 2 : H);
+    // one row of this wave's taps T0 .. T0 + NT_ - 1: 4 pixel sub-tiles x NT_ taps, the fragments of
+    // the next (sub-tile, tap) read before the MFMAs of the current one
+    auto row = [&](int y, auto tag) {
+        constexpr int T0 = decltype(tag)::value * WW_TPW;
+        constexpr int NT_ = 9 - T0 < WW_TPW ? 9 - T0 : WW_TPW;
+        constexpr int NJ = 4 * NT_;
         const _Float16* const Db = Dy + (y & 1) * WW_DROW;
         const _Float16* Xs[3];
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + 3 + ty) & 3) * WW_XROW;  // row y - 1 + ty
-        // 36 (pixel sub-tile k, tap) steps; the fragments of step j + 1 are read before the MFMAs of
-        // step j, so their LDS latency hides behind three MFMAs
         auto rdA = [&](int k, f16x8& h, f16x8& l) {
             h = ww_frag(Db + aoff + k * 16 * 64);
             if constexpr (NP == 3) l = ww_frag(Db + WW_SW * 64 + aoff + k * 16 * 64);
         };
         auto rdB = [&](int j, f16x8& h, f16x8& l) {
-            const int k = j / 9, tap = j % 9, ty = tap / 3, tx = tap % 3;
+            const int k = j / NT_, tap = T0 + j % NT_, ty = tap / 3, tx = tap % 3;
             h = ww_frag(Xs[ty] + boff[tx] + k * 16 * 64);
             if constexpr (NP == 3) l = ww_frag(Xs[ty] + WW_WP * 64 + boff[tx] + k * 16 * 64);
         };
@@ -583,31 +579,40 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         rdA(0, ah, al);
         rdB(0, bh, bl);
 #pragma unroll
-        for (int j = 0; j < 36; ++j) {
-            if (j + 1 < 36) {
-                if ((j + 1) % 9 == 0) rdA((j + 1) / 9, nah, nal);
+        for (int j = 0; j < NJ; ++j) {
+            if (j + 1 < NJ) {
+                if ((j + 1) % NT_ == 0) rdA((j + 1) / NT_, nah, nal);
                 rdB(j + 1, nbh, nbl);
             }
-            floatx16& tt = t[j % 9];
+            floatx16& tt = t[j % NT_];
             if constexpr (NP == 3) {
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tt, 0, 0, 0);
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
             }
             tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tt, 0, 0, 0);
-            if (j == 17) {  // stage the rows loaded above into the buffers this row does not read
+            if (j == NJ / 2 - 1) {  // stage the rows loaded above into the buffers this row does not read
                 st_dy((y + 1) & 1);
                 st_x((y + 2) & 3);
             }
             bh = nbh;
             bl = nbl;
-            if ((j + 1) % 9 == 0) {
+            if ((j + 1) % NT_ == 0) {
                 ah = nah;
                 al = nal;
             }
         }
+    };
+
+#pragma unroll 1
+    for (int y = y_beg; y < y_end; ++y) {
+        // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
+        ld_dy(y + 1 < y_end ? y + 1 : y);
+        ld_x(y + 2 <= H ? y + 2 : H);
+        if (half == 0) row(y, std::integral_constant<int, 0>{});
+        else row(y, std::integral_constant<int, 1>{});
         if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) {
+            for (int i = 0; i < WW_TPW; ++i) {
                 acc[i] += t[i];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) t[i][r] = 0.f;
@@ -621,12 +626,16 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     float* const slab = ws + (long long)split * Co * 9 * C;
     const int col = ci0 + 32 * cib + (lane & 31);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int i = 0; i < WW_TPW; ++i) {
+        const int tap = half * WW_TPW + i;
+        if (tap < 9) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = co0 + 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            slab[(long long)row * 9 * C + tap * C + col] = __builtin_ldexpf(acc[tap][r], eab);
+            for (int r = 0; r < 16; ++r) {
+                const int row = co0 + 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                slab[(long long)row * 9 * C + tap * C + col] = __builtin_ldexpf(acc[i][r], eab);
+            }
         }
+    }
 }
 
 struct WWPlan {
