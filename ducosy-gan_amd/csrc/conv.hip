@@ -171,6 +171,9 @@ constexpr int NT = 256;
 #ifndef DCS_H3_NSUB
 #define DCS_H3_NSUB 2  // f16x3 rows, 128-column tiles: 16-k sub-tiles per barrier (64-column tiles: 1)
 #endif
+#ifndef DCS_H3_BM256_TAG0
+#define DCS_H3_BM256_TAG0 0  // fp16 modes: 256 x 128 tiles for the non-residual 128-column rows passes
+#endif
 #ifndef DCS_X6_BM256
 #define DCS_X6_BM256 1  // bf16x6 residual rows: 256 x 128 tiles (512 threads)
 #endif
@@ -2216,6 +2219,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
     const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3 || d.mma == MMA_F16;  // split-at-store pipelines
+    const ClassGeom g0 = class_geom(d, 0);
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16X3>), G, dim3(2 * BM_), 0, s, d, src, src2, \
@@ -2237,6 +2241,15 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
             DCS_ROWS_X6F(256, 128, 1, 1, grid2)
             if (bm_used) *bm_used = 256;
         } else if (BN == 128 && res) { DCS_ROWS_X6F(128, 128, 1, 1, grid) }
+        else if (BN == 128 && DCS_H3_BM256_TAG0 && d.mma != MMA_BF16X6 && fold == 0 && Mmax % 256 == 0 &&
+                 (!parts || ((long long)g0.My * g0.Mx) % 256 == 0)) {
+            // fp16 modes: 256-row tiles for the other 128-column layers (half the weight-tile
+            // traffic per output; these passes stream their fp32 operands from L2)
+            gxx = (int)cdiv(Mmax, 256);
+            const dim3 grid2((unsigned)(gxx * gy * ncls));
+            DCS_ROWS_X6F(256, 128, 1, 0, grid2)
+            if (bm_used) *bm_used = 256;
+        }
         else if (BN == 128) { DCS_ROWS_X6F(128, 128, 1, 0, grid) }
         else { DCS_ROWS_X6F(128, 64, 1, 0, grid) }
         return check_launch("conv_rows");

@@ -19,6 +19,10 @@
 #include "conv_common.hpp"
 #include <type_traits>
 
+#ifndef DCS_WIN_SPREAD
+#define DCS_WIN_SPREAD 0  // 1: window staging spread over the slice's k-tiles (no VGPR spills, but 3-5 % slower: profiles/r03g)
+#endif
+
 namespace dcs {
 namespace {
 
@@ -163,7 +167,31 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         }
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
-    float4 wr_[WIN_UNITS][2];
+#if DCS_WIN_SPREAD
+    // the next slice's window is staged one unit per k-tile (unit q in k-tile ty = q): 8 VGPRs in
+    // flight instead of 24 held across the slice
+    float4 wq[2];
+    auto win_load_q = [&](int s, int q) {
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+        __builtin_memcpy(&wq[0], &v0, 16);
+        __builtin_memcpy(&wq[1], &v1, 16);
+    };
+    auto win_store_q = [&](int buf, int q) {
+        const int u = tid + q * WIN_NT;
+        const int wpix = u >> 1, h = u & 1;
+        if (wpix < npix) {
+            f16x8 hi, lo;
+            split8h(wq[0], wq[1], asc, hi, lo);
+            *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
+        }
+    };
+    static_assert(WIN_UNITS == 3, "one window unit per k-tile of a slice");
+#endif
+    float4 wr_[DCS_WIN_SPREAD ? 1 : WIN_UNITS][2];
     auto win_load = [&](int s) {
 #pragma unroll
         for (int q = 0; q < WIN_UNITS; ++q) {
@@ -238,9 +266,17 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
     // prologue: window of slice 0, B tile 0; B tile 1 in flight
+#if DCS_WIN_SPREAD
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        win_load_q(0, q);
+        win_store_q(0, q);
+    }
+#else
     win_load(0);
-    b_load(0);
     win_store(0);
+#endif
+    b_load(0);
     b_store(0);
     __syncthreads();
     b_load(1);
@@ -251,10 +287,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int last = 3 * nslice - 1;
     for (int s = 0; s < nslice; ++s) {
         const int wbuf = s & 1;
-        win_load(s + 1 < nslice ? s + 1 : s);
+        if (!DCS_WIN_SPREAD) win_load(s + 1 < nslice ? s + 1 : s);
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) {
             const int tt = 3 * s + ty, bbuf = tt & 1;
+#if DCS_WIN_SPREAD
+            win_load_q(s + 1 < nslice ? s + 1 : s, ty);
+#endif
 #pragma unroll
             for (int tx = 0; tx < 3; ++tx) {
                 f16x8 ah[2], al[2], bh[2], bl[2];
@@ -285,7 +324,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             // a repeat into a buffer nobody reads again)
             b_store(bbuf ^ 1);
             b_load(tt + 2 < last ? tt + 2 : last);
+#if DCS_WIN_SPREAD
+            win_store_q(wbuf ^ 1, ty);
+#else
             if (ty == 2) win_store(wbuf ^ 1);
+#endif
             __syncthreads();
         }
         // close the slice's accumulation chain (144 k)
