@@ -698,8 +698,12 @@ template <int BM, int BN, int VEC, int TAG, int MMA = MMA_F32>
 __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || MMA == MMA_F16) ? (BM == 256 ? 2 : DCS_X6_OCC) : 2) void conv_rows_kernel(
     const dcs_conv_desc din, const float* __restrict__ src, const float* __restrict__ src2,
     const float* __restrict__ wp, const float* __restrict__ bias, const float* __restrict__ psc,
-    const float* __restrict__ psh, float* __restrict__ out, int gx, int gy, Part* __restrict__ parts, int fold) {
+    const float* __restrict__ psh, float* __restrict__ out_, int gx, int gy, Part* __restrict__ parts, int fold_) {
     const dcs_conv_desc d = specialise<TAG>(din);
+    // fold_ = mode (bits 0-1: 0 none, 1 interior + ring, 2 ring rows only) | K splits << 2 (ring rows:
+    // the grid's z index is the split, each split writes its own copy of the ring, summed by the fold)
+    const int fold = fold_ & 3;
+    const int ksplit = (fold_ >> 2) > 1 ? (fold_ >> 2) : 1;
     static_assert(BM == 128 || (BM == 256 && (MMA == MMA_BF16X6 || MMA == MMA_BF16P || MMA == MMA_F16X3 || MMA == MMA_F16) && BN == 128 && VEC == 1),
                   "A loader: 2 threads per row; 256-row tiles only for the x6 128-column kernel");
     constexpr int NTH = 2 * BM;                    // threads (two per A row)
@@ -755,9 +759,11 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     const int ntile = L % gy;
     const int rest = L / gy;
     const int mtile = rest % gx;
-    const int z = rest / gx;
+    const int z = ksplit > 1 ? 0 : rest / gx;
+    const int ks = ksplit > 1 ? rest / gx : 0;
     const ClassGeom g = class_geom(d, z);
     const long long M = fold == 2 ? (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2)) : (long long)g.My * g.Mx * d.N;
+    float* __restrict__ const out = out_ + (long long)ks * M * d.Co;
     const long long m0 = (long long)mtile * BM;
     if (m0 >= M) return;
     const int n0 = ntile * BN;
@@ -776,7 +782,11 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
     const int K = g.ntaps * d.Cs;
-    const int nkt = (K + BKT - 1) / BKT;
+    const int nkt_all = (K + BKT - 1) / BKT;
+    const int kper = (nkt_all + ksplit - 1) / ksplit;
+    const int kt_beg = ks * kper;                                         // this split's k-tiles
+    const int nkt = kt_beg + kper < nkt_all ? kt_beg + kper : nkt_all;  // (exclusive end)
+    const int kb0 = kt_beg * BKT;
     const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
     const float* srow = src + ri.n * d.s_n;
     const long long so = (long long)ri.n * d.Cs;
@@ -820,21 +830,21 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     constexpr bool KS = TAG == 1 || KSB;
     int aj, ac;
     if constexpr (KS) {
-        const int p0 = akq >> 4;
+        const int p0 = (kb0 + akq) >> 4;
         aj = p0 % g.ntaps;
         ac = (p0 / g.ntaps) * 16 + (akq & 15);
     } else {
-        aj = akq / d.Cs;
-        ac = akq - (akq / d.Cs) * d.Cs;
+        aj = (kb0 + akq) / d.Cs;
+        ac = (kb0 + akq) - ((kb0 + akq) / d.Cs) * d.Cs;
     }
     int bj, bc;
     if constexpr (KSB) {
-        const int p0 = bkq >> 4;
+        const int p0 = (kb0 + bkq) >> 4;
         bj = p0 % g.ntaps;
         bc = (p0 / g.ntaps) * 16 + (bkq & 15);
     } else {
-        bj = bkq / d.Cs;
-        bc = bkq - (bkq / d.Cs) * d.Cs;
+        bj = (kb0 + bkq) / d.Cs;
+        bc = (kb0 + bkq) - ((kb0 + bkq) / d.Cs) * d.Cs;
     }
     auto advance = [&](int& j, int& c) {
         if constexpr (KS) {
@@ -1162,8 +1172,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
     int pa0[NSUB], pa1[NSUB];
-    load_a(0, ra, pa0);
-    load_b(0, rb);
+    load_a(kt_beg, ra, pa0);
+    load_b(kt_beg, rb);
     store_tiles(0, ra, rb, pa0);
     __syncthreads();
 
@@ -1288,9 +1298,9 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             // assume it may be missing and wait for every load at the next LDS store.
             float4 ra2[ACH], rb2[BCH];
             int pa2[NSUB];
-            load_a(1, ra, pa1);
-            load_b(1, rb);
-            for (int kt = 0; kt < nkt; kt += 2) {
+            load_a(kt_beg + 1, ra, pa1);
+            load_b(kt_beg + 1, rb);
+            for (int kt = kt_beg; kt < nkt; kt += 2) {
                 load_a(kt + 2, ra2, pa2);
                 load_b(kt + 2, rb2);
                 step(0, 0);
@@ -1322,8 +1332,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
                 __syncthreads();
             }
         } else {
-            for (int kt = 0; kt < nkt; ++kt) {
-                const int cur = kt & 1;
+            for (int kt = kt_beg; kt < nkt; ++kt) {
+                const int cur = (kt - kt_beg) & 1;
 #pragma unroll
                 for (int st = 0; st < NST / 2; ++st) step(cur, st);
                 if (kt + 1 < nkt) { load_a(kt + 1, ra, pa1); load_b(kt + 1, rb); }
@@ -1335,8 +1345,8 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             }
         }
     } else
-    for (int kt = 0; kt < nkt; ++kt) {
-        const int cur = kt & 1;
+    for (int kt = kt_beg; kt < nkt; ++kt) {
+        const int cur = (kt - kt_beg) & 1;
         float4 af[IM][4], bf[JN][4];
 #pragma unroll
         for (int i = 0; i < IM; ++i)
@@ -2027,7 +2037,7 @@ __global__ void reflect_fold_scalar_kernel(const float* __restrict__ dxp, const 
 // (image, target pixel, 4 channels); targets: the two rows over every column, then the two
 // columns over the remaining rows.
 __global__ void reflect_ring_fold_kernel(const float* __restrict__ ring, float* __restrict__ dx, int N, int H, int W,
-                                         int C4) {
+                                         int C4, int nsplit) {
     const int ntgt = 2 * W + 2 * (H - 2);
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long long)N * ntgt * C4) return;
@@ -2054,8 +2064,10 @@ __global__ void reflect_ring_fold_kernel(const float* __restrict__ ring, float* 
             const int yp = ay[p], xp = ax[q];
             if (yp >= 1 && yp <= H && xp >= 1 && xp <= W) continue;  // interior: in the epilogue
             const int ri = yp == 0 ? xp : (yp == Hp - 1 ? Wp + xp : 2 * Wp + 2 * (yp - 1) + (xp == 0 ? 0 : 1));
-            const float4 v = reinterpret_cast<const float4*>(ring)[((long long)n * ringlen + ri) * C4 + c4];
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            for (int q = 0; q < nsplit; ++q) {  // the K splits' ring copies, in split order
+                const float4 v = reinterpret_cast<const float4*>(ring)[(((long long)q * N + n) * ringlen + ri) * C4 + c4];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
         }
     *o = s;
 }
@@ -2180,6 +2192,17 @@ namespace dcs {
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
                    const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream,
                    int fold = 0);
+// K splits of the ring-rows pass (fold 2) of a padded-grid data gradient: enough workgroups for two
+// per CU, at least 4 k-tiles per split, at most 8 ring copies
+int ring_ksplit(const dcs_conv_desc& d) {
+    const long long M = (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2));
+    const long long tiles = cdiv(M, 128) * cdiv(d.Co, d.Co > 64 ? 128 : 64);
+    const long long nkt = cdiv((long long)d.KH * d.KW * d.Cs, 32);
+    long long k = cdiv(512, tiles);
+    if (k > 8) k = 8;
+    while (k > 1 && nkt / k < 4) --k;
+    return k < 1 ? 1 : (int)k;
+}
 }  // namespace dcs
 namespace dcs {
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
@@ -2204,7 +2227,11 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     }
     if (fold == 2) Mmax = (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2));  // ring rows only
     const int gx = (int)cdiv(Mmax, 128), gy = (int)cdiv(d.Co, BN);
-    dim3 grid((unsigned)(gx * gy * ncls));
+    // ring rows (fold 2): K split over the grid's z so the few ring tiles fill the chip (each split
+    // writes its own ring copy; reflect_ring_fold sums them)
+    const int ksplit = fold == 2 ? ring_ksplit(d) : 1;
+    const int fold_arg = fold | (ksplit > 1 ? ksplit << 2 : 0);
+    dim3 grid((unsigned)(gx * gy * ncls * ksplit));
     if (bm_used) *bm_used = 128;
     const bool vec = vec_ok(dp, src);
     const bool v4 = !vec && vec4_ok(dp, src) && d.pro_act == DCS_ACT_NONE && !d.parity;
@@ -2223,13 +2250,13 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16X3>), G, dim3(2 * BM_), 0, s, d, src, src2, \
-                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);                                        \
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold_arg);                                        \
     else if (d.mma == MMA_F16)                                                                                       \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16>), G, dim3(2 * BM_), 0, s, d, src, src2,   \
-                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);                                        \
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold_arg);                                        \
     else                                                                                                             \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_BF16X6>), G, dim3(2 * BM_), 0, s, d, src, src2, \
-                           wpack, bias, psc, psh, out, gxx, gy, parts, fold);
+                           wpack, bias, psc, psh, out, gxx, gy, parts, fold_arg);
     if (vec && x6f && (BN == 128 || DCS_X6_BN64) && !DCS_ROWS_F32) {  // x6 / f16x3: 128- or 64-column tiles
         // 256-row tiles where they divide the pixels evenly (the forward over whole 128 x 128
         // images); the 130 x 130 padded data gradient keeps 128-row tiles (measured: its partial
@@ -2267,33 +2294,33 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         if (DCS_BF16P_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
             const int gx2 = (int)cdiv(Mmax, 256);
             hipLaunchKernelGGL((conv_rows_kernel<256, 128, 1, 1, MMA_BF16P>), dim3((unsigned)(gx2 * gy)), dim3(512), 0, s,
-                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts, fold);
+                               d, src, src2, wpack, bias, psc, psh, out, gx2, gy, parts, fold_arg);
             if (bm_used) *bm_used = 256;
         } else {
             hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, MMA_BF16P>), grid, dim3(NT), 0, s, d, src, src2, wpack,
-                               bias, psc, psh, out, gx, gy, parts, fold);
+                               bias, psc, psh, out, gx, gy, parts, fold_arg);
         }
         return check_launch("conv_rows");
     }
     const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \
-    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold); \
-    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);  \
-    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+    if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg); \
+    else if (BN == 128) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);  \
+    else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
         if (d.mma == MMA_BF16) { DCS_ROWS_MMA(MMA_BF16) } else { DCS_ROWS_MMA(MMA_BF16X3) }
 #undef DCS_ROWS_MMA
         return check_launch("conv_rows");
     }
     if (BN == 128) {
-        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        if (vec && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
+        else if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 128, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
     } else {
-        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
-        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold);
+        if (vec) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 1, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
+        else if (v4) hipLaunchKernelGGL((conv_rows_kernel<128, 64, 2, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
+        else hipLaunchKernelGGL((conv_rows_kernel<128, 64, 0, 0>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg);
     }
     return check_launch("conv_rows");
 }
@@ -2770,7 +2797,8 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
 namespace dcs {
 bool wgrad_win_check(const dcs_conv_desc& d);
 size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
-int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh, float* ws,
+                     hipStream_t s);
 }  // namespace dcs
 
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
@@ -2803,7 +2831,8 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
     if (DCS_WGRAD_WIN && wgrad_win_check(d)) {  // f16x3 residual geometry: the rolling-window kernel
-        const int ns = wgrad_win_launch(d, dy, x, w, s);
+        if (d.pro_act != DCS_ACT_NONE && (!psc || !psh)) return fail(DCS_E_INVALID, "conv_wgrad: missing prologue");
+        const int ns = wgrad_win_launch(d, dy, x, psc, psh, w, s);
         if (ns < 0) return -ns;
         const long long total = (long long)d.Co * 9 * d.Cs;
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
@@ -3013,7 +3042,8 @@ extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* 
 
 extern "C" size_t dcs_conv_dgrad_reflect_ring_size(const dcs_conv_desc* dp) {
     if (!dp || dp->Ho < 6 || dp->Wo < 6) return 0;
-    return (size_t)dp->N * (2 * dp->Wo + 2 * (dp->Ho - 2)) * dp->Co * sizeof(float);
+    // the window path's ring pass writes one ring copy per K split
+    return (size_t)ring_ksplit(*dp) * dp->N * (2 * dp->Wo + 2 * (dp->Ho - 2)) * dp->Co * sizeof(float);
 }
 
 extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, const float* wpack,
@@ -3033,16 +3063,17 @@ extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, 
     const int H = d.Ho - 2, W = d.Wo - 2, C4 = d.Co / 4;
     const long long total = (long long)d.N * (2 * W + 2 * (H - 2)) * C4;
     hipLaunchKernelGGL(reflect_ring_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), ring,
-                       dx, d.N, H, W, C4);
+                       dx, d.N, H, W, C4, 1);
     return check_launch("reflect_ring_fold");
 }
 
 namespace dcs {
 // fold the padded grid's ring (dcs_conv_dgrad_reflect's ring layout) onto dx's border (H x W interior)
-int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, hipStream_t s) {
+int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, hipStream_t s) {
     const int C4 = C / 4;
     const long long total = (long long)N * (2 * W + 2 * (H - 2)) * C4;
-    hipLaunchKernelGGL(reflect_ring_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, ring, dx, N, H, W, C4);
+    hipLaunchKernelGGL(reflect_ring_fold_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, ring, dx, N, H, W, C4,
+                       nsplit);
     return check_launch("reflect_ring_fold");
 }
 }  // namespace dcs

@@ -39,7 +39,10 @@ struct WinArgs {
     int R, tiles;        // image rows per tile (256 / W), tiles per image (H / R)
     int gy;              // column tiles (Co / 128)
     int rng_n;           // partial maxima of the source range record
+    int pro_act;         // DCS_ACT_*: InstanceNorm apply (+ act) of the source at staging, per (image, channel)
 };
+
+constexpr int WIN_PRO_CMAX = 512;  // source channels the staged prologue covers
 
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 
@@ -113,16 +116,22 @@ __device__ __forceinline__ void win_stats(const floatx16 (&acc)[2][2], int p0, i
     }
 }
 
-// NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only)
-template <int NP>
+// NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only);
+// PRO: the source prologue (a separate instance: the prologue-free passes keep their register budget)
+template <int NP, bool PRO>
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
                                                                  const _Float16* __restrict__ wh,
                                                                  const _Float16* __restrict__ wl,
                                                                  const float* __restrict__ rng,
                                                                  const int* __restrict__ wexp,
                                                                  const float* __restrict__ addend,
-                                                                 float* __restrict__ out, Part* __restrict__ parts) {
+                                                                 float* __restrict__ out, Part* __restrict__ parts,
+                                                                 const float* __restrict__ psc,
+                                                                 const float* __restrict__ psh) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT];
+    // the source prologue's scale / shift of this tile's image (the window kernels' tiles never
+    // straddle images), read at staging from LDS so the staging issues no global load of its own
+    __shared__ __attribute__((aligned(16))) float prl[PRO ? 2 * WIN_PRO_CMAX : 4];
     _Float16* const Wn = smem;                               // [2][2][WIN_PIX][16]
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;        // [2][6][WIN_SLOT]
 
@@ -144,6 +153,23 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int ea = f16x3_exp(rng, a.rng_n);
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
     const float asc = __builtin_ldexpf(1.f, ea);
+    if constexpr (PRO) {
+        for (int i = tid; i < C; i += WIN_NT) {
+            prl[i] = psc[(long long)n * C + i];
+            prl[WIN_PRO_CMAX + i] = psh[(long long)n * C + i];
+        }
+        __syncthreads();
+    }
+    // prologue of one staged unit (8 channels c0 .. c0 + 7 of a real source pixel)
+    auto pro8 = [&](float4& v0, float4& v1, int c0) {
+        const float4 s0 = *reinterpret_cast<const float4*>(prl + c0), s1 = *reinterpret_cast<const float4*>(prl + c0 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(prl + WIN_PRO_CMAX + c0);
+        const float4 b1 = *reinterpret_cast<const float4*>(prl + WIN_PRO_CMAX + c0 + 4);
+        v0.x = act_apply(fmaf(v0.x, s0.x, b0.x), a.pro_act); v0.y = act_apply(fmaf(v0.y, s0.y, b0.y), a.pro_act);
+        v0.z = act_apply(fmaf(v0.z, s0.z, b0.z), a.pro_act); v0.w = act_apply(fmaf(v0.w, s0.w, b0.w), a.pro_act);
+        v1.x = act_apply(fmaf(v1.x, s1.x, b1.x), a.pro_act); v1.y = act_apply(fmaf(v1.y, s1.y, b1.y), a.pro_act);
+        v1.z = act_apply(fmaf(v1.z, s1.z, b1.z), a.pro_act); v1.w = act_apply(fmaf(v1.w, s1.w, b1.w), a.pro_act);
+    };
 
     // window staging units of this thread: (pixel, 8-channel half); the byte offset of the unit's
     // source channel 0 (OOB_OFF-style sentinel -1 for zero padding / past the window)
@@ -179,10 +205,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         __builtin_memcpy(&wq[0], &v0, 16);
         __builtin_memcpy(&wq[1], &v1, 16);
     };
-    auto win_store_q = [&](int buf, int q) {
+    auto win_store_q = [&](int buf, int q, int cur_slice) {
         const int u = tid + q * WIN_NT;
         const int wpix = u >> 1, h = u & 1;
         if (wpix < npix) {
+            if (PRO && uoff[q] >= 0) pro8(wq[0], wq[1], cur_slice * 16 + 8 * h);
             f16x8 hi, lo;
             split8h(wq[0], wq[1], asc, hi, lo);
             *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
@@ -203,12 +230,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             __builtin_memcpy(&wr_[q][1], &v1, 16);
         }
     };
-    auto win_store = [&](int buf) {
+    auto win_store = [&](int buf, int cur_slice) {
 #pragma unroll
         for (int q = 0; q < WIN_UNITS; ++q) {
             const int u = tid + q * WIN_NT;
             const int wpix = u >> 1, h = u & 1;
             if (wpix < npix) {
+                if (PRO && uoff[q] >= 0) pro8(wr_[q][0], wr_[q][1], cur_slice * 16 + 8 * h);
                 f16x8 hi, lo;
                 split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
@@ -270,11 +298,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #pragma unroll
     for (int q = 0; q < WIN_UNITS; ++q) {
         win_load_q(0, q);
-        win_store_q(0, q);
+        win_store_q(0, q, 0);
     }
 #else
     win_load(0);
-    win_store(0);
+    win_store(0, 0);
 #endif
     b_load(0);
     b_store(0);
@@ -325,9 +353,9 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             b_store(bbuf ^ 1);
             b_load(tt + 2 < last ? tt + 2 : last);
 #if DCS_WIN_SPREAD
-            win_store_q(wbuf ^ 1, ty);
+            win_store_q(wbuf ^ 1, ty, s + 1 < nslice ? s + 1 : s);
 #else
-            if (ty == 2) win_store(wbuf ^ 1);
+            if (ty == 2) win_store(wbuf ^ 1, s + 1 < nslice ? s + 1 : s);
 #endif
             __syncthreads();
         }
@@ -456,6 +484,7 @@ struct WWArgs {
     int strips, rchunks, rows_per;  // 64-pixel strips per row, row chunks per strip, rows per chunk
     int gco, gci;        // 64-channel tiles of co / ci
     int rng_a_n, rng_b_n;
+    int pro_act;         // DCS_ACT_*: InstanceNorm apply (+ act) of the source at staging, per (image, channel)
 };
 
 __device__ __forceinline__ int ww_swz(int pix) { return ((pix >> 1) & 1) << 2; }
@@ -474,8 +503,11 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                                                                  const float* __restrict__ src,
                                                                  const float* __restrict__ rnga,
                                                                  const float* __restrict__ rngb,
-                                                                 float* __restrict__ ws) {
+                                                                 float* __restrict__ ws,
+                                                                 const float* __restrict__ psc,
+                                                                 const float* __restrict__ psh) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
+    __shared__ __attribute__((aligned(16))) float prl[2 * 64];  // source prologue of this tile's 64 channels
     _Float16* const Xr = smem;                 // [4][2][66][64]
     _Float16* const Dy = smem + 4 * WW_XROW;   // [2][2][64][64]
 
@@ -495,6 +527,19 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 
     const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
     const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+    if (a.pro_act != DCS_ACT_NONE && tid < 64) {  // made visible by the prologue's barrier below
+        prl[tid] = psc[(long long)n * C + ci0 + tid];
+        prl[64 + tid] = psh[(long long)n * C + ci0 + tid];
+    }
+    auto pro8 = [&](float4& v0, float4& v1, int c0) {
+        const float4 s0 = *reinterpret_cast<const float4*>(prl + c0), s1 = *reinterpret_cast<const float4*>(prl + c0 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(prl + 64 + c0);
+        const float4 b1 = *reinterpret_cast<const float4*>(prl + 64 + c0 + 4);
+        v0.x = act_apply(fmaf(v0.x, s0.x, b0.x), a.pro_act); v0.y = act_apply(fmaf(v0.y, s0.y, b0.y), a.pro_act);
+        v0.z = act_apply(fmaf(v0.z, s0.z, b0.z), a.pro_act); v0.w = act_apply(fmaf(v0.w, s0.w, b0.w), a.pro_act);
+        v1.x = act_apply(fmaf(v1.x, s1.x, b1.x), a.pro_act); v1.y = act_apply(fmaf(v1.y, s1.y, b1.y), a.pro_act);
+        v1.z = act_apply(fmaf(v1.z, s1.z, b1.z), a.pro_act); v1.w = act_apply(fmaf(v1.w, s1.w, b1.w), a.pro_act);
+    };
 
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
@@ -557,6 +602,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int q = 0; q < WW_XU; ++q) {
             if (xls[q] >= 0) {
+                if (a.pro_act != DCS_ACT_NONE && xoff[q] >= 0) pro8(xr[q][0], xr[q][1], 8 * ((tid + q * WW_NT) & 7));
                 f16x8 hi, lo;
                 split8h(xr[q][0], xr[q][1], bsc, hi, lo);
                 *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
@@ -589,6 +635,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
 
+    if (a.pro_act != DCS_ACT_NONE) __syncthreads();  // prl
     // prologue: source rows y_beg-1 .. y_beg+1 into their ring slots, dy row y_beg into buffer 0
 #pragma unroll 1
     for (int r = y_beg - 1; r <= y_beg + 1; ++r) {
@@ -706,7 +753,8 @@ bool wgrad_win_check(const dcs_conv_desc& d) {
            d.pt == 1 && d.pl == 1 && d.Ho == d.Hs && d.Wo == d.Ws && d.Cs % 64 == 0 && d.Co % 64 == 0 &&
            d.Ws % WW_SW == 0 && d.Hs >= 2 && d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
            d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) &&
-           d.pro_act == DCS_ACT_NONE && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 &&
+           (d.pro_act == DCS_ACT_NONE || d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU ||
+            d.pro_act == DCS_ACT_LRELU) && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 &&
            d.rng_b_n > 0 && d.rng_b_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
            (long long)d.N * d.Hs * d.Ws * d.Co * 4 < 0x7fffff00LL - 64;
 }
@@ -717,7 +765,8 @@ size_t wgrad_win_workspace_size(const dcs_conv_desc& d) {
 }
 
 // partial slabs into ws (wgrad_win_workspace_size bytes); returns the split count (< 0: error)
-int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s) {
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh, float* ws,
+                     hipStream_t s) {
     const WWPlan p = ww_plan(d);
     WWArgs a;
     a.N = d.N; a.H = d.Hs; a.W = d.Ws; a.C = d.Cs; a.Co = d.Co;
@@ -725,11 +774,14 @@ int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, fl
     a.strips = p.strips; a.rchunks = p.rchunks; a.rows_per = p.rows_per;
     a.gco = d.Co / 64; a.gci = d.Cs / 64;
     a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n;
+    a.pro_act = d.pro_act;
     const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
     if (d.mma == DCS_MMA_F16)
-        hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws,
+                           psc, psh);
     else
-        hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws,
+                           psc, psh);
     const int e = check_launch("wgrad3_win");
     return e ? -e : p.nsplit;
 }
@@ -740,28 +792,38 @@ int win_check(const dcs_conv_desc& d, bool fwd) {
     const bool geom = d.KH == 3 && d.KW == 3 && d.stride == 1 && d.up == 1 && !d.parity && d.Cs % 16 == 0 &&
                       d.Co % WIN_BN == 0 && d.Ws <= 128 && 256 % d.Ws == 0 && d.Hs % (256 / d.Ws) == 0 &&
                       d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
-                      d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                      d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs &&
                       d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_a_n > 0 &&
                       d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL;
     if (!geom) return 0;
+    // a source prologue (IN apply + act at staging) on the forward only
+    const bool pro_ok = d.pro_act == DCS_ACT_NONE ||
+                        (fwd && d.Cs <= WIN_PRO_CMAX && (d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU ||
+                                                         d.pro_act == DCS_ACT_LRELU));
+    if (!pro_ok) return 0;
     if (fwd) return d.Ho == d.Hs && d.Wo == d.Ws && d.pt == 1 && d.pl == 1;
     return d.Ho == d.Hs + 2 && d.Wo == d.Ws + 2 && d.pt == 2 && d.pl == 2 && d.pad_mode == DCS_PAD_ZERO;
 }
 
 int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* src, const void* wh, const void* wl,
-               const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s) {
+               const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s,
+               const float* psc = nullptr, const float* psh = nullptr) {
     WinArgs a;
     a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
+    a.pro_act = d.pro_act;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
-    if (d.mma == DCS_MMA_F16)
-        hipLaunchKernelGGL(conv3_win_h3_kernel<1>, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
-                           reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
-                           addend, out, parts);
-    else
-        hipLaunchKernelGGL(conv3_win_h3_kernel<3>, dim3(blocks), dim3(WIN_NT), 0, s, a, src,
-                           reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp,
-                           addend, out, parts);
+#define DCS_WIN_LAUNCH(NP_, PRO_)                                                                                   \
+    hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, PRO_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                     \
+                       reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
+                       out, parts, psc, psh);
+    const bool pro = d.pro_act != DCS_ACT_NONE;
+    if (d.mma == DCS_MMA_F16) {
+        if (pro) { DCS_WIN_LAUNCH(1, true) } else { DCS_WIN_LAUNCH(1, false) }
+    } else {
+        if (pro) { DCS_WIN_LAUNCH(3, true) } else { DCS_WIN_LAUNCH(3, false) }
+    }
+#undef DCS_WIN_LAUNCH
     return check_launch("conv3_win");
 }
 
@@ -770,7 +832,8 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
 // conv.hip: the generic rows pass (ring rows of the padded data gradient) and the ring fold
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
                    const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream, int fold);
-int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, hipStream_t s);
+int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, hipStream_t s);
+int ring_ksplit(const dcs_conv_desc& d);
 
 }  // namespace dcs
 
@@ -795,11 +858,13 @@ extern "C" int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, 
 
 extern "C" int dcs_conv3_win_ok(const dcs_conv_desc* dp, int dgrad) { return dp ? win_check(*dp, !dgrad) : 0; }
 
-extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
-                                      const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk,
-                                      void* stream) {
+extern "C" int dcs_conv3_win_in_stats_pro(const dcs_conv_desc* dp, const float* src, const float* pro_scale,
+                                          const float* pro_shift, const void* w_hi, const void* w_lo, const int* wexp,
+                                          float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
     if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "conv3_win: null pointer");
     const dcs_conv_desc& d = *dp;
+    if (d.pro_act != DCS_ACT_NONE && (!pro_scale || !pro_shift))
+        return fail(DCS_E_INVALID, "conv3_win: the source prologue needs pro_scale / pro_shift");
     if (!win_check(d, true))
         return fail(DCS_E_INVALID, "conv3_win: needs a 3x3 stride-1 'same' f16x3 conv over contiguous NHWC rows "
                                    "(W <= 128, 256 % W == 0, H % (256 / W) == 0, Cs % 16 == 0, Co % 128 == 0)");
@@ -810,7 +875,15 @@ extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src,
         *nchunk = tiles;
     }
     return launch_win(d, d.Hs, d.Ws, d.pad_mode == DCS_PAD_REFLECT, src, w_hi, w_lo, wexp, nullptr, out,
-                      reinterpret_cast<Part*>(parts), as_stream(stream));
+                      reinterpret_cast<Part*>(parts), as_stream(stream), pro_scale, pro_shift);
+}
+
+extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
+                                      const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk,
+                                      void* stream) {
+    if (dp && dp->pro_act != DCS_ACT_NONE)
+        return fail(DCS_E_INVALID, "conv3_win: a descriptor with a prologue goes through dcs_conv3_win_in_stats_pro");
+    return dcs_conv3_win_in_stats_pro(dp, src, nullptr, nullptr, w_hi, w_lo, wexp, out, parts, parts_bytes, nchunk, stream);
 }
 
 extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* dy, const float* wpack,
@@ -828,5 +901,5 @@ extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* 
     if (e) return e;
     // the padded grid's one-pixel ring by the generic rows pass, then folded onto the border
     if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
-    return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, s);
+    return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, ring_ksplit(d), s);
 }

@@ -283,6 +283,32 @@ extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, voi
     return check_launch("channel_sum_final");
 }
 
+// range record of relu(x * scale + shift) from the InstanceNorm statistics (dcs_range_from_in_stats):
+// with scale > 0 the largest value of a (image, channel) plane is relu(xmax * scale + shift), so
+// part i is the max over the planes j = i (mod DCS_RANGE_PARTS) of that value -- the same number the
+// materialising dcs_in_apply would have recorded, without a pass over the tensor
+__global__ __launch_bounds__(256) void range_from_in_stats_kernel(const float* __restrict__ sc,
+                                                                  const float* __restrict__ sh,
+                                                                  const float* __restrict__ xmax, int n,
+                                                                  float* __restrict__ parts) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= DCS_RANGE_PARTS) return;
+    float m = 0.f;
+    for (int j = i; j < n; j += DCS_RANGE_PARTS) m = fmaxf(m, act_apply(fmaf(xmax[j], sc[j], sh[j]), DCS_ACT_RELU));
+    parts[i] = m;
+}
+
+extern "C" int dcs_range_from_in_stats(const float* scale, const float* shift, const float* xmax, int n, int act,
+                                       float* parts, void* stream) {
+    if (!scale || !shift || !xmax || !parts || n <= 0)
+        return fail(DCS_E_INVALID, "range_from_in_stats: bad arguments");
+    if (act != DCS_ACT_RELU)
+        return fail(DCS_E_INVALID, "range_from_in_stats: DCS_ACT_RELU only (the bound needs scale > 0 and a floor at 0)");
+    hipLaunchKernelGGL(range_from_in_stats_kernel, dim3((DCS_RANGE_PARTS + 255) / 256), dim3(256), 0, as_stream(stream),
+                       scale, shift, xmax, n, parts);
+    return check_launch("range_from_in_stats");
+}
+
 extern "C" int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale, const float* shift,
                                int act, float* parts, void* stream) {
     if (!x || !parts || n_img <= 0 || per_img <= 0 || per_img % 4 || (reinterpret_cast<uintptr_t>(x) & 15))
