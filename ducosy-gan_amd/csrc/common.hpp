@@ -121,4 +121,11 @@ struct Part {
     int pad[3];
 };
 
+// Partial sums of the InstanceNorm backward over a chunk of one image's pixels, per channel:
+// a = sum g, b = sum g * xhat with g = da * act'(xhat) (norm.hip in_bwd_*; the window data gradient's
+// epilogue and the ring fold write them too, conv_win.hip / conv.hip)
+struct Sum2 {
+    float a, b;
+};
+
 }  // namespace dcs

@@ -3067,7 +3067,98 @@ extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, 
     return check_launch("reflect_ring_fold");
 }
 
+// The same fold, and the InstanceNorm-backward partial sums of the folded pixels (the window data
+// gradient's epilogue leaves rows 1, H - 2 and columns 1, W - 2 to it): block (n, chunk fc) folds the
+// targets fc * tpc .. of image n, 256 / C4 targets at a time, and writes per channel sum g and
+// sum g * xhat over them (g = final da * act'(xhat), xhat = y * sc + sh) to parts chunk chunk0 + fc,
+// reduced over the block's target lanes in a fixed order.
+__global__ __launch_bounds__(256) void reflect_ring_fold_ibw_kernel(const float* __restrict__ ring, float* __restrict__ dx,
+                                                                    int N, int H, int W, int C4, int nsplit,
+                                                                    const float* __restrict__ yin,
+                                                                    const float* __restrict__ sc,
+                                                                    const float* __restrict__ sh, int act,
+                                                                    Sum2* __restrict__ parts, int nchunk, int chunk0,
+                                                                    int nfc) {
+    const int n = blockIdx.x / nfc, fc = blockIdx.x - n * nfc;
+    const int ntgt = 2 * W + 2 * (H - 2);
+    const int tpc = (ntgt + nfc - 1) / nfc;
+    const int lanes = 256 / C4, c4 = threadIdx.x % C4, tl = threadIdx.x / C4;
+    const int Hp = H + 2, Wp = W + 2, ringlen = 2 * Wp + 2 * H;
+    const int C = 4 * C4;
+    const float4 s4 = *reinterpret_cast<const float4*>(sc + (long long)n * C + 4 * c4);
+    const float4 b4 = *reinterpret_cast<const float4*>(sh + (long long)n * C + 4 * c4);
+    float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+    const int t1 = (fc + 1) * tpc < ntgt ? (fc + 1) * tpc : ntgt;
+    for (int t = fc * tpc + tl; t < t1; t += lanes) {
+        int y, x;
+        if (t < 2 * W) {
+            y = t < W ? 1 : H - 2;
+            x = t < W ? t : t - W;
+        } else {
+            const int u = t - 2 * W;
+            const int rr = u >> 1;
+            y = rr == 0 ? 0 : (rr <= H - 4 ? rr + 1 : H - 1);
+            x = (u & 1) ? W - 2 : 1;
+        }
+        int ay[3], ax[3];
+        const int ny = reflect_pre(y, H, 1, ay), nx = reflect_pre(x, W, 1, ax);
+        const long long pix = ((long long)n * H + y) * W + x;
+        float4* o = reinterpret_cast<float4*>(dx) + pix * C4 + c4;
+        float4 v = *o;
+        for (int p = 0; p < ny; ++p)
+            for (int q = 0; q < nx; ++q) {
+                const int yp = ay[p], xp = ax[q];
+                if (yp >= 1 && yp <= H && xp >= 1 && xp <= W) continue;
+                const int ri = yp == 0 ? xp : (yp == Hp - 1 ? Wp + xp : 2 * Wp + 2 * (yp - 1) + (xp == 0 ? 0 : 1));
+                for (int qq = 0; qq < nsplit; ++qq) {
+                    const float4 r = reinterpret_cast<const float4*>(ring)[(((long long)qq * N + n) * ringlen + ri) * C4 + c4];
+                    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+                }
+            }
+        *o = v;
+        const float4 y4 = reinterpret_cast<const float4*>(yin)[pix * C4 + c4];
+        const float dv[4] = {v.x, v.y, v.z, v.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
+        const float s_[4] = {s4.x, s4.y, s4.z, s4.w}, b_[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float xh = fmaf(yv[e], s_[e], b_[e]);
+            const float g = dv[e] * act_grad(xh, act);
+            sa[e] += g;
+            sb[e] = fmaf(g, xh, sb[e]);
+        }
+    }
+    __shared__ float red[8][256];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[e][threadIdx.x] = sa[e];
+        red[4 + e][threadIdx.x] = sb[e];
+    }
+    __syncthreads();
+    if (tl == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float a = 0.f, b = 0.f;
+            for (int l = 0; l < lanes; ++l) {
+                a += red[e][l * C4 + c4];
+                b += red[4 + e][l * C4 + c4];
+            }
+            parts[((long long)n * nchunk + chunk0 + fc) * C + 4 * c4 + e] = Sum2{a, b};
+        }
+    }
+}
+
 namespace dcs {
+// fold + IN-backward partial sums of the folded pixels (reflect_ring_fold_ibw_kernel); C / 4 divides 256
+int reflect_ring_fold_ibw(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, const float* y,
+                          const float* sc, const float* sh, int act, Sum2* parts, int nchunk, int chunk0, int nfc,
+                          hipStream_t s) {
+    const int C4 = C / 4;
+    if (C % 4 || 256 % C4) return fail(DCS_E_INVALID, "reflect_ring_fold_ibw: C / 4 must divide 256");
+    hipLaunchKernelGGL(reflect_ring_fold_ibw_kernel, dim3((unsigned)(N * nfc)), dim3(256), 0, s, ring, dx, N, H, W, C4,
+                       nsplit, y, sc, sh, act, parts, nchunk, chunk0, nfc);
+    return check_launch("reflect_ring_fold_ibw");
+}
+
 // fold the padded grid's ring (dcs_conv_dgrad_reflect's ring layout) onto dx's border (H x W interior)
 int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, hipStream_t s) {
     const int C4 = C / 4;

@@ -26,7 +26,7 @@
 namespace dcs {
 namespace {
 
-constexpr int WIN_BM = 256, WIN_BN = 128, WIN_NT = 512;
+constexpr int WIN_BN = 128, WIN_NT = 512;  // tiles: 256 pixels (whole rows) x WIN_BN channels
 constexpr int WIN_PIX = 520;             // window pixels for W <= 128: (256 / W + 2) * (W + 2) <= 520
 // halves per B plane-slot: 128 rows x 16 k + 48 (96 B: the three tx slots of a row, written by
 // neighbouring lanes, land on distinct banks)
@@ -116,9 +116,75 @@ __device__ __forceinline__ void win_stats(const floatx16 (&acc)[2][2], int p0, i
     }
 }
 
+// The InstanceNorm backward's partial sums over a data-gradient tile (IBW instances): the output is
+// da of a layer a = act(IN(y)); per channel sum g and sum g * xhat with xhat = y * sc + sh and
+// g = da * act'(xhat), over the tile's pixels except the ones the reflection ring fold still adds to
+// (rows 1, H - 2 and columns 1, W - 2: the fold kernel sums those with their final values).
+struct IbwArgs {
+    const float* y;
+    const float* sc;
+    const float* sh;
+    Sum2* parts;  // [N][nchunk][Co]
+    int act, nchunk;
+};
+
+// y of the tile's outputs, every load issued before the first use
+__device__ __forceinline__ void win_ibw_load(float (&yv)[2][2][16], const IbwArgs& ib, long long obase, int p0, int Co,
+                                             int n0, int wm, int wn, int lane) {
+    const int kh = lane >> 5, l32 = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                yv[i][j][r] = ib.y[obase + (long long)pix * Co + n0 + wn * 64 + j * 32 + l32];
+            }
+}
+
+__device__ __forceinline__ void win_ibw(const floatx16 (&acc)[2][2], const float (&yv)[2][2][16], const IbwArgs& ib,
+                                        int n, int p0, int H, int W, int Co, int n0, int wm, int wn, int lane, int tid,
+                                        int tile, float* lds) {
+    const int kh = lane >> 5, l32 = lane & 31;
+    Sum2* sp = reinterpret_cast<Sum2*>(lds);  // [4][128]; the k-loop's last barrier freed the LDS
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + l32;
+        const float s = ib.sc[(long long)n * Co + col], b = ib.sh[(long long)n * Co + col];
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int py = pix / W, px = pix - py * W;
+                if (py == 1 || py == H - 2 || px == 1 || px == W - 2) continue;  // the ring fold's pixels
+                const float xh = fmaf(yv[i][j][r], s, b);
+                const float g = acc[i][j][r] * act_grad(xh, ib.act);
+                sa += g;
+                sb = fmaf(g, xh, sb);
+            }
+        sa += __shfl_xor(sa, 32, 64);  // the same operand pair on both lanes: order-free
+        sb += __shfl_xor(sb, 32, 64);
+        if (kh == 0) sp[wm * 128 + wn * 64 + j * 32 + l32] = Sum2{sa, sb};
+    }
+    __syncthreads();
+    if (tid < 128 && n0 + tid < Co) {
+        Sum2 t = sp[tid];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            t.a += sp[w * 128 + tid].a;
+            t.b += sp[w * 128 + tid].b;
+        }
+        ib.parts[((long long)n * ib.nchunk + tile) * Co + n0 + tid] = t;
+    }
+}
+
 // NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only);
-// PRO: the source prologue (a separate instance: the prologue-free passes keep their register budget)
-template <int NP, bool PRO>
+// PRO: the source prologue (a separate instance: the prologue-free passes keep their register budget);
+// IBW: the InstanceNorm-backward partial sums of the output (data gradients without addend)
+template <int NP, bool PRO, bool IBW>
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
                                                                  const _Float16* __restrict__ wh,
                                                                  const _Float16* __restrict__ wl,
@@ -127,7 +193,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                                                                  const float* __restrict__ addend,
                                                                  float* __restrict__ out, Part* __restrict__ parts,
                                                                  const float* __restrict__ psc,
-                                                                 const float* __restrict__ psh) {
+                                                                 const float* __restrict__ psh, IbwArgs ib) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT];
     // the source prologue's scale / shift of this tile's image (the window kernels' tiles never
     // straddle images), read at staging from LDS so the staging issues no global load of its own
@@ -384,6 +450,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
         return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 32 + l32;
     };
+
     if (addend) {  // wave-uniform: all 64 addend loads issued before the first use
         floatx16 ad[2][2];
 #pragma unroll
@@ -408,6 +475,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     }
     if (parts) win_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(smem), parts,
                          (long long)n * a.tiles + tile);
+    if constexpr (IBW) {  // (y loaded here, after the stores: issuing them earlier spills ~70 VGPRs)
+        float yv[2][2][16];
+        win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm, wn, lane);
+        win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(smem));
+    }
 }
 
 // pre-split weight pack (dcs_pack_weights_h3): the range of the raw weights first, then every block
@@ -807,21 +879,24 @@ int win_check(const dcs_conv_desc& d, bool fwd) {
 
 int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* src, const void* wh, const void* wl,
                const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s,
-               const float* psc = nullptr, const float* psh = nullptr) {
+               const float* psc = nullptr, const float* psh = nullptr, const IbwArgs* ibw = nullptr) {
     WinArgs a;
     a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
     a.pro_act = d.pro_act;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
-#define DCS_WIN_LAUNCH(NP_, PRO_)                                                                                   \
-    hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, PRO_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                     \
+    const IbwArgs ib = ibw ? *ibw : IbwArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
+#define DCS_WIN_LAUNCH(NP_, PRO_, IBW_)                                                                             \
+    hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, PRO_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,              \
                        reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
-                       out, parts, psc, psh);
+                       out, parts, psc, psh, ib);
     const bool pro = d.pro_act != DCS_ACT_NONE;
-    if (d.mma == DCS_MMA_F16) {
-        if (pro) { DCS_WIN_LAUNCH(1, true) } else { DCS_WIN_LAUNCH(1, false) }
+    if (ibw) {
+        if (d.mma == DCS_MMA_F16) { DCS_WIN_LAUNCH(1, false, true) } else { DCS_WIN_LAUNCH(3, false, true) }
+    } else if (d.mma == DCS_MMA_F16) {
+        if (pro) { DCS_WIN_LAUNCH(1, true, false) } else { DCS_WIN_LAUNCH(1, false, false) }
     } else {
-        if (pro) { DCS_WIN_LAUNCH(3, true) } else { DCS_WIN_LAUNCH(3, false) }
+        if (pro) { DCS_WIN_LAUNCH(3, true, false) } else { DCS_WIN_LAUNCH(3, false, false) }
     }
 #undef DCS_WIN_LAUNCH
     return check_launch("conv3_win");
@@ -833,7 +908,11 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
 int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2, const float* wpack, const float* bias,
                    const float* psc, const float* psh, float* out, Part* parts, int* bm_used, void* stream, int fold);
 int reflect_ring_fold(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, hipStream_t s);
+int reflect_ring_fold_ibw(const float* ring, float* dx, int N, int H, int W, int C, int nsplit, const float* y,
+                          const float* sc, const float* sh, int act, Sum2* parts, int nchunk, int chunk0, int nfc,
+                          hipStream_t s);
 int ring_ksplit(const dcs_conv_desc& d);
+constexpr int IBW_FOLD_CHUNKS = 16;  // partial-sum chunks of the ring fold per image
 
 }  // namespace dcs
 
@@ -902,4 +981,37 @@ extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* 
     // the padded grid's one-pixel ring by the generic rows pass, then folded onto the border
     if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
     return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, ring_ksplit(d), s);
+}
+
+extern "C" size_t dcs_conv_dgrad_reflect_win_inbwd_parts_size(const dcs_conv_desc* dp) {
+    if (!dp || dp->Ws <= 0 || 256 % dp->Ws) return 0;
+    const int H = dp->Ho - 2, W = dp->Wo - 2;
+    if (H <= 0 || W <= 0 || (long long)H * W % 256) return 0;
+    return (size_t)dp->N * (H * W / 256 + IBW_FOLD_CHUNKS) * dp->Co * sizeof(Sum2);
+}
+
+extern "C" int dcs_conv_dgrad_reflect_win_inbwd(const dcs_conv_desc* dp, const float* dy, const float* wpack,
+                                                const void* w_hi, const void* w_lo, const int* wexp, float* dx,
+                                                float* ring, const float* y, const float* scale, const float* shift,
+                                                int act, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
+    if (!dp || !dy || !wpack || !w_hi || !w_lo || !wexp || !dx || !ring || !y || !scale || !shift || !parts || !nchunk)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect_win_inbwd: null pointer");
+    const dcs_conv_desc& d = *dp;
+    if (!win_check(d, false) || d.Co % 4 != 0 || 256 % (d.Co / 4) || d.Hs < 4 || d.Ws < 4)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect_win_inbwd: a dcs_conv_dgrad_reflect_win geometry with Co / 4 "
+                                   "dividing 256 expected");
+    if (act != DCS_ACT_AFFINE && act != DCS_ACT_RELU && act != DCS_ACT_LRELU)
+        return fail(DCS_E_INVALID, "conv_dgrad_reflect_win_inbwd: act must be DCS_ACT_AFFINE / _RELU / _LRELU");
+    if (parts_bytes < dcs_conv_dgrad_reflect_win_inbwd_parts_size(dp))
+        return fail(DCS_E_WORKSPACE, "conv_dgrad_reflect_win_inbwd: parts buffer too small");
+    hipStream_t s = as_stream(stream);
+    const int tiles = d.Hs * d.Ws / 256;
+    const int nch = tiles + IBW_FOLD_CHUNKS;
+    const IbwArgs ib{y, scale, shift, reinterpret_cast<Sum2*>(parts), act, nch};
+    int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, nullptr, dx, nullptr, s, nullptr, nullptr, &ib);
+    if (e) return e;
+    if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
+    *nchunk = nch;
+    return reflect_ring_fold_ibw(ring, dx, d.N, d.Hs, d.Ws, d.Co, ring_ksplit(d), y, scale, shift, act,
+                                 reinterpret_cast<Sum2*>(parts), nch, tiles, IBW_FOLD_CHUNKS, s);
 }

@@ -305,9 +305,6 @@ __global__ __launch_bounds__(256) void in_apply_pow2_kernel(const float4* __rest
 }
 
 // ---- backward of a = act(IN(y)) -------------------------------------------------------
-struct Sum2 {
-    float a, b;
-};
 
 __global__ __launch_bounds__(256) void in_bwd_partial_kernel(const float* __restrict__ da, const float* __restrict__ y,
                                                              const float* __restrict__ sc, const float* __restrict__ sh,
@@ -576,6 +573,49 @@ extern "C" int dcs_in_apply(const float* x, const float* scale, const float* shi
     return check_launch("in_apply");
 }
 
+namespace {
+// finalize (partial sums -> per-(image, channel) coefficients) + apply of the IN backward
+int in_bwd_finish(const float* da, const float* y, const float* scale, const float* shift, float* dy, int N, int HW,
+                  int C, int act, const Sum2* parts, int nchunk, Sum2* coef, float* rng, bool v4, hipStream_t s) {
+    hipLaunchKernelGGL(in_bwd_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts, N,
+                       C, nchunk, HW, coef);
+    int e = check_launch("in_bwd_finalize");
+    if (e) return e;
+    if ((e = range_zero(rng, s))) return e;
+    const float4* da4 = reinterpret_cast<const float4*>(da);
+    const float4* y4 = reinterpret_cast<const float4*>(y);
+    long long total = (long long)N * HW * C;
+    const bool pow2 = v4 && (C & (C - 1)) == 0 && (long long)HW * C / 4 < (1ll << 30);
+    if (pow2) {
+        const int per_n4 = (int)((long long)HW * C / 4);
+        dim3 g((unsigned)cdiv(per_n4, 1024), (unsigned)N);
+        float4* dy4 = reinterpret_cast<float4*>(dy);
+        if (act == DCS_ACT_RELU)
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
+        else if (act == DCS_ACT_LRELU)
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
+        else
+            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
+    } else {
+        hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
+                           coef, dy, total, HW, C, act, rng);
+    }
+    return check_launch("in_bwd_apply");
+}
+}  // namespace
+
+extern "C" int dcs_in_act_backward_parts(const float* da, const float* y, const float* scale, const float* shift,
+                                         float* dy, int N, int HW, int C, int act, const void* parts, int nchunk,
+                                         void* ws, size_t ws_bytes, float* rng, void* stream) {
+    if (!da || !y || !scale || !shift || !dy || !parts || !ws || N <= 0 || HW <= 0 || C <= 0 || nchunk <= 0)
+        return fail(DCS_E_INVALID, "in_act_backward_parts: bad arguments");
+    if (ws_bytes < (size_t)N * C * sizeof(Sum2)) return fail(DCS_E_WORKSPACE, "in_act_backward_parts: workspace too small");
+    const bool v4 = v4_ok(C, da) && v4_ok(C, y) && v4_ok(C, dy) && v4_ok(C, scale) && v4_ok(C, shift) &&
+                    (act == DCS_ACT_RELU || act == DCS_ACT_LRELU || act == DCS_ACT_AFFINE);
+    return in_bwd_finish(da, y, scale, shift, dy, N, HW, C, act, reinterpret_cast<const Sum2*>(parts), nchunk,
+                         reinterpret_cast<Sum2*>(ws), rng, v4, as_stream(stream));
+}
+
 extern "C" int dcs_in_act_backward(const float* da, const float* y, const float* scale, const float* shift, float* dy,
                                    int N, int HW, int C, int act, void* ws, size_t ws_bytes, float* rng, void* stream) {
     if (!da || !y || !scale || !shift || !dy || !ws || N <= 0 || HW <= 0 || C <= 0)
@@ -605,26 +645,5 @@ extern "C" int dcs_in_act_backward(const float* da, const float* y, const float*
     }
     int e = check_launch("in_bwd_partial");
     if (e) return e;
-    hipLaunchKernelGGL(in_bwd_finalize8_kernel, dim3((unsigned)cdiv((long long)N * C, 32)), dim3(256), 0, s, parts, N,
-                       C, nchunk, HW, coef);
-    e = check_launch("in_bwd_finalize");
-    if (e) return e;
-    if ((e = range_zero(rng, s))) return e;
-    long long total = (long long)N * HW * C;
-    const bool pow2 = v4 && (C & (C - 1)) == 0 && (long long)HW * C / 4 < (1ll << 30);
-    if (pow2) {
-        const int per_n4 = (int)((long long)HW * C / 4);
-        dim3 g((unsigned)cdiv(per_n4, 1024), (unsigned)N);
-        float4* dy4 = reinterpret_cast<float4*>(dy);
-        if (act == DCS_ACT_RELU)
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_RELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
-        else if (act == DCS_ACT_LRELU)
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_LRELU>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
-        else
-            hipLaunchKernelGGL(in_bwd_apply_pow2_kernel<DCS_ACT_AFFINE>, g, dim3(256), 0, s, da4, y4, scale, shift, coef, dy4, per_n4, C - 1, rng);
-    } else {
-        hipLaunchKernelGGL(in_bwd_apply_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, da, y, scale, shift,
-                           coef, dy, total, HW, C, act, rng);
-    }
-    return check_launch("in_bwd_apply");
+    return in_bwd_finish(da, y, scale, shift, dy, N, HW, C, act, parts, nchunk, coef, rng, v4, s);
 }

@@ -56,6 +56,8 @@ SIGNATURES = {
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_conv3_win_in_stats_pro": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_conv_dgrad_reflect_win": (c_int, [DP, P, P, P, P, P, P, P, P, P]),
+    "dcs_conv_dgrad_reflect_win_inbwd_parts_size": (c_size_t, [DP]),
+    "dcs_conv_dgrad_reflect_win_inbwd": (c_int, [DP, P, P, P, P, P, P, P, P, P, P, c_int, P, c_size_t, P, P]),
     "dcs_conv_rows": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_rows_in_stats_parts_size": (c_size_t, [DP]),
     "dcs_conv_rows_in_stats": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, P, P]),
@@ -75,6 +77,7 @@ SIGNATURES = {
     "dcs_in_stats": (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P, P, c_size_t, P]),
     "dcs_in_apply": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P]),
     "dcs_in_act_backward": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_size_t, P, P]),
+    "dcs_in_act_backward_parts": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, c_size_t, P, P]),
     "dcs_conv_rows_narrow": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_conv_wgrad_narrow_workspace_size": (c_size_t, [DP]),
     "dcs_conv_wgrad_narrow": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),

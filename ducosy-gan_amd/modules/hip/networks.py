@@ -69,6 +69,54 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
 _FUSE_PRO = os.environ.get("DUCOSY_FUSE_PRO", "0") == "1"
 
 
+# the InstanceNorm backward's partial sums of each residual block's first IN fused into the data
+# gradient that produces its input gradient (window path); "0" = separate partial-sum pass (A/B)
+_FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
+
+# parameter gradients written in place into freshly zeroed .grad buffers; "0" = always through autograd (A/B)
+_GRAD_SINK = os.environ.get("DUCOSY_GRAD_SINK", "1") == "1"
+
+
+class _GradSink:
+    """Parameter gradients of one backward pass.  A parameter whose ``.grad`` the fused optimizer has
+    just zeroed (modules/optim.py FusedAdam.zero_grad marks it ``_dcs_fresh``) receives its gradient
+    in place: the producing kernel writes straight into ``.grad`` and autograd gets None, so there is
+    no AccumulateGrad add and no zero fill.  Any other parameter gets its gradient back through
+    autograd as usual (the second batched G_A2B call of a step, plain ``.backward()`` without the
+    fused optimizer: same values, same ``.grad`` contents as accumulation gives)."""
+
+    def __init__(self, params):
+        self.params = params or {}
+        self.out = {}
+
+    def dest(self, k, view=None) -> Optional[torch.Tensor]:
+        p = self.params.get(k)
+        g = None if (p is None or not _GRAD_SINK) else p.grad
+        if g is None or not getattr(p, "_dcs_fresh", False) or not g.is_contiguous() or g.dtype != torch.float32:
+            return None
+        p._dcs_fresh = False
+        return g if view is None else g.view(view)
+
+    def put(self, k, fn, view=None):
+        d = self.dest(k, view)
+        r = fn(d)
+        self.out[k] = None if d is not None else r
+
+    def zero(self, k, like, device=None):
+        """A bias an InstanceNorm follows: exact zero gradient (nothing to add to an existing .grad).
+        ``like``: a tensor of the bias' shape, or the shape (with ``device``)."""
+        p = self.params.get(k)
+        if p is not None and p.grad is not None:
+            self.out[k] = None
+        elif torch.is_tensor(like):
+            self.out[k] = torch.zeros_like(like)
+        else:
+            self.out[k] = torch.zeros(like, device=device, dtype=torch.float32)
+
+    def get(self, k):
+        return self.out.get(k)
+
+
 class _Block:
     __slots__ = ("x", "y1", "s1", "a1", "pro1", "y2", "s2", "cb")
 
@@ -105,23 +153,32 @@ def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
     res = L["res"]
     if use_cbam:
         w1, w2, wsa = W[f"r{b}.fc1"], W[f"r{b}.fc2"], W[f"r{b}.sa"]
-        dy2, dw1, dw2, dwsa = ops.cbam_backward(
-            dout, blk.y2, blk.s2, w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1),
-            wsa.reshape(2, wsa.shape[-2], wsa.shape[-1]), blk.cb)
-        grads[f"r{b}.fc1"] = dw1.view_as(w1)
-        grads[f"r{b}.fc2"] = dw2.view_as(w2)
-        grads[f"r{b}.sa"] = dwsa.view_as(wsa)
+        k1, k2, k3 = f"r{b}.fc1", f"r{b}.fc2", f"r{b}.sa"
+        w1m, w2m, wsam = (w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1),
+                          wsa.reshape(2, wsa.shape[-2], wsa.shape[-1]))
+        o = (grads.dest(k1, w1m.shape), grads.dest(k2, w2m.shape), grads.dest(k3, wsam.shape))
+        dy2, dw1, dw2, dwsa = ops.cbam_backward(dout, blk.y2, blk.s2, w1m, w2m, wsam, blk.cb, out_dw=o)
+        grads.out[k1] = None if o[0] is not None else dw1.view_as(w1)
+        grads.out[k2] = None if o[1] is not None else dw2.view_as(w2)
+        grads.out[k3] = None if o[2] is not None else dwsa.view_as(wsa)
     else:
         dy2 = ops.in_act_backward(dout, blk.y2, blk.s2, ACT_AFFINE)
     H, Wd = blk.x.shape[1], blk.x.shape[2]
     if blk.a1 is None:  # IN + ReLU applied in the window staging
-        grads[f"r{b}.c2.w"] = res.wgrad(dy2, Src.nhwc(blk.y1), pro=blk.pro1)
+        grads.put(f"r{b}.c2.w", lambda o: res.wgrad(dy2, Src.nhwc(blk.y1), pro=blk.pro1, out=o))
     else:
-        grads[f"r{b}.c2.w"] = res.wgrad(dy2, Src.nhwc(blk.a1))
-    da1 = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd)
-    dy1 = ops.in_act_backward(da1, blk.y1, blk.s1, ACT_RELU)
+        grads.put(f"r{b}.c2.w", lambda o: res.wgrad(dy2, Src.nhwc(blk.a1), out=o))
+    if _FUSE_IBW:  # IN1's backward partial sums from the data gradient's epilogue (window path)
+        da1, parts, nch = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd, inbwd=(blk.y1, blk.s1, ACT_RELU))
+        if parts is not None:
+            dy1 = ops.in_act_backward_parts(da1, blk.y1, blk.s1, ACT_RELU, parts, nch)
+        else:
+            dy1 = ops.in_act_backward(da1, blk.y1, blk.s1, ACT_RELU)
+    else:
+        da1 = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd)
+        dy1 = ops.in_act_backward(da1, blk.y1, blk.s1, ACT_RELU)
     del da1
-    grads[f"r{b}.c1.w"] = res.wgrad(dy1, Src.nhwc(blk.x))
+    grads.put(f"r{b}.c1.w", lambda o: res.wgrad(dy1, Src.nhwc(blk.x), out=o))
     # residual: dx = dout + dgrad(conv1)
     return res.dgrad(dy1, res.pack_dgrad(W[f"r{b}.c1.w"]), H, Wd, addend=dout)
 
@@ -170,28 +227,31 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     return out, saved
 
 
-def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, dx_from: int = 0):
-    """Returns (dx NHWC [N,H,W,dx_channels] or None, grads dict keyed like gen_param_names).
+def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, dx_from: int = 0,
+                       params: Optional[Dict[str, torch.Tensor]] = None):
+    """Returns (dx NHWC [N,H,W,dx_channels] or None, _GradSink keyed like gen_param_names: .get(k)
+    is the gradient to hand to autograd, None where it went into the parameter's .grad in place).
     dx is computed for samples dx_from.. only (zero before)."""
     L, W = S["L"], S["W"]
     nb, use_cbam = S["nb"], S["use_cbam"]
-    grads: Dict[str, torch.Tensor] = {}
+    grads = _GradSink(params)
     N, _, H, Wd = dout.shape
     dout = dout.contiguous()
     # head: tanh backward, bias, wgrad, dgrad
     dpre = ops.act_backward(dout, S["out"], ACT_TANH).view(N, H, Wd, 1)
-    grads["head.b"] = ops.channel_sum(dpre)
+    grads.put("head.b", lambda o: ops.channel_sum(dpre, out=o))
     su2, su1 = S["su2"], S["su1"]
-    grads["head.w"] = L["head"].wgrad(dpre, Src.nhwc(S["yu2"]), pro=(su2.scale, su2.shift, ACT_RELU))
+    grads.put("head.w", lambda o: L["head"].wgrad(dpre, Src.nhwc(S["yu2"]), pro=(su2.scale, su2.shift, ACT_RELU),
+                                                   out=o))
     da = L["head"].dgrad(dpre, L["head"].pack_dgrad(W["head.w"]), H, Wd)
     del dpre
     # up2
     dy = ops.in_act_backward(da, S["yu2"], su2, ACT_RELU)
-    grads["up2.w"] = L["up2"].wgrad(dy, Src.nhwc(S["au1"]))
+    grads.put("up2.w", lambda o: L["up2"].wgrad(dy, Src.nhwc(S["au1"]), out=o))
     da = L["up2"].dgrad(dy, L["up2"].pack_dgrad(W["up2.w"]), H // 2, Wd // 2)
     # up1
     dy = ops.in_act_backward(da, S["yu1"], su1, ACT_RELU)
-    grads["up1.w"] = L["up1"].wgrad(dy, Src.nhwc(S["h"]))
+    grads.put("up1.w", lambda o: L["up1"].wgrad(dy, Src.nhwc(S["h"]), out=o))
     dh = L["up1"].dgrad(dy, L["up1"].pack_dgrad(W["up1.w"]), H // 4, Wd // 4)
     del dy, da
     # residual blocks
@@ -201,14 +261,14 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     # x0 = relu(IN(y2))
     s2, s1, s0 = S["s2"], S["s1"], S["s0"]
     dy = ops.in_act_backward(dh, S["y2"], s2, ACT_RELU)
-    grads["down2.w"] = L["down2"].wgrad(dy, Src.nhwc(S["a1"]))
+    grads.put("down2.w", lambda o: L["down2"].wgrad(dy, Src.nhwc(S["a1"]), out=o))
     da = L["down2"].dgrad(dy, L["down2"].pack_dgrad(W["down2.w"]), H // 2, Wd // 2)
     dy = ops.in_act_backward(da, S["y1"], s1, ACT_RELU)
-    grads["down1.w"] = L["down1"].wgrad(dy, Src.nhwc(S["a0"]))
+    grads.put("down1.w", lambda o: L["down1"].wgrad(dy, Src.nhwc(S["a0"]), out=o))
     da = L["down1"].dgrad(dy, L["down1"].pack_dgrad(W["down1.w"]), H, Wd)
     dy = ops.in_act_backward(da, S["y0"], s0, ACT_RELU)
     del da
-    grads["stem.w"] = L["stem"].wgrad(dy, S["xs"])
+    grads.put("stem.w", lambda o: L["stem"].wgrad(dy, S["xs"], out=o))
     dx = None
     if need_dx:
         stem = L["stem"]
@@ -221,10 +281,10 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
             dx = stem.dgrad(dy, wd, H, Wd, ci_count=dx_channels)
     # biases feeding an InstanceNorm: exact zero gradient
     for key in ("stem.b", "down1.b", "down2.b", "up1.b", "up2.b"):
-        grads[key] = torch.zeros_like(W[key])
+        grads.zero(key, W[key])
     for b in range(nb):
-        grads[f"r{b}.c1.b"] = torch.zeros_like(W[f"r{b}.c1.b"])
-        grads[f"r{b}.c2.b"] = torch.zeros_like(W[f"r{b}.c2.b"])
+        grads.zero(f"r{b}.c1.b", W[f"r{b}.c1.b"])
+        grads.zero(f"r{b}.c2.b", W[f"r{b}.c2.b"])
     return dx, grads
 
 
@@ -241,6 +301,8 @@ class GeneratorFunction(torch.autograd.Function):
         ctx.saved = saved
         if keep:
             ctx.save_for_backward(out)  # tanh backward needs the output (no ctx attribute cycle)
+            # the parameters themselves: freshly zeroed .grad buffers take their gradients in place
+            ctx.params = {k: p for i, (k, p) in enumerate(zip(keys, params)) if ctx.needs_input_grad[3 + i]}
         ctx.keys = keys
         ctx.x_channels = x.shape[1]
         return out
@@ -250,14 +312,15 @@ class GeneratorFunction(torch.autograd.Function):
         S = ctx.saved
         S["out"] = ctx.saved_tensors[0]
         need_dx = ctx.needs_input_grad[0]
-        dx_nhwc, grads = generator_backward(S, dout, need_dx, ctx.x_channels, ctx.dx_from)
+        dx_nhwc, grads = generator_backward(S, dout, need_dx, ctx.x_channels, ctx.dx_from, ctx.params)
         ctx.saved = None
+        ctx.params = None
         dx = None
         if need_dx:
             dx = dx_nhwc.permute(0, 3, 1, 2)
             if ctx.x_channels > 1:
                 dx = dx.contiguous()
-        dparams = [grads[k] if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(ctx.keys)]
+        dparams = [grads.get(k) if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(ctx.keys)]
         return (dx, None, None, *dparams)
 
 
@@ -303,28 +366,29 @@ def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: boo
     return out, saved
 
 
-def discriminator_backward(S, dout, need_dx, need_w):
+def discriminator_backward(S, dout, need_dx, need_w, params=None):
+    """Returns (dx or None, _GradSink keyed 0..9 in DISC_KEYS order)."""
     L, ws, ys, sts = S["L"], S["ws"], S["ys"], S["sts"]
     N, _, H4, W4 = dout.shape
     d = dout.contiguous().view(N, H4, W4, 1)
-    grads = [None] * 10
+    grads = _GradSink(params)
     if need_w:
-        grads[9] = ops.channel_sum(d)
+        grads.put(9, lambda o: ops.channel_sum(d, out=o))
         st = sts[3]
-        grads[8] = L[4].wgrad(d, Src.nhwc(ys[3]), pro=(st.scale, st.shift, ACT_LRELU))
+        grads.put(8, lambda o: L[4].wgrad(d, Src.nhwc(ys[3]), pro=(st.scale, st.shift, ACT_LRELU), out=o))
     da = L[4].dgrad(d, L[4].pack_dgrad(ws[4]), ys[3].shape[1], ys[3].shape[2])
     for i in (3, 2, 1):
         dy = ops.in_act_backward(da, ys[i], sts[i], ACT_LRELU)
         if need_w:
             st = sts[i - 1]
-            grads[2 * i] = L[i].wgrad(dy, Src.nhwc(ys[i - 1]), pro=(st.scale, st.shift, ACT_LRELU))
-            grads[2 * i + 1] = torch.zeros(L[i].cout, device=d.device, dtype=torch.float32)
+            grads.put(2 * i, lambda o: L[i].wgrad(dy, Src.nhwc(ys[i - 1]), pro=(st.scale, st.shift, ACT_LRELU), out=o))
+            grads.zero(2 * i + 1, (L[i].cout,), d.device)
         da = L[i].dgrad(dy, L[i].pack_dgrad(ws[i]), ys[i - 1].shape[1], ys[i - 1].shape[2])
     # layer 0: y0 includes the bias; a0 = lrelu(y0)
     dy0 = ops.act_backward(da, ys[0], ACT_LRELU)
     if need_w:
-        grads[1] = ops.channel_sum(dy0)
-        grads[0] = L[0].wgrad(dy0, S["xs"])
+        grads.put(1, lambda o: ops.channel_sum(dy0, out=o))
+        grads.put(0, lambda o: L[0].wgrad(dy0, S["xs"], out=o))
     dx = None
     if need_dx:
         xs = S["xs"]
@@ -338,19 +402,21 @@ class DiscriminatorFunction(torch.autograd.Function):
         keep = any(ctx.needs_input_grad)
         out, saved = discriminator_forward(list(params), x, keep)
         ctx.saved = saved
+        ctx.params = {i: p for i, p in enumerate(params) if ctx.needs_input_grad[1 + i]} if keep else None
         return out
 
     @staticmethod
     def backward(ctx, dout):
         need_dx = ctx.needs_input_grad[0]
         need_w = any(ctx.needs_input_grad[1:])
-        dx, grads = discriminator_backward(ctx.saved, dout, need_dx, need_w)
+        dx, grads = discriminator_backward(ctx.saved, dout, need_dx, need_w, ctx.params)
         ctx.saved = None
+        ctx.params = None
         if dx is not None:
             dx = dx.permute(0, 3, 1, 2)
             if dx.shape[1] > 1:
                 dx = dx.contiguous()
-        return (dx, *[g if ctx.needs_input_grad[1 + i] else None for i, g in enumerate(grads)])
+        return (dx, *[grads.get(i) if ctx.needs_input_grad[1 + i] else None for i in range(10)])
 
 
 class ResBlockFunction(torch.autograd.Function):
@@ -370,10 +436,10 @@ class ResBlockFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         L, W, blk, use_cbam, keys = ctx.state
-        grads = {}
+        grads = _GradSink(None)
         dx = _res_block_backward(L, W, 0, blk, dout.permute(0, 2, 3, 1).contiguous(), use_cbam, grads)
-        grads["r0.c1.b"] = torch.zeros_like(W["r0.c1.b"])
-        grads["r0.c2.b"] = torch.zeros_like(W["r0.c2.b"])
+        grads.zero("r0.c1.b", W["r0.c1.b"])
+        grads.zero("r0.c2.b", W["r0.c2.b"])
         ctx.state = None
         return (dx.permute(0, 3, 1, 2).contiguous(), None, None,
-                *[grads[k] if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(keys)])
+                *[grads.get(k) if ctx.needs_input_grad[3 + i] else None for i, k in enumerate(keys)])

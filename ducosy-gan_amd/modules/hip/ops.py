@@ -497,8 +497,16 @@ class ConvGeom:
 
     # ---- data gradient ---------------------------------------------------------------
     def dgrad(self, dy: torch.Tensor, wpack_d: torch.Tensor, H: int, W: int,
-              ci_count: Optional[int] = None, addend: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """dL/d(input) [N,H,W,ci] (NHWC) of this conv given dy [N,Ho,Wo,cout] (NHWC)."""
+              ci_count: Optional[int] = None, addend: Optional[torch.Tensor] = None, inbwd=None):
+        """dL/d(input) [N,H,W,ci] (NHWC) of this conv given dy [N,Ho,Wo,cout] (NHWC).  ``inbwd`` = (y,
+        INStats, act) of the layer a = act(IN(y)) whose input gradient this is: where the window path
+        applies, its partial sums are fused (dcs_conv_dgrad_reflect_win_inbwd) and the call returns
+        (dx, parts, nchunk) for in_act_backward_parts, else (dx, None, 0)."""
+        if inbwd is not None:
+            r = self._dgrad_inbwd(dy, wpack_d, H, W, inbwd)
+            if r is not None:
+                return r
+            return self.dgrad(dy, wpack_d, H, W, ci_count, addend), None, 0
         _check_dev(dy, wpack_d, addend)
         N, Ho, Wo, Co = dy.shape
         assert Co == self.cout
@@ -608,6 +616,44 @@ class ConvGeom:
             lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
         return out
 
+    def _dgrad_inbwd(self, dy, wpack_d, H, W, inbwd):
+        h3 = getattr(wpack_d, "_dcs_h3", None)
+        if h3 is None or not dy.is_contiguous() or self.pad_mode != DCS_PAD_REFLECT or self.pads != (1, 1, 1, 1):
+            return None
+        N, Ho, Wo, Co = dy.shape
+        d = lib.ConvDesc()
+        d.N, d.Hs, d.Ws, d.Cs = N, Ho, Wo, Co
+        d.s_n, d.s_c, d.s_h, d.s_w = Ho * Wo * Co, 1, Wo * Co, Co
+        d.csplit = Co
+        d.up, d.pad_mode = 1, DCS_PAD_ZERO
+        d.KH = d.KW = self.k
+        d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
+        d.mma = _fallback() if _h3() else _MMA
+        _set_mma(d, dy, None, _wrng(wpack_d))
+        d.korder = lib.KORDER_SLICE if self.kslice else lib.KORDER_TAP
+        d.Co = self.cin
+        d.stride, d.parity = 1, 0
+        d.pt = d.pl = self.k - 1
+        d.Ho, d.Wo = H + 2, W + 2
+        if not lib.query("dcs_conv3_win_ok", ctypes.byref(d), 1):
+            return None
+        nb = lib.query("dcs_conv_dgrad_reflect_win_inbwd_parts_size", ctypes.byref(d))
+        if nb == 0:
+            return None
+        y, st, act = inbwd
+        dev = dy.device
+        out = torch.empty(N, H, W, self.cin, device=dev, dtype=torch.float32)
+        ring = torch.empty(lib.query("dcs_conv_dgrad_reflect_ring_size", ctypes.byref(d)) // 4, device=dev,
+                           dtype=torch.float32)
+        parts = torch.empty(nb // 4, device=dev, dtype=torch.float32)
+        nchunk = ctypes.c_int(0)
+        e0 = PROBE.begin() if _is_res_geom(self) else None
+        lib.call("dcs_conv_dgrad_reflect_win_inbwd", ctypes.byref(d), _p(dy), _p(wpack_d), _p(h3[0]), _p(h3[1]),
+                 _p(h3[2]), _p(out), _p(ring), _p(y), _p(st.scale), _p(st.shift), act, _p(parts), nb,
+                 ctypes.byref(nchunk), _stream())
+        PROBE.end(e0, 2.0 * N * H * W * self.cout * self.cin * self.k * self.k)
+        return out, parts, nchunk.value
+
     # ---- weight gradient ---------------------------------------------------------------
     def wgrad(self, dy: torch.Tensor, s: Src,
               pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
@@ -694,16 +740,29 @@ def in_act_backward(da: torch.Tensor, y: torch.Tensor, st: INStats, act: int) ->
     return dy
 
 
+def in_act_backward_parts(da: torch.Tensor, y: torch.Tensor, st: INStats, act: int, parts: torch.Tensor,
+                          nchunk: int) -> torch.Tensor:
+    """in_act_backward with the partial sums its producer wrote (ConvGeom.dgrad(..., inbwd=...))."""
+    N, H, W, C = y.shape
+    dy = torch.empty_like(y)
+    ws = workspace(N * C * 8, y.device)
+    lib.call("dcs_in_act_backward_parts", _p(da), _p(y), _p(st.scale), _p(st.shift), _p(dy), N, H * W, C, act,
+             _p(parts), nchunk, _p(ws), ws.numel(), _out_rng(dy), _stream())
+    return dy
+
+
 def act_backward(da: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
     out = torch.empty_like(y)
     lib.call("dcs_act_backward", _p(da.contiguous()), _p(y), _p(out), y.numel(), act, _out_rng(out), _stream())
     return out
 
 
-def channel_sum(x: torch.Tensor) -> torch.Tensor:
+def channel_sum(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     C = x.shape[-1]
     Pn = x.numel() // C
-    out = torch.empty(C, device=x.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty(C, device=x.device, dtype=torch.float32)
+    assert out.numel() == C and out.is_contiguous()
     ws = workspace(lib.query("dcs_channel_sum_workspace_size", Pn, C), x.device)
     lib.call("dcs_channel_sum", _p(x), Pn, C, _p(out), _p(ws), ws.numel(), _stream())
     return out
@@ -741,15 +800,18 @@ def cbam_forward(x, y, st: INStats, w1, w2, wsa):
     return out, (ca, sin_, sarg, sa)
 
 
-def cbam_backward(dout, y, st: INStats, w1, w2, wsa, saved):
+def cbam_backward(dout, y, st: INStats, w1, w2, wsa, saved, out_dw=(None, None, None)):
+    """``out_dw``: optional destinations of (dw1, dw2, dwsa) shaped like w1 / w2 / wsa."""
     ca, sin_, sarg, sa = saved
     N, H, W, C = y.shape
     Cr = w1.shape[0]
     ksa = wsa.shape[-1]
     dy = torch.empty_like(y)
-    dw1 = torch.empty_like(w1)
-    dw2 = torch.empty_like(w2)
-    dwsa = torch.empty_like(wsa)
+    dw1 = torch.empty_like(w1) if out_dw[0] is None else out_dw[0]
+    dw2 = torch.empty_like(w2) if out_dw[1] is None else out_dw[1]
+    dwsa = torch.empty_like(wsa) if out_dw[2] is None else out_dw[2]
+    for o, ref in ((dw1, w1), (dw2, w2), (dwsa, wsa)):
+        assert o.shape == ref.shape and o.is_contiguous()
     nb = lib.query("dcs_cbam_backward_workspace_size", N, H, W, C, Cr, ksa)
     ws = workspace(nb, y.device)
     lib.call("dcs_cbam_backward", _p(dout), _p(y), _p(st.scale), _p(st.shift), _p(st.xmax),

@@ -44,8 +44,12 @@ class FusedAdam(torch.optim.Optimizer):
         self._t = 0
 
     def zero_grad(self, set_to_none: bool = True):
-        """Zero the flat gradient buffer (the per-parameter grads stay views of it)."""
+        """Zero the flat gradient buffer (the per-parameter grads stay views of it).  Each parameter is
+        marked fresh: the fused networks' backward (modules/hip/networks.py _GradSink) then writes its
+        first gradient straight into the zeroed .grad instead of handing it to AccumulateGrad."""
         self.flat_g.zero_()
+        for p in self.param_groups[0]["params"]:
+            p._dcs_fresh = True
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -205,6 +205,18 @@ int dcs_conv3_win_in_stats_pro(const dcs_conv_desc* d, const float* src, const f
 int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* d, const float* dy, const float* wpack, const void* w_hi,
                                const void* w_lo, const int* wexp, const float* addend, float* dx, float* ring,
                                void* stream);
+/* The same data gradient dx = da of a layer a = act(InstanceNorm(y)) (the first conv of a residual
+ * block, modules/model.py:74-76), with the InstanceNorm backward's partial sums fused: the window
+ * epilogue sums g = da * act'(xhat) and g * xhat (xhat = y * scale + shift) per (256-pixel tile,
+ * channel) over the pixels the ring fold does not touch, and the fold sums its pixels with their final
+ * values, into parts (Sum2 {float a, b} [N][*nchunk][Co], dcs_conv_dgrad_reflect_win_inbwd_parts_size
+ * bytes) for dcs_in_act_backward_parts.  No addend; act DCS_ACT_AFFINE / _RELU / _LRELU; Co / 4
+ * divides 256. */
+size_t dcs_conv_dgrad_reflect_win_inbwd_parts_size(const dcs_conv_desc* d);
+int dcs_conv_dgrad_reflect_win_inbwd(const dcs_conv_desc* d, const float* dy, const float* wpack, const void* w_hi,
+                                     const void* w_lo, const int* wexp, float* dx, float* ring, const float* y,
+                                     const float* scale, const float* shift, int act, void* parts, size_t parts_bytes,
+                                     int* nchunk, void* stream);
 
 /* Forward / data-gradient pass: out = gather(src) x B (+ bias, epilogue act). */
 int dcs_conv_rows(const dcs_conv_desc* d, const float* src, const float* src2, const float* wpack,
@@ -306,6 +318,11 @@ int dcs_in_act_backward(const float* da, const float* y, const float* scale, con
                         float* dy, int N, int HW, int C, int act, void* ws, size_t ws_bytes,
                         float* rng,
                         void* stream);
+/* The same, its partial sums written by the producer of da (parts [N][nchunk][C] Sum2 records,
+ * dcs_conv_dgrad_reflect_win_inbwd): merged per (n,c) in a fixed order, then applied.  ws: N*C*8 bytes. */
+int dcs_in_act_backward_parts(const float* da, const float* y, const float* scale, const float* shift, float* dy,
+                              int N, int HW, int C, int act, const void* parts, int nchunk, void* ws,
+                              size_t ws_bytes, float* rng, void* stream);
 
 /* ---- narrow-output convolutions (Co <= 4: Generator head, PatchGAN last layer, and the
  *      input-image gradients of the stem and the first PatchGAN layer) ---- */

@@ -196,3 +196,33 @@ def test_win_prologue_vs_fp64(ops, N, H, W):
     Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dw = g.wgrad(Rd, ops.Src.nhwc(yd), pro=pro)
     assert _relmax(dw, w.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128)])
+def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
+    """The InstanceNorm backward of a = relu(IN(y)) with its partial sums fused into the window data
+    gradient that produces da (dcs_conv_dgrad_reflect_win_inbwd: tile epilogue + ring fold) against the
+    separate partial-sum pass on the same da (dcs_in_act_backward): dx bit-identical (same kernels),
+    dy within 1e-5 of max |dy| (the sums run in a different order), and against float64."""
+    from modules.hip.lib import ACT_RELU
+    ops.set_mma("f16x3")
+    g = _geom(ops)
+    y = rnd((N, 256, H, W), 111, "y").float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    st = ops.in_stats(y)
+    w = torch.from_numpy(prng.normal(112, "w", (256, 256, 3, 3), 0, 0.05)).float().to(DEV)
+    R = torch.from_numpy(prng.normal(113, "R", (N, 256, H, W))).float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wd = g.pack_dgrad(w)
+    da_f, parts, nch = g.dgrad(R, wd, H, W, inbwd=(y, st, ACT_RELU))
+    assert parts is not None and nch == H * W // 256 + 16
+    dy_f = ops.in_act_backward_parts(da_f, y, st, ACT_RELU, parts, nch)
+    da_s = g.dgrad(R, wd, H, W)
+    assert torch.equal(da_f, da_s)
+    dy_s = ops.in_act_backward(da_s, y, st, ACT_RELU)
+    assert _relmax(dy_f, dy_s.double().cpu()) <= 1e-5
+    # float64 IN backward of the same da
+    yd = y.double().cpu().requires_grad_(True)
+    m = yd.mean(dim=(1, 2), keepdim=True)
+    v = yd.var(dim=(1, 2), unbiased=False, keepdim=True)
+    a = torch.relu((yd - m) / torch.sqrt(v + 1e-5))
+    (a * da_s.double().cpu()).sum().backward()
+    assert _relmax(dy_f, yd.grad) <= 1e-4
