@@ -253,6 +253,30 @@ class Src:
 
 BN_MAX = 128
 
+# Packed-weight cache: a pack is reused while its weight tensor is unchanged -- same autograd version
+# and storage (in-place torch ops, load_state_dict, broadcasts bump the version; a .data reassignment
+# changes the storage) and same weights epoch (the fused Adam
+# kernel writes parameters behind the version counter and bumps the epoch, modules/optim.py).  Within a
+# step the second batched G_A2B call and the G-step / D-step Discriminator calls reuse the packs.
+_EPOCH = [0]
+
+
+def bump_weights_epoch() -> None:
+    _EPOCH[0] += 1
+
+
+def _cached_pack(w: torch.Tensor, key, make):
+    stamp = (w.data_ptr(), w._version, _EPOCH[0], _MMA, _WIN, _KSLICE)
+    c = getattr(w, "_dcs_packs", None)
+    if c is None or c[0] != stamp:
+        c = (stamp, {})
+        w._dcs_packs = c
+    pk = c[1].get(key)
+    if pk is None:
+        pk = make()
+        c[1][key] = pk
+    return pk
+
 
 def _wrng(wpack: torch.Tensor) -> Optional[torch.Tensor]:
     """Range record a packed weight tensor carries (dcs_pack_weights_r), None if packed without."""
@@ -326,7 +350,18 @@ class ConvGeom:
         wpack._dcs_h3 = (hi, lo, wexp)
         return wpack
 
+    def _key(self):
+        return (self.cin, self.cout, self.k, self.stride, self.pads, self.pad_mode, self.up)
+
     def pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
+        """B operand of the forward GEMM (cached per weight version, _cached_pack)."""
+        return _cached_pack(w, ("fwd", self._key(), cin_pad), lambda: self._pack_fwd(w, cin_pad))
+
+    def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
+        """B operand of the data-gradient GEMM (cached per weight version, _cached_pack)."""
+        return _cached_pack(w, ("dgrad", self._key(), ci_count), lambda: self._pack_dgrad(w, ci_count))
+
+    def _pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
         """B operand of the forward GEMM: N-major [Np][Kpad] for the MFMA rows pass (ldb =
         Kpad), K-major [K][1|4] for the narrow kernels (ldb = columns).  ``cin_pad``: the
         source carries that many channels (zero-padded beyond cin; the 4-channel stem)."""
@@ -354,7 +389,7 @@ class ConvGeom:
         return (ci == 1 and self.cout == 64 and self.up == 1 and (self.k, self.stride) in ((7, 1), (4, 2))
                 and (self.pad_mode == DCS_PAD_ZERO or (t == b and l == r)))
 
-    def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
+    def _pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
         ci = self.cin if ci_count is None else ci_count
         if self.c1_dgrad and ci == self.cin:  # forward K-major weights: [(ty*K+tx)*cin + c]
             return self._pack(w, 0, self.cin, self.k * self.k * self.cin, 1)

@@ -137,3 +137,28 @@ def test_train_step_mma_modes_vs_reference_golden(mode, tol0):
                 assert abs(v - float(z[k][i])) <= tol * max(scale, 1e-2), (mode, i, k, v, float(z[k][i]))
     finally:
         ops.set_mma(prev)
+
+
+def test_pack_cache_follows_weight_updates():
+    """Packed weights are reused while the weight is unchanged (same version, storage and weights epoch)
+    and rebuilt after an in-place torch update, a .data reassignment and a fused Adam step (which writes
+    the parameters through a kernel and bumps the epoch)."""
+    from modules.hip import ops
+    from modules.hip.lib import DCS_PAD_REFLECT
+    from modules.optim import FusedAdam
+    g = ops.ConvGeom(256, 256, 3, 1, (1, 1, 1, 1), DCS_PAD_REFLECT)
+    w = torch.nn.Parameter(torch.randn(256, 256, 3, 3, device=DEV) * 0.05)
+    p1 = g.pack_fwd(w)
+    assert g.pack_fwd(w) is p1
+    with torch.no_grad():
+        w.mul_(2.0)
+    p2 = g.pack_fwd(w)
+    assert p2 is not p1 and torch.allclose(p2[:, :16], 2.0 * p1[:, :16])
+    opt = FusedAdam([w], lr=1e-2)  # re-binds w.data to the flat buffer
+    p3 = g.pack_fwd(w)
+    assert p3 is not p2
+    w.grad.fill_(1.0)
+    opt.step()
+    p4 = g.pack_fwd(w)
+    assert p4 is not p3 and not torch.equal(p4, p3)
+    assert g.pack_dgrad(w) is g.pack_dgrad(w)
