@@ -113,6 +113,9 @@ constexpr int NT = 256;
 #ifndef DCS_X6_BK
 #define DCS_X6_BK 16
 #endif
+#ifndef DCS_TAG2
+#define DCS_TAG2 1  // TAG-2 instances (no prologue / epilogue activation) for the generic x6 / f16x3 passes
+#endif
 #ifndef DCS_WGRAD_WIN
 #define DCS_WGRAD_WIN 1  // f16x3 residual weight gradient on the rolling-window kernel (conv_win.hip)
 #endif
@@ -587,6 +590,11 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
         d.Cs = 256; d.csplit = 256; d.s_c = 1;
         d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
     }
+    if constexpr (TAG == 2) {  // any geometry without prologue / epilogue activation: the runtime
+        // activation dispatch (and its tanh) leaves the k-loop, so the staging stays one basic block
+        // the MFMAs can interleave with
+        d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
+    }
 #endif
     return d;
 }
@@ -750,7 +758,7 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     // bf16x6 prologue (TAG 0): the per-(image, channel) scale / shift of the <= 2 images a tile
     // spans, staged once, so the affine at the LDS store reads LDS instead of issuing global
     // loads that would wait behind the prefetched gathers
-    constexpr bool PRO_LDS = X6F && TAG != 1;
+    constexpr bool PRO_LDS = X6F && TAG == 0;
     constexpr int PRO_CMAX = 512;
     __shared__ __attribute__((aligned(16))) float prol[PRO_LDS ? 4 * PRO_CMAX : 4];
 
@@ -2246,6 +2254,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
     const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3 || d.mma == MMA_F16;  // split-at-store pipelines
+    const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;  // TAG 2 instances
     const ClassGeom g0 = class_geom(d, 0);
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
@@ -2277,13 +2286,17 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
             DCS_ROWS_X6F(256, 128, 1, 0, grid2)
             if (bm_used) *bm_used = 256;
         }
+        else if (BN == 128 && plain) { DCS_ROWS_X6F(128, 128, 1, 2, grid) }
         else if (BN == 128) { DCS_ROWS_X6F(128, 128, 1, 0, grid) }
+        else if (plain) { DCS_ROWS_X6F(128, 64, 1, 2, grid) }
         else { DCS_ROWS_X6F(128, 64, 1, 0, grid) }
         return check_launch("conv_rows");
     }
     if (v4 && x6f && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
         const int gxx = gx;
-        if (BN == 128) { DCS_ROWS_X6F(128, 128, 2, 0, grid) }
+        if (BN == 128 && plain) { DCS_ROWS_X6F(128, 128, 2, 2, grid) }
+        else if (BN == 128) { DCS_ROWS_X6F(128, 128, 2, 0, grid) }
+        else if (plain) { DCS_ROWS_X6F(128, 64, 2, 2, grid) }
         else { DCS_ROWS_X6F(128, 64, 2, 0, grid) }
         return check_launch("conv_rows");
     }
@@ -2865,11 +2878,14 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
+        const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE;
         if (d.mma == MMA_F16X3) {  // f16x3: two 16-pixel sub-tiles per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (d.mma == MMA_F16) {  // f16: the same pipeline, one product
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
