@@ -177,6 +177,9 @@ constexpr int NT = 256;
 #ifndef DCS_H3_BM256_TAG0
 #define DCS_H3_BM256_TAG0 0  // fp16 modes: 256 x 128 tiles for the non-residual 128-column rows passes
 #endif
+#ifndef DCS_UWALK
+#define DCS_UWALK 1  // slice-major rows gathers: the (tap, slice) walk in uniform registers (no per-lane tap decode)
+#endif
 #ifndef DCS_X6_BM256
 #define DCS_X6_BM256 1  // bf16x6 residual rows: 256 x 128 tiles (512 threads)
 #endif
@@ -590,10 +593,11 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
         d.Cs = 256; d.csplit = 256; d.s_c = 1;
         d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
     }
-    if constexpr (TAG == 2) {  // any geometry without prologue / epilogue activation: the runtime
-        // activation dispatch (and its tanh) leaves the k-loop, so the staging stays one basic block
-        // the MFMAs can interleave with
+    if constexpr (TAG == 2) {  // zero padding, no upsampling in the gather, no prologue / epilogue
+        // activation: the runtime activation dispatch (and its tanh) leaves the k-loop, and the gather
+        // address is linear in the tap (the reflection / upsampling coordinate maps compile away)
         d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
+        d.pad_mode = DCS_PAD_ZERO; d.up = 1;
     }
 #endif
     return d;
@@ -863,6 +867,63 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             while (c >= d.Cs) { c -= d.Cs; ++j; }
         }
     };
+    // Uniform tap walk of the slice-major order (KS): every thread of the workgroup walks the same
+    // (tap, 16-channel slice) sequence, only the channel within the slice (akq / bkq & 15) differs
+    // per lane.  The walk state lives in SGPRs (readfirstlane at init, scalar selects per step) and
+    // the tap's kernel position is tracked as (ty, tx) instead of decoded from j per sub-tile: the
+    // per-lane decode (an integer division by KW for A and again for B) was ~20 % of the VALU
+    // instructions of the non-residual rows kernels, which are VALU bound.
+    int wntx, wnty, wty0 = 0, wtx0 = 0;  // taps of this class along x / y; parity-1 first taps
+    if (!d.parity) {
+        wntx = d.KW; wnty = d.KH;
+    } else if (d.parity == 2) {
+        wntx = 2; wnty = 2;
+    } else {
+        wty0 = (g.ry + d.pt) & 1; wtx0 = (g.rx + d.pl) & 1;
+        wntx = (d.KW - wtx0 + 1) >> 1; wnty = (d.KH - wty0 + 1) >> 1;
+    }
+    struct Walk {
+        int ty, tx, cs;  // tap position within the class, first channel of the slice
+    };
+    auto walk_init = [&](int p0) {  // p0: index of the first 16-k step (uniform)
+        Walk w;
+        const int j = p0 % g.ntaps;
+        w.cs = __builtin_amdgcn_readfirstlane((p0 / g.ntaps) * 16);
+        w.ty = __builtin_amdgcn_readfirstlane(j / wntx);
+        w.tx = __builtin_amdgcn_readfirstlane(j - (j / wntx) * wntx);
+        return w;
+    };
+    auto walk_step = [&](Walk& w) {
+        const bool wx = w.tx + 1 == wntx;
+        const bool wy = wx && w.ty + 1 == wnty;
+        w.tx = wx ? 0 : w.tx + 1;
+        w.ty = wy ? 0 : (wx ? w.ty + 1 : w.ty);
+        w.cs += wy ? 16 : 0;
+    };
+    // (ady, adx): source offset of the tap; bt: its column block in the packed weights (tap_decode).
+    // All three are affine in (ty, tx) with per-class constants (parity 1: ady = (ry + pt - ty0) / 2
+    // - ty, the numerator being even), so the walk needs no per-step case analysis.
+    int woy, wsy, wox, wsx, wb0, wbty, wbtx;
+    if (!d.parity) {
+        woy = 0; wsy = 1; wox = 0; wsx = 1; wb0 = 0; wbty = d.KW; wbtx = 1;
+    } else if (d.parity == 2) {
+        woy = g.ry - 1; wsy = 1; wox = g.rx - 1; wsx = 1; wb0 = (2 * g.ry + g.rx) * 4; wbty = 2; wbtx = 1;
+    } else {
+        woy = (g.ry + d.pt - wty0) >> 1; wsy = -1; wox = (g.rx + d.pl - wtx0) >> 1; wsx = -1;
+        wb0 = wty0 * d.KW + wtx0; wbty = 2 * d.KW; wbtx = 2;
+    }
+    auto walk_tap = [&](const Walk& w, int& ady, int& adx, int& bt) {
+        ady = woy + wsy * w.ty;
+        adx = wox + wsx * w.tx;
+        bt = wb0 + wbty * w.ty + wbtx * w.tx;
+    };
+    constexpr bool UWALK = KS && DCS_UWALK;
+    Walk wa = walk_init(kb0 >> 4), wb = wa;
+    const int alo = akq & 15, blo = bkq & 15;
+    // linear gather (zero padding, no upsampling): the lane's element offset of tap (0, 0) at channel
+    // alo of the slice; a tap adds ady * s_h + adx * s_w + slice base (uniform)
+    const bool lin = d.pad_mode == DCS_PAD_ZERO && d.up == 1;
+    const int abase = ri.n * (int)d.s_n + ri.by * (int)d.s_h + ri.bx * (int)d.s_w + alo;
     // one 16-k sub-tile step (NSUB > 1); equal to advance for 16-k tiles
     auto advance16 = [&](int& j, int& c) {
         if constexpr (KS) {
@@ -923,25 +984,56 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             // per thread each, by the branch-free select gather of the bf16x6 tiles below
 #pragma unroll
             for (int sub = 0; sub < NSUB; ++sub) {
-                const bool kin = aj < g.ntaps && ac < d.Cs;
-                int ady, adx, bt, sy = 0, sx = 0;
-                tap_decode(d, g, kin ? aj : 0, ady, adx, bt);
-                const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
-                const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
-                const int off = (kin && rvalid && yok && xok)
-                                    ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + ac) * 4
-                                    : OOB_OFF;
+                int ady, adx, bt, sy = 0, sx = 0, c;
+                bool kin;
+                if constexpr (UWALK) {
+                    kin = wa.cs < d.Cs;
+                    walk_tap(wa, ady, adx, bt);
+                    c = wa.cs + alo;
+                } else {
+                    kin = aj < g.ntaps && ac < d.Cs;
+                    tap_decode(d, g, kin ? aj : 0, ady, adx, bt);
+                    c = ac;
+                }
+                int off;
+                if (UWALK && lin) {  // zero padding, no upsampling: lane base + uniform tap offset
+                    const int vy = ri.by + ady, vx = ri.bx + adx;
+                    const bool ok = kin && rvalid && (unsigned)vy < (unsigned)Hv && (unsigned)vx < (unsigned)Wv;
+                    off = ok ? (abase + ady * (int)d.s_h + adx * (int)d.s_w + wa.cs) * 4 : OOB_OFF;
+                } else {
+                    const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                    const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                    off = (kin && rvalid && yok && xok) ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + c) * 4
+                                                        : OOB_OFF;
+                }
                 dst[2 * sub] = buf_load4(arsrc, off);
                 dst[2 * sub + 1] = buf_load4(arsrc, off + 16);
-                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[sub] = (int)so + ac;
-                advance16(aj, ac);
+                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[sub] = (int)so + c;
+                if constexpr (UWALK) walk_step(wa);
+                else advance16(aj, ac);
             }
         } else if (VEC && MMA != MMA_F32 && DCS_BF16_BUFGATHER) {
             // bf16 modes: branch-free gather through a buffer descriptor (OOB -> zeros)
             int sy = 0, sx = 0, off = OOB_OFF;
             // past the last k-tile (the x6 pipeline's unconditional prefetch) the walk leaves the
             // range through aj (tap-major) or through ac (slice-major): both must stay in range
-            if constexpr (X6F && DCS_X6_SELGATHER) {
+            int c = ac;
+            if constexpr (UWALK && X6F && DCS_X6_SELGATHER && BKT == 16) {
+                const bool kin = wa.cs < d.Cs;
+                int ady, adx, bt;
+                walk_tap(wa, ady, adx, bt);
+                c = wa.cs + alo;
+                if (lin) {
+                    const int vy = ri.by + ady, vx = ri.bx + adx;
+                    const bool ok = kin && rvalid && (unsigned)vy < (unsigned)Hv && (unsigned)vx < (unsigned)Wv;
+                    off = ok ? (abase + ady * (int)d.s_h + adx * (int)d.s_w + wa.cs) * 4 : OOB_OFF;
+                } else {
+                    const bool yok = map_coord_sel(ri.by + ady, Hv, d.up, d.pad_mode, sy);
+                    const bool xok = map_coord_sel(ri.bx + adx, Wv, d.up, d.pad_mode, sx);
+                    off = (kin && rvalid && yok && xok) ? (ri.n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + c) * 4
+                                                        : OOB_OFF;
+                }
+            } else if constexpr (X6F && DCS_X6_SELGATHER) {
                 // select form (tap 0 stands in for a tap past the end): no exec-mask branch
                 // splits the k-loop body, so the scheduler can spread the next tile's split
                 // arithmetic over this tile's MFMAs
@@ -962,12 +1054,16 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
 #pragma unroll
             for (int i = 0; i < ACH; ++i) dst[i] = buf_load4(arsrc, off + 16 * i);
             if constexpr (X6F) {
-                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[0] = (int)so + ac;
+                if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) pa[0] = (int)so + c;
             } else if (d.pro_act != DCS_ACT_NONE && off != OOB_OFF) {
 #pragma unroll
                 for (int i = 0; i < ACH; ++i) dst[i] = affine_act4(dst[i], psc + so + ac + 4 * i, psh + so + ac + 4 * i, d.pro_act);
             }
-            advance(aj, ac);
+            if constexpr (UWALK && X6F && DCS_X6_SELGATHER && BKT == 16) {
+                walk_step(wa);
+            } else {
+                advance(aj, ac);
+            }
         } else if (VEC) {
             // (a buffer-descriptor variant of this gather, as in the wgrad pass, measured 3-7 %
             //  slower here: invalid taps would issue loads that the branch now skips)
@@ -1029,6 +1125,12 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
                 bool ok = true;
                 if (!d.parity && !KSB) {
                     col = (long long)kt * BKT + 16 * sub + bkq;
+                } else if constexpr (KSB && DCS_UWALK) {
+                    ok = wb.cs < d.Cs;
+                    int ady, adx, bt;
+                    walk_tap(wb, ady, adx, bt);
+                    col = bt * d.Cs + wb.cs + blo;
+                    walk_step(wb);
                 } else {
                     ok = bj < g.ntaps && bc < d.Cs;
                     int ady, adx, bt = 0;
@@ -1046,6 +1148,12 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
         bool ok = true;
         if (!d.parity && !KSB) {
             col = kt * BKT + bkq;
+        } else if constexpr (KSB && DCS_UWALK && X6F && DCS_BF16_BUFGATHER && BKT == 16) {
+            ok = wb.cs < d.Cs;
+            int ady, adx, bt;
+            walk_tap(wb, ady, adx, bt);
+            col = bt * d.Cs + wb.cs + blo;
+            walk_step(wb);
         } else {  // the BKPT k of this thread share one tap (Cs % 16 == 0)
             ok = bj < g.ntaps && bc < d.Cs;
             int ady, adx, bt = 0;
@@ -2254,7 +2362,8 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     if (d.korder != DCS_KORDER_TAP && d.korder != DCS_KORDER_SLICE) return fail(DCS_E_INVALID, "conv_rows: bad korder");
     hipStream_t s = as_stream(stream);
     const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3 || d.mma == MMA_F16;  // split-at-store pipelines
-    const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;  // TAG 2 instances
+    const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO &&
+                       d.up == 1;  // TAG 2 instances
     const ClassGeom g0 = class_geom(d, 0);
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
@@ -2500,13 +2609,15 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     auto load = [&](long long kt, float4 (&ra)[2 * NSUB], float4 (&rb)[2 * NSUB], int (&pro)[NSUB]) {
 #pragma unroll
       for (int sub = 0; sub < NSUB; ++sub) {
-        long long p = NSUB > 1 ? px_beg + kt * (NSUB * BKP) + sub * BKP + kr : kt * BKP + kr;
-        const bool pok = p < (NSUB > 1 ? px_end : P);
+        // 32-bit pixel / offset arithmetic: the dispatch requires dy < 2 GiB (dy_small), so every
+        // pixel index and byte offset of dy fits (64-bit products here were ~10 % of the VALU)
+        int p = NSUB > 1 ? (int)px_beg + (int)kt * (NSUB * BKP) + sub * BKP + kr : (int)kt * BKP + kr;
+        const bool pok = p < (NSUB > 1 ? (int)px_end : (int)P);
         const int co = m0 + cc;
-        if (d.parity == 2) p = ((long long)pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
+        if (d.parity == 2) p = (pn * d.Ho + 2 * pqy + g.ry) * d.Wo + 2 * pqx + g.rx;  // phase pixel
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            ra[2 * sub + i] = buf_load4(dyrsrc, (pok && co + 4 * i < d.Co) ? (int)((p * d.Co + co + 4 * i) * 4) : OOB_OFF);
+            ra[2 * sub + i] = buf_load4(dyrsrc, (pok && co + 4 * i < d.Co) ? (p * d.Co + co + 4 * i) * 4 : OOB_OFF);
         // sub-pixel phases: the tap offsets already include the padding
         const int vy = d.parity == 2 ? pqy + bady : pqy * d.stride - d.pt + bady;
         const int vx = d.parity == 2 ? pqx + badx : pqx * d.stride - d.pl + badx;
@@ -2878,7 +2989,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
-        const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE;
+        const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO && d.up == 1;
         if (d.mma == MMA_F16X3) {  // f16x3: two 16-pixel sub-tiles per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
