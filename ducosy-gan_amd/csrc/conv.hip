@@ -177,6 +177,9 @@ constexpr int NT = 256;
 #ifndef DCS_H3_BM256_TAG0
 #define DCS_H3_BM256_TAG0 0  // fp16 modes: 256 x 128 tiles for the non-residual 128-column rows passes
 #endif
+#ifndef DCS_TAG3
+#define DCS_TAG3 1  // PatchGAN layers 1-3: rows / x6 weight-gradient instances with the IN + LeakyReLU gather fixed
+#endif
 #ifndef DCS_UWALK
 #define DCS_UWALK 1  // slice-major rows gathers: the (tap, slice) walk in uniform registers (no per-lane tap decode)
 #endif
@@ -599,6 +602,11 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
         d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
         d.pad_mode = DCS_PAD_ZERO; d.up = 1;
     }
+    if constexpr (TAG == 3) {  // the PatchGAN layers 1-3: the gather applies IN + LeakyReLU of the
+        // previous layer (compile-time activation), zero padding, no upsampling, no epilogue activation
+        d.pro_act = DCS_ACT_LRELU; d.epi_act = DCS_ACT_NONE;
+        d.pad_mode = DCS_PAD_ZERO; d.up = 1;
+    }
 #endif
     return d;
 }
@@ -762,7 +770,7 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     // bf16x6 prologue (TAG 0): the per-(image, channel) scale / shift of the <= 2 images a tile
     // spans, staged once, so the affine at the LDS store reads LDS instead of issuing global
     // loads that would wait behind the prefetched gathers
-    constexpr bool PRO_LDS = X6F && TAG == 0;
+    constexpr bool PRO_LDS = X6F && (TAG == 0 || TAG == 3);
     constexpr int PRO_CMAX = 512;
     __shared__ __attribute__((aligned(16))) float prol[PRO_LDS ? 4 * PRO_CMAX : 4];
 
@@ -2363,6 +2371,8 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     hipStream_t s = as_stream(stream);
     const bool x6f = d.mma == MMA_BF16X6 || d.mma == MMA_F16X3 || d.mma == MMA_F16;  // split-at-store pipelines
     const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO &&
+                       d.up == 1;
+    const bool lrelu = DCS_TAG3 && d.pro_act == DCS_ACT_LRELU && d.epi_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO &&
                        d.up == 1;  // TAG 2 instances
     const ClassGeom g0 = class_geom(d, 0);
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
@@ -2396,8 +2406,10 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
             if (bm_used) *bm_used = 256;
         }
         else if (BN == 128 && plain) { DCS_ROWS_X6F(128, 128, 1, 2, grid) }
+        else if (BN == 128 && lrelu) { DCS_ROWS_X6F(128, 128, 1, 3, grid) }
         else if (BN == 128) { DCS_ROWS_X6F(128, 128, 1, 0, grid) }
         else if (plain) { DCS_ROWS_X6F(128, 64, 1, 2, grid) }
+        else if (lrelu) { DCS_ROWS_X6F(128, 64, 1, 3, grid) }
         else { DCS_ROWS_X6F(128, 64, 1, 0, grid) }
         return check_launch("conv_rows");
     }
@@ -2990,9 +3002,11 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The
         // 64-output-channel layers could run the 128-row tile half masked: slower than f32.)
         const bool plain = DCS_TAG2 && d.pro_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO && d.up == 1;
+        const bool lrelu = DCS_TAG3 && d.pro_act == DCS_ACT_LRELU && d.pad_mode == DCS_PAD_ZERO && d.up == 1;
         if (d.mma == MMA_F16X3) {  // f16x3: two 16-pixel sub-tiles per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else if (lrelu) hipLaunchKernelGGL((conv_wgrad_x6_kernel<3, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16X3>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (d.mma == MMA_F16) {  // f16: the same pipeline, one product
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
