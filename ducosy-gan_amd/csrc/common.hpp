@@ -30,9 +30,13 @@ inline int check_launch(const char* what) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-// zero an f16x3 range record before its producer's atomic maxima (a no-op for rng == nullptr)
+// records inside a registered range-record arena (dcs_range_arena_register) are zeroed by the
+// caller in bulk, once per reuse of the arena
+bool in_range_arena(const void* p);
+// zero an f16x3 range record before its producer's atomic maxima (a no-op for rng == nullptr and
+// for records of a registered arena)
 inline int range_zero(float* rng, hipStream_t s) {
-    if (!rng) return 0;
+    if (!rng || in_range_arena(rng)) return 0;
     const hipError_t e = hipMemsetAsync(rng, 0, DCS_RANGE_PARTS * sizeof(float), s);
     return e == hipSuccess ? 0 : fail((int)e, "range record memset failed");
 }

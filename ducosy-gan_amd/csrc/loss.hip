@@ -637,6 +637,292 @@ __global__ void ssim_vt_kernel(const float* __restrict__ T, const float* __restr
     grad[e] = a[0] + 2.f * X[e] * a[1] + Y[e] * a[2];
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Fused G-step loss planes (north star: one cycle / identity / SSIM / gradient / contrast-loss
+// kernel; modules/trainer.py:469-512).  One launch walks every (pred, target) plane pair of the
+// step in 32 x 32 output tiles: a tile's pred / target (/ source) region with a 10-pixel halo is
+// staged in LDS once, and the job's terms are evaluated from it:
+//   L1     nn.L1Loss                         (trainer.py:348-349)
+//   GRAD   GradientLoss                      (trainer.py:22-40)
+//   SSIM   pytorch_msssim.SSIM, 11-tap valid gaussian, value and gradient in one pass: the
+//          forward blur over the tile + 10 px halo, the derivative maps, and the adjoint blur
+//          back onto the tile (the 4-pass ssim_v / ssim_h / ssim_ht / ssim_vt chain fused)
+//   CA     ContrastAttentionLoss (7x7 box, count_include_pad; trainer.py:43-86)
+//   MSEC   nn.MSELoss against a constant label (the PatchGAN terms, trainer.py:459-460, 470)
+// The job's gradient plane receives the WEIGHTED SUM of its terms' d/dpred (the coefficients are
+// the terms' weights in loss_G), plus up to two addends (the batch-coupled ContrastRegion /
+// ContrastEdge gradients of the same plane, computed by their own phases first): one write per
+// pixel, no per-term gradient planes and no adds.  Per-tile double partials of every term go to
+// part[block][8]; gl_final_kernel sums them in a fixed order (deterministic) and composes the
+// step's loss values from a coefficient recipe.
+// ---------------------------------------------------------------------------------------
+constexpr int GLT = 32, GLH = 10, GLR = GLT + 2 * GLH;  // tile, halo, staged region (52)
+constexpr int GLQ = GLT + GLH;                           // SSIM window positions per tile side (42)
+constexpr int GL_MAXJOB = 8;
+
+struct GLJobK {
+    const float* p;
+    const float* t;
+    const float* s;
+    const float* add0;
+    const float* add1;
+    float* g;
+    int nimg, flags, blk0, H, W, tiles_x, tiles, pad;
+    float c_l1, c_grad, c_ssim, c_ca, c_mse, t_const, c_add0, c_add1;
+};
+struct GLArgsK {
+    GLJobK j[GL_MAXJOB];
+    int njobs;
+    float gw[12];
+    float C1, C2, sigma, minw, maxw;
+};
+
+__global__ __launch_bounds__(256) void gl_planes_kernel(GLArgsK a, double* __restrict__ part) {
+    __shared__ float P[GLR * GLR], T[GLR * GLR], S[GLR * GLR];
+    __shared__ float V[5 * GLQ * GLR];  // SSIM vertical pass; reused by the CA maps and the adjoint
+    __shared__ float D[3 * GLQ * GLQ];
+    const int tid = threadIdx.x;
+    int jb = 0;
+#pragma unroll 1
+    for (int q = 1; q < a.njobs; ++q)
+        if ((int)blockIdx.x >= a.j[q].blk0) jb = q;
+    const GLJobK& J = a.j[jb];
+    const int H = J.H, W = J.W;
+    const int local = blockIdx.x - J.blk0;
+    const int n = local / J.tiles, tl = local - n * J.tiles;
+    const int ty = tl / J.tiles_x, tx = tl - ty * J.tiles_x;
+    const int i0 = ty * GLT, j0 = tx * GLT;
+    const long long base = (long long)n * H * W;
+    const int fl = J.flags;
+
+    // stage the region (zeros outside the image)
+    for (int e = tid; e < GLR * GLR; e += 256) {
+        const int r = e / GLR, c = e - r * GLR;
+        const int y = i0 - GLH + r, x = j0 - GLH + c;
+        const bool in = y >= 0 && y < H && x >= 0 && x < W;
+        const long long o = base + (long long)y * W + x;
+        P[e] = in ? J.p[o] : 0.f;
+        T[e] = in && J.t ? J.t[o] : 0.f;
+        if (fl & 8) S[e] = in ? J.s[o] : 0.f;
+    }
+    __syncthreads();
+
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // l1, grad x, grad y, ssim, ca / mse
+    float gout[4] = {0.f, 0.f, 0.f, 0.f};       // the thread's 4 pixels: (row tid/8, cols 4*(tid%8) ..)
+    const int orow = tid >> 3, oc0 = (tid & 7) * 4;
+    const float nhw = (float)((long long)J.nimg * H * W);
+    // pointwise and gradient-difference terms
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + orow, jx = j0 + oc0 + u;
+        if (i >= H || jx >= W) continue;
+        const int e = (orow + GLH) * GLR + oc0 + u + GLH;
+        const float pv = P[e], tv = T[e];
+        float g = 0.f;
+        if (fl & 1) {
+            const float d = pv - tv;
+            acc[0] += fabsf(d);
+            g += J.c_l1 * sgnf(d) / nhw;
+        }
+        if (fl & 16) {
+            const float d = pv - J.t_const;
+            acc[4] += (double)d * d;
+            g += J.c_mse * 2.f * d / nhw;
+        }
+        if (fl & 2) {
+            const float ix = J.c_grad / (float)((long long)J.nimg * H * (W - 1));
+            const float iy = J.c_grad / (float)((long long)J.nimg * (H - 1) * W);
+            if (jx + 1 < W) {
+                const float dp = P[e + 1] - pv, dt = T[e + 1] - tv, ex = fabsf(dp) - fabsf(dt);
+                acc[1] += fabsf(ex);
+                g -= sgnf(ex) * sgnf(dp) * ix;
+            }
+            if (jx > 0) {
+                const float dp = pv - P[e - 1], dt = tv - T[e - 1], ex = fabsf(dp) - fabsf(dt);
+                g += sgnf(ex) * sgnf(dp) * ix;
+            }
+            if (i + 1 < H) {
+                const float dp = P[e + GLR] - pv, dt = T[e + GLR] - tv, ey = fabsf(dp) - fabsf(dt);
+                acc[2] += fabsf(ey);
+                g -= sgnf(ey) * sgnf(dp) * iy;
+            }
+            if (i > 0) {
+                const float dp = pv - P[e - GLR], dt = tv - T[e - GLR], ey = fabsf(dp) - fabsf(dt);
+                g += sgnf(ey) * sgnf(dp) * iy;
+            }
+        }
+        gout[u] = g;
+    }
+
+    if (fl & 8) {  // ContrastAttention: box means on the tile + 3 px, gmap, adjoint box onto the tile
+        constexpr int CR = 3, CN = GLT + 2 * CR;  // 38
+        float* tb = V;
+        float* sb = V + CN * CN;
+        float* gm = V + 2 * CN * CN;
+        for (int e = tid; e < CN * CN; e += 256) {
+            const int r = e / CN, c = e - r * CN;
+            const int rr = r + GLH - CR, cc = c + GLH - CR;  // region coords of the box centre
+            float st = 0.f, ss = 0.f, sp = 0.f;
+            for (int dy = -CR; dy <= CR; ++dy)
+                for (int dx = -CR; dx <= CR; ++dx) {
+                    const int q = (rr + dy) * GLR + cc + dx;
+                    st += T[q];
+                    ss += S[q];
+                    sp += P[q];
+                }
+            st *= 1.f / 49.f; ss *= 1.f / 49.f; sp *= 1.f / 49.f;
+            const int y = i0 - CR + r, x = j0 - CR + c;
+            const bool in = y >= 0 && y < H && x >= 0 && x < W;
+            const float w = a.minw + (a.maxw - a.minw) * (1.f - expf(-fabsf(st - ss) / a.sigma));
+            tb[e] = w * fabsf(sp - st);
+            gm[e] = in ? w * sgnf(sp - st) / nhw : 0.f;
+            sb[e] = in ? 1.f : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + orow, jx = j0 + oc0 + u;
+            if (i >= H || jx >= W) continue;
+            const int r = orow + CR, c = oc0 + u + CR;
+            acc[4] += tb[r * CN + c];
+            float s = 0.f;
+            for (int dy = -CR; dy <= CR; ++dy)
+                for (int dx = -CR; dx <= CR; ++dx) s += gm[(r + dy) * CN + c + dx];
+            gout[u] += J.c_ca * s * (1.f / 49.f);
+        }
+        __syncthreads();
+    }
+
+    if (fl & 4) {  // SSIM, value + gradient (pytorch_msssim: valid gaussian, size_average)
+        const int Hv = H - 10, Wv = W - 10;
+        const float inv = 1.f / (float)((long long)J.nimg * Hv * Wv);
+        // vertical valid pass: window positions r (q_y = i0 - 10 + r), all 52 columns
+        for (int e = tid; e < GLQ * GLR; e += 256) {
+            const int r = e / GLR, c = e - r * GLR;
+            float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, m4 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 11; ++q) {
+                const float x = P[(r + q) * GLR + c], y = T[(r + q) * GLR + c], g = a.gw[q];
+                m0 = fmaf(g, x, m0); m1 = fmaf(g, y, m1);
+                m2 = fmaf(g, x * x, m2); m3 = fmaf(g, y * y, m3); m4 = fmaf(g, x * y, m4);
+            }
+            V[e] = m0; V[GLQ * GLR + e] = m1; V[2 * GLQ * GLR + e] = m2; V[3 * GLQ * GLR + e] = m3;
+            V[4 * GLQ * GLR + e] = m4;
+        }
+        __syncthreads();
+        // horizontal pass, ssim map and its derivative maps at the 42 x 42 window positions
+        for (int e = tid; e < GLQ * GLQ; e += 256) {
+            const int r = e / GLQ, c = e - r * GLQ;
+            const int qy = i0 - GLH + r, qx = j0 - GLH + c;
+            float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 11; ++q) {
+                const float g = a.gw[q];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) m[k] = fmaf(g, V[k * GLQ * GLR + r * GLR + c + q], m[k]);
+            }
+            const bool valid = qy >= 0 && qy < Hv && qx >= 0 && qx < Wv;
+            float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+            if (valid) {
+                const float mu1 = m[0], mu2 = m[1];
+                const float s11 = m[2] - mu1 * mu1, s22 = m[3] - mu2 * mu2, s12 = m[4] - mu1 * mu2;
+                const float A = 2.f * mu1 * mu2 + a.C1, B = mu1 * mu1 + mu2 * mu2 + a.C1;
+                const float Cc = 2.f * s12 + a.C2, Dd = s11 + s22 + a.C2;
+                const float s = (A / B) * (Cc / Dd);
+                if (r >= GLH && c >= GLH) acc[3] += s;  // window positions this tile owns
+                const float BD = B * Dd;
+                d0 = (2.f * mu2 * (Cc - A) / BD - s * 2.f * mu1 * (1.f / B - 1.f / Dd)) * inv;
+                d1 = (-s / Dd) * inv;
+                d2 = (2.f * A / BD) * inv;
+            }
+            D[e] = d0; D[GLQ * GLQ + e] = d1; D[2 * GLQ * GLQ + e] = d2;
+        }
+        __syncthreads();
+        // adjoint horizontal onto the tile's 32 columns (all 42 window rows): Tm[r][v]
+        float* Tm = V;
+        for (int e = tid; e < GLQ * GLT; e += 256) {
+            const int r = e / GLT, v = e - r * GLT;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int b = 0; b < 11; ++b) {
+                const int c = v + GLH - b;
+                const float g = a.gw[b];
+                s0 = fmaf(g, D[r * GLQ + c], s0);
+                s1 = fmaf(g, D[GLQ * GLQ + r * GLQ + c], s1);
+                s2 = fmaf(g, D[2 * GLQ * GLQ + r * GLQ + c], s2);
+            }
+            Tm[e] = s0; Tm[GLQ * GLT + e] = s1; Tm[2 * GLQ * GLT + e] = s2;
+        }
+        __syncthreads();
+        // adjoint vertical + chain rule: dX = R0 + 2 X R1 + Y R2
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int v = oc0 + u;
+            float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+#pragma unroll
+            for (int b = 0; b < 11; ++b) {
+                const int r = orow + GLH - b;
+                const float g = a.gw[b];
+                r0 = fmaf(g, Tm[r * GLT + v], r0);
+                r1 = fmaf(g, Tm[GLQ * GLT + r * GLT + v], r1);
+                r2 = fmaf(g, Tm[2 * GLQ * GLT + r * GLT + v], r2);
+            }
+            const int e = (orow + GLH) * GLR + v + GLH;
+            gout[u] += J.c_ssim * (r0 + 2.f * P[e] * r1 + T[e] * r2);
+        }
+    }
+
+    // one write per pixel: the weighted term gradients + the batch-coupled terms' addends
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + orow, jx = j0 + oc0 + u;
+        if (i >= H || jx >= W) continue;
+        const long long o = base + (long long)i * W + jx;
+        float g = gout[u];
+        if (J.add0) g += J.c_add0 * J.add0[o];
+        if (J.add1) g += J.c_add1 * J.add1[o];
+        if (J.g) J.g[o] = g;
+    }
+    block_partials<5>(acc, part);
+}
+
+// term values per job (fixed-order sums of the tile partials) and the composed outputs:
+// out[o] = bias[o] + sum_k coef[o][k] * val[k] + sum_x coef_x[o][x] * extra[x][0]
+// val[5 j + q]: q = 0 L1 mean, 1 gradient-loss x mean, 2 y mean, 3 SSIM mean, 4 CA / MSE mean
+constexpr int GL_MAXOUT = 12, GL_NEXTRA = 4;
+struct GLRecipeK {
+    float bias[GL_MAXOUT];
+    float coef[GL_MAXOUT][GL_MAXJOB * 5];
+    float coefx[GL_MAXOUT][GL_NEXTRA];
+    const float* extra[GL_NEXTRA];
+    int nout;
+};
+__global__ void gl_final_kernel(GLArgsK a, GLRecipeK rc, const double* __restrict__ part, float* __restrict__ out) {
+    __shared__ float val[GL_MAXJOB * 5];
+    for (int j = 0; j < a.njobs; ++j) {
+        const int H = a.j[j].H, W = a.j[j].W;
+        const int b0 = a.j[j].blk0, nb = a.j[j].nimg * a.j[j].tiles;
+        const double ni = a.j[j].nimg;
+        const double nrm[5] = {ni * H * W, ni * H * (W - 1), ni * (H - 1) * W, ni * (H - 10) * (W - 10), ni * H * W};
+        for (int q = 0; q < 5; ++q) {
+            double s = 0.0;
+            for (int b = threadIdx.x; b < nb; b += 64) s += part[(long long)(b0 + b) * 8 + q];
+            s = wave_sum_d(s);
+            if (threadIdx.x == 0) val[5 * j + q] = nrm[q] > 0 ? (float)(s / nrm[q]) : 0.f;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < rc.nout) {
+        const int o = threadIdx.x;
+        float v = rc.bias[o];
+        for (int k = 0; k < 5 * a.njobs; ++k) v += rc.coef[o][k] * val[k];
+        for (int x = 0; x < GL_NEXTRA; ++x)
+            if (rc.extra[x]) v += rc.coefx[o][x] * rc.extra[x][0];
+        out[o] = v;
+    }
+}
+
 }  // namespace dcs
 
 using namespace dcs;
@@ -921,4 +1207,66 @@ extern "C" int dcs_loss_ssim(const float* X, const float* Y, int N, int H, int W
                            H, W, win, G, grad);
     }
     return check_launch("loss_ssim");
+}
+
+extern "C" size_t dcs_gen_loss_fused_ws(const dcs_gl_job* jobs, int njobs) {
+    if (!jobs || njobs <= 0 || njobs > GL_MAXJOB) return 0;
+    long long blocks = 0;
+    for (int j = 0; j < njobs; ++j) blocks += (long long)jobs[j].n_img * cdiv(jobs[j].H, GLT) * cdiv(jobs[j].W, GLT);
+    return (size_t)blocks * 8 * sizeof(double) + 256;
+}
+
+extern "C" int dcs_gen_loss_fused(const dcs_gl_job* jobs, int njobs, float ssim_data_range, float ca_sigma,
+                                  float ca_min_w, float ca_max_w, const float* bias, const float* coef,
+                                  const float* coefx, const float* const* extra, int nout, float* out, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    if (!jobs || njobs <= 0 || njobs > GL_MAXJOB || nout < 0 || nout > GL_MAXOUT || (nout > 0 && (!out || !bias || !coef)))
+        return fail(DCS_E_INVALID, "gen_loss_fused: bad arguments");
+    if (!ws || ws_bytes < dcs_gen_loss_fused_ws(jobs, njobs)) return fail(DCS_E_WORKSPACE, "gen_loss_fused: workspace too small");
+    GLArgsK a{};
+    a.njobs = njobs;
+    int blk = 0;
+    for (int j = 0; j < njobs; ++j) {
+        const dcs_gl_job& s = jobs[j];
+        GLJobK& k = a.j[j];
+        if (!s.pred || s.n_img <= 0 || s.H < 2 || s.W < 2) return fail(DCS_E_INVALID, "gen_loss_fused: bad job");
+        if ((s.flags & ~31) || ((s.flags & (1 | 2 | 4 | 8)) && !s.target) || ((s.flags & 8) && !s.source) ||
+            ((s.flags & 4) && (s.H < 11 || s.W < 11)) || ((s.flags & 8) && (s.flags & 16)))
+            return fail(DCS_E_INVALID, "gen_loss_fused: bad job flags");
+        k.p = s.pred; k.t = s.target; k.s = s.source; k.add0 = s.add0; k.add1 = s.add1; k.g = s.grad;
+        k.nimg = s.n_img; k.flags = s.flags; k.H = s.H; k.W = s.W;
+        k.tiles_x = (int)cdiv(s.W, GLT);
+        k.tiles = k.tiles_x * (int)cdiv(s.H, GLT);
+        k.blk0 = blk;
+        blk += k.nimg * k.tiles;
+        k.c_l1 = s.c_l1; k.c_grad = s.c_grad; k.c_ssim = s.c_ssim; k.c_ca = s.c_ca; k.c_mse = s.c_mse;
+        k.t_const = s.t_const; k.c_add0 = s.c_add0; k.c_add1 = s.c_add1;
+    }
+    // pytorch_msssim: 11-tap gaussian, sigma 1.5, K = (0.01, 0.03)
+    float gs = 0.f;
+    for (int i = 0; i < 11; ++i) {
+        const float c = (float)(i - 5);
+        a.gw[i] = expf(-(c * c) / (2.f * 1.5f * 1.5f));
+        gs += a.gw[i];
+    }
+    for (int i = 0; i < 11; ++i) a.gw[i] /= gs;
+    a.gw[11] = 0.f;
+    a.C1 = (0.01f * ssim_data_range) * (0.01f * ssim_data_range);
+    a.C2 = (0.03f * ssim_data_range) * (0.03f * ssim_data_range);
+    a.sigma = ca_sigma; a.minw = ca_min_w; a.maxw = ca_max_w;
+    double* part = reinterpret_cast<double*>(ws);
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(gl_planes_kernel, dim3((unsigned)blk), dim3(256), 0, s, a, part);
+    if (nout > 0) {
+        GLRecipeK rc{};
+        rc.nout = nout;
+        for (int o = 0; o < nout; ++o) {
+            rc.bias[o] = bias[o];
+            for (int k = 0; k < 5 * njobs; ++k) rc.coef[o][k] = coef[o * 5 * njobs + k];
+            for (int x = 0; x < GL_NEXTRA; ++x) rc.coefx[o][x] = coefx ? coefx[o * GL_NEXTRA + x] : 0.f;
+        }
+        for (int x = 0; x < GL_NEXTRA; ++x) rc.extra[x] = extra ? extra[x] : nullptr;
+        hipLaunchKernelGGL(gl_final_kernel, dim3(1), dim3(64), 0, s, a, rc, part, out);
+    }
+    return check_launch("gen_loss_fused");
 }

@@ -6,6 +6,22 @@ namespace dcs {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+// registered range-record arenas (dcs_range_arena_register): [base, base + bytes)
+namespace {
+constexpr int ARENA_MAX = 32;
+struct ArenaRange {
+    uintptr_t lo, hi;
+};
+ArenaRange g_arenas[ARENA_MAX];
+int g_narena = 0;
+}  // namespace
+bool in_range_arena(const void* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (int i = 0; i < g_narena; ++i)
+        if (a >= g_arenas[i].lo && a < g_arenas[i].hi) return true;
+    return false;
+}
+
 // One launch over the flat parameter buffer of an optimizer.  Matches torch's Adam
 // (amsgrad=False, weight_decay=0):
 //   m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
@@ -319,4 +335,70 @@ extern "C" int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C
     hipLaunchKernelGGL(range_parts_kernel, dim3(DCS_RANGE_PARTS), dim3(512), 0, as_stream(stream), x,
                        (long long)n_img * per_img / 4, (long long)per_img, C, scale, shift, act, parts);
     return check_launch("range_parts");
+}
+
+// ---------------------------------------------------------------------------------------
+// dst[i] += src[i] over a list of tensors in one launch (the second contribution to parameter
+// gradients a model called twice in one step receives: one launch instead of one add per tensor)
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int MA_MAX = 64;
+struct MultiAddArgs {
+    const float* src[MA_MAX];
+    float* dst[MA_MAX];
+    long long n[MA_MAX];
+    int count;
+};
+__global__ __launch_bounds__(256) void multi_add_kernel(MultiAddArgs a) {
+    const int t = blockIdx.y;
+    if (t >= a.count) return;  // block-uniform
+    const long long n = a.n[t];
+    const float* __restrict__ s = a.src[t];
+    float* __restrict__ d = a.dst[t];
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) d[i] += s[i];
+}
+}  // namespace
+
+extern "C" int dcs_multi_add(int count, const float* const* src, float* const* dst, const int64_t* n, void* stream) {
+    if (count < 0 || (count > 0 && (!src || !dst || !n))) return fail(DCS_E_INVALID, "multi_add: bad arguments");
+    for (int c0 = 0; c0 < count; c0 += MA_MAX) {
+        MultiAddArgs a{};
+        a.count = count - c0 < MA_MAX ? count - c0 : MA_MAX;
+        long long mx = 1;
+        for (int i = 0; i < a.count; ++i) {
+            if (!src[c0 + i] || !dst[c0 + i] || n[c0 + i] < 0) return fail(DCS_E_INVALID, "multi_add: bad tensor");
+            a.src[i] = src[c0 + i];
+            a.dst[i] = dst[c0 + i];
+            a.n[i] = n[c0 + i];
+            mx = n[c0 + i] > mx ? n[c0 + i] : mx;
+        }
+        const unsigned gx = (unsigned)(cdiv(mx, 256) < 1024 ? cdiv(mx, 256) : 1024);
+        hipLaunchKernelGGL(multi_add_kernel, dim3(gx, (unsigned)a.count), dim3(256), 0, as_stream(stream), a);
+        const int e = check_launch("multi_add");
+        if (e) return e;
+    }
+    return DCS_OK;
+}
+
+extern "C" int dcs_range_arena_register(const void* base, size_t bytes) {
+    if (!base || bytes == 0) return fail(DCS_E_INVALID, "range_arena_register: bad arguments");
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
+    for (int i = 0; i < g_narena; ++i)
+        if (g_arenas[i].lo == lo) {
+            g_arenas[i].hi = lo + bytes;
+            return DCS_OK;
+        }
+    if (g_narena >= ARENA_MAX) return fail(DCS_E_INVALID, "range_arena_register: too many arenas");
+    g_arenas[g_narena++] = {lo, lo + bytes};
+    return DCS_OK;
+}
+
+extern "C" int dcs_range_arena_unregister(const void* base) {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
+    for (int i = 0; i < g_narena; ++i)
+        if (g_arenas[i].lo == lo) {
+            g_arenas[i] = g_arenas[--g_narena];
+            return DCS_OK;
+        }
+    return fail(DCS_E_INVALID, "range_arena_unregister: not registered");
 }

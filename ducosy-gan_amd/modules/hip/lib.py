@@ -36,6 +36,18 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class GLJob(ctypes.Structure):
+    """Mirror of dcs_gl_job (include/ducosy_hip.h): one plane set of the fused G-step loss kernel."""
+    _fields_ = [
+        ("pred", c_void_p), ("target", c_void_p), ("source", c_void_p), ("add0", c_void_p), ("add1", c_void_p),
+        ("grad", c_void_p), ("n_img", c_int32), ("H", c_int32), ("W", c_int32), ("flags", c_int32),
+        ("c_l1", c_float), ("c_grad", c_float), ("c_ssim", c_float), ("c_ca", c_float), ("c_mse", c_float),
+        ("t_const", c_float), ("c_add0", c_float), ("c_add1", c_float),
+    ]
+
+
+GL_L1, GL_GRAD, GL_SSIM, GL_CA, GL_MSEC = 1, 2, 4, 8, 16
+
 P = c_void_p
 DP = POINTER(ConvDesc)
 
@@ -87,6 +99,11 @@ SIGNATURES = {
     "dcs_cbam_backward": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int,
                                   c_int, c_int, P, P, P, P, P, c_size_t, P, P]),
     "dcs_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "dcs_gen_loss_fused_ws": (c_size_t, [P, c_int]),
+    "dcs_gen_loss_fused": (c_int, [P, c_int, c_float, c_float, c_float, c_float, P, P, P, P, c_int, P, P, c_size_t, P]),
+    "dcs_multi_add": (c_int, [c_int, P, P, P, P]),
+    "dcs_range_arena_register": (c_int, [P, c_size_t]),
+    "dcs_range_arena_unregister": (c_int, [P]),
     "dcs_loss_l1": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
     "dcs_loss_mse": (c_int, [P, P, c_int64, P, P, P, c_size_t, P]),
     "dcs_loss_mse_const": (c_int, [P, c_float, c_int64, P, P, P, c_size_t, P]),

@@ -75,6 +75,9 @@ _FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
 
 # parameter gradients written in place into freshly zeroed .grad buffers; "0" = always through autograd (A/B)
 _GRAD_SINK = os.environ.get("DUCOSY_GRAD_SINK", "1") == "1"
+# a second contribution to an existing .grad (the model called twice in one step) written to scratch
+# and added by one multi-tensor launch at the end of the backward; "0" = through autograd's adds
+_GRAD_ACC = os.environ.get("DUCOSY_GRAD_ACC", "1") == "1"
 
 
 class _GradSink:
@@ -88,14 +91,26 @@ class _GradSink:
     def __init__(self, params):
         self.params = params or {}
         self.out = {}
+        self.acc = []  # (scratch, .grad) pairs: second contributions, added by finish()
 
     def dest(self, k, view=None) -> Optional[torch.Tensor]:
         p = self.params.get(k)
         g = None if (p is None or not _GRAD_SINK) else p.grad
-        if g is None or not getattr(p, "_dcs_fresh", False) or not g.is_contiguous() or g.dtype != torch.float32:
+        if g is None or not g.is_contiguous() or g.dtype != torch.float32:
             return None
-        p._dcs_fresh = False
-        return g if view is None else g.view(view)
+        if getattr(p, "_dcs_fresh", False):
+            p._dcs_fresh = False
+            return g if view is None else g.view(view)
+        if not _GRAD_ACC:
+            return None
+        s = torch.empty_like(g)  # every producer overwrites its destination
+        self.acc.append((s, g))
+        return s if view is None else s.view(view)
+
+    def finish(self):
+        """Add the second contributions into their .grad buffers (one launch per 64 tensors)."""
+        ops.multi_add(self.acc)
+        self.acc = []
 
     def put(self, k, fn, view=None):
         d = self.dest(k, view)
@@ -228,10 +243,11 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
 
 
 def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, dx_from: int = 0,
-                       params: Optional[Dict[str, torch.Tensor]] = None):
+                       params: Optional[Dict[str, torch.Tensor]] = None, slice_only: bool = False):
     """Returns (dx NHWC [N,H,W,dx_channels] or None, _GradSink keyed like gen_param_names: .get(k)
     is the gradient to hand to autograd, None where it went into the parameter's .grad in place).
-    dx is computed for samples dx_from.. only (zero before)."""
+    dx is computed for samples dx_from.. only (zero before; with slice_only, dx holds those samples
+    only: [N - dx_from, H, W, dx_channels], no zero fill)."""
     L, W = S["L"], S["W"]
     nb, use_cbam = S["nb"], S["use_cbam"]
     grads = _GradSink(params)
@@ -273,7 +289,9 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     if need_dx:
         stem = L["stem"]
         wd = stem.pack_dgrad(W["stem.w"], dx_channels)
-        if dx_from > 0:
+        if dx_from > 0 and slice_only:
+            dx = stem.dgrad(dy[dx_from:], wd, H, Wd, ci_count=dx_channels)
+        elif dx_from > 0:
             dx = torch.zeros(N, H, Wd, dx_channels, device=dy.device, dtype=torch.float32)
             if dx_from < N:
                 dx[dx_from:] = stem.dgrad(dy[dx_from:], wd, H, Wd, ci_count=dx_channels)
@@ -285,6 +303,7 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     for b in range(nb):
         grads.zero(f"r{b}.c1.b", W[f"r{b}.c1.b"])
         grads.zero(f"r{b}.c2.b", W[f"r{b}.c2.b"])
+    grads.finish()
     return dx, grads
 
 
@@ -338,6 +357,18 @@ DISC_KEYS = ["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias",
              "model.5.bias", "model.8.weight", "model.8.bias", "model.12.weight", "model.12.bias"]
 
 
+_UNIT = {}
+
+
+def _unit_affine(N: int, dev) -> tuple:
+    """(ones, zeros) [N, 64]: the identity prologue of PatchGAN layer 1 (read-only, cached)."""
+    key = (N, str(dev))
+    if key not in _UNIT:
+        _UNIT[key] = (torch.ones(N, 64, device=dev, dtype=torch.float32),
+                      torch.zeros(N, 64, device=dev, dtype=torch.float32))
+    return _UNIT[key]
+
+
 def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: bool):
     L = disc_layers(x.shape[1])
     ws = params[0::2]
@@ -349,8 +380,7 @@ def discriminator_forward(params: List[torch.Tensor], x: torch.Tensor, keep: boo
     dev = x.device
     # layer 0: conv + bias; its LeakyReLU is the next conv's prologue (scale 1, shift 0)
     y0 = L[0].forward(xs, pk[0], bias=bs[0])
-    ones = torch.ones(N, 64, device=dev, dtype=torch.float32)
-    zeros = torch.zeros(N, 64, device=dev, dtype=torch.float32)
+    ones, zeros = _unit_affine(N, dev)
     ys, sts = [y0], [ops.INStats(ones, zeros)]
     h = y0
     for i in (1, 2, 3):
@@ -393,6 +423,7 @@ def discriminator_backward(S, dout, need_dx, need_w, params=None):
     if need_dx:
         xs = S["xs"]
         dx = L[0].dgrad(dy0, L[0].pack_dgrad(ws[0]), xs.H, xs.W)
+    grads.finish()
     return dx, grads
 
 

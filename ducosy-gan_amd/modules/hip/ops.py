@@ -67,6 +67,10 @@ def _p(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -110,6 +114,43 @@ def _round_up(x, m):
 # ---------------------------------------------------------------------------------------
 # f16x3 operand range records (include/ducosy_hip.h DCS_MMA_F16X3, dcs_range_parts)
 # ---------------------------------------------------------------------------------------
+# Range-record arena per (device, stream): producers' records are slots of one buffer, zeroed in one
+# launch when the arena is reset (range_arena_reset, once per training step) instead of one memset
+# per record (include/ducosy_hip.h dcs_range_arena_register).  A record remembers the arena
+# generation it was handed out in; after a reset it is stale and range_rec recomputes it.
+_ARENA = {}
+_ARENA_SLOTS = int(os.environ.get("DUCOSY_RANGE_ARENA", "256"))
+
+
+def _arena(dev):
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    a = _ARENA.get(key)
+    if a is None and _ARENA_SLOTS > 0:
+        buf = torch.zeros(_ARENA_SLOTS * lib.RANGE_PARTS, device=dev, dtype=torch.float32)
+        lib.call("dcs_range_arena_register", _p(buf), buf.numel() * 4)
+        a = _ARENA[key] = [buf, 0, 0, key]  # buffer, next slot, generation, key
+    return a
+
+
+def range_arena_reset(device) -> None:
+    """Zero the used records of this stream's arena (one launch) and start a new generation:
+    every record handed out before is stale from here on."""
+    a = _arena(torch.device(device))
+    if a is None:
+        return
+    if a[1]:
+        a[0][:a[1] * lib.RANGE_PARTS].zero_()
+    a[1] = 0
+    a[2] += 1
+
+
+def _rng_valid(cached) -> bool:
+    if len(cached) < 6 or cached[4] is None:
+        return True
+    a = _ARENA.get(cached[5])
+    return a is not None and a[2] == cached[4]
+
+
 def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None) -> torch.Tensor:
     """DCS_RANGE_PARTS partial maxima of |t| (or of |act(t * scale + shift)| with a per-(image,
     channel) prologue) for an NHWC tensor: the f16x3 kernels reduce them to the operand's power-of-two
@@ -120,7 +161,7 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
         return pro[3]
     cached = getattr(t, "_dcs_rng", None)
     if cached is not None and cached[0] == t._version and cached[1] is (pro[0] if pro else None) \
-            and cached[2] == (pro[2] if pro else ACT_NONE):
+            and cached[2] == (pro[2] if pro else ACT_NONE) and _rng_valid(cached):
         return cached[3]
     parts = torch.empty(lib.RANGE_PARTS, device=t.device, dtype=torch.float32)
     N, C = t.shape[0], t.shape[-1]
@@ -145,8 +186,14 @@ def _out_rng(out: torch.Tensor):
     kernel zeroes it and folds max |value| in; attached to ``out`` like range_rec's cache."""
     if not _h3():
         return None
-    rng = torch.empty(lib.RANGE_PARTS, device=out.device, dtype=torch.float32)
-    out._dcs_rng = (out._version, None, ACT_NONE, rng)
+    a = _arena(out.device)
+    if a is not None and a[1] < _ARENA_SLOTS:  # a pre-zeroed arena slot: the producer skips its memset
+        rng = a[0][a[1] * lib.RANGE_PARTS:(a[1] + 1) * lib.RANGE_PARTS]
+        a[1] += 1
+        out._dcs_rng = (out._version, None, ACT_NONE, rng, a[2], a[3])
+    else:
+        rng = torch.empty(lib.RANGE_PARTS, device=out.device, dtype=torch.float32)
+        out._dcs_rng = (out._version, None, ACT_NONE, rng)
     return _p(rng)
 
 
@@ -968,6 +1015,60 @@ def loss_ssim(X, Y, data_range=1.0, win=11, sigma=1.5, K=(0.01, 0.03), want_grad
     return _loss_call("dcs_loss_ssim", x,
                       lambda N, H, W: (_p(x), _p(y), N, H, W, float(data_range), int(win),
                                        float(sigma), float(K[0]), float(K[1])), want_grad)
+
+
+def gen_loss_fused(jobs, recipe=None, extra=(), ssim_data_range=1.0, ca=(0.15, 1.0, 3.0)):
+    """The fused G-step loss kernel (include/ducosy_hip.h dcs_gen_loss_fused).
+
+    jobs: dicts with pred [n,1,H,W] (contiguous), and as needed target, source, grad (written with
+    the weighted sum of the selected terms' d/dpred), flags (lib.GL_*), c_l1 / c_grad / c_ssim /
+    c_ca / c_mse coefficients, t_const, add0 / add1 with c_add0 / c_add1.
+    recipe: (bias [nout], coef [nout][5 * len(jobs)], coefx [nout][4]) composing the outputs from
+    the job terms' means (val[5 j + q]: q = 0 L1, 1 / 2 gradient-loss x / y, 3 SSIM, 4 CA or MSE)
+    and up to four device scalars ``extra``.  Returns the [nout] output tensor (or None)."""
+    arr = (lib.GLJob * len(jobs))()
+    dev = jobs[0]["pred"].device
+    for k, j in enumerate(jobs):
+        p = j["pred"]
+        _check_dev(p)
+        assert p.is_contiguous() and p.dim() == 4 and p.shape[1] == 1, "loss planes: contiguous [n,1,H,W]"
+        for key in ("target", "source", "grad", "add0", "add1"):
+            t = j.get(key)
+            if t is not None:
+                assert t.is_contiguous() and t.shape == p.shape, key
+        a = arr[k]
+        a.pred, a.target, a.source = p.data_ptr(), _ptr(j.get("target")), _ptr(j.get("source"))
+        a.add0, a.add1, a.grad = _ptr(j.get("add0")), _ptr(j.get("add1")), _ptr(j.get("grad"))
+        a.n_img, a.H, a.W, a.flags = p.shape[0], p.shape[2], p.shape[3], int(j["flags"])
+        for key in ("c_l1", "c_grad", "c_ssim", "c_ca", "c_mse", "t_const", "c_add0", "c_add1"):
+            setattr(a, key, float(j.get(key, 0.0)))
+    ws = workspace(lib.query("dcs_gen_loss_fused_ws", arr, len(jobs)), dev)
+    out, nout = None, 0
+    bias = coef = coefx = ex = None
+    if recipe is not None:
+        b, c, cx = recipe
+        nout = len(b)
+        bias = (ctypes.c_float * nout)(*b)
+        coef = (ctypes.c_float * (nout * 5 * len(jobs)))(*[float(v) for row in c for v in row])
+        coefx = (ctypes.c_float * (nout * 4))(*[float(v) for row in cx for v in row])
+        ex = (ctypes.c_void_p * 4)(*[_ptr(e) for e in (list(extra) + [None] * 4)[:4]])
+        out = torch.empty(nout, device=dev, dtype=torch.float32)
+    lib.call("dcs_gen_loss_fused", arr, len(jobs), float(ssim_data_range), float(ca[0]), float(ca[1]), float(ca[2]),
+             bias, coef, coefx, ex, nout, _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
+def multi_add(pairs) -> None:
+    """dst += src for a list of (src, dst) float32 tensors of equal numel, one launch per 64."""
+    if not pairs:
+        return
+    n = len(pairs)
+    src = (ctypes.c_void_p * n)(*[s.data_ptr() for s, _ in pairs])
+    dst = (ctypes.c_void_p * n)(*[d.data_ptr() for _, d in pairs])
+    cnt = (ctypes.c_int64 * n)(*[d.numel() for _, d in pairs])
+    for s_, d_ in pairs:
+        assert s_.numel() == d_.numel() and s_.is_contiguous() and d_.is_contiguous() and d_.dtype == torch.float32
+    lib.call("dcs_multi_add", n, src, dst, cnt, _stream())
 
 
 # ---------------------------------------------------------------------------------------

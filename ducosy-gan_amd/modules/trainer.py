@@ -35,6 +35,16 @@ from .optim import FusedAdam
 LAMBDA_GRAD, LAMBDA_GRAD_ID, LAMBDA_SSIM = 5.0, 2.5, 2.0        # trainer.py:493-495
 LAMBDA_CA, LAMBDA_CR, LAMBDA_CE = 2.0, 1.5, 1.0                 # trainer.py:500-502
 
+# The step as an explicit schedule of the fused forward / backward functions and the fused loss
+# kernel (no autograd graph: no slice / cat backward fills and copies, no per-term scalar
+# arithmetic, no gradient adds); "0" = the autograd step over the same kernels (A/B, reference
+# structure)
+_EXPLICIT_STEP = os.environ.get("DUCOSY_EXPLICIT_STEP", "1") == "1"
+
+# loss_G's output slots of the fused loss recipe (and the train_step dict keys)
+_G_TERMS = ("loss_G", "loss_GAN", "loss_cycle", "loss_id", "loss_grad_cycle", "loss_grad_id", "loss_ssim",
+            "loss_contrast_attention", "loss_contrast_region", "loss_contrast_edge")
+
 
 def apply_windowing(tensor_img, args):
     """modules/preprocess.py:58-65 (used for the validation image grid)."""
@@ -99,6 +109,149 @@ class CycleGANSystem:
     def train_step(self, real_A, real_B, masks=None):
         """One pass of trainer.py:463-525.  Returns the loss terms as 0-d device tensors (no
         host synchronisation inside)."""
+        if _EXPLICIT_STEP:
+            return self._train_step_explicit(real_A, real_B, masks)
+        return self._train_step_autograd(real_A, real_B, masks)
+
+    # ---- the step as an explicit schedule ---------------------------------------------------
+    def _g_loss_recipe(self, njobs):
+        """Coefficients composing _G_TERMS from the fused loss jobs' term means (job order of
+        _train_step_explicit: 0 rec_A, 1 rec_B, 2 id_A, 3 id_B, 4 fake_B, 5 D_B(fake_B),
+        6 D_A(fake_A); value q: 0 L1, 1/2 gradient x/y, 3 SSIM, 4 CA / MSE) and two extra scalars
+        (ContrastRegion, ContrastEdge).  trainer.py:469-512."""
+        lc, li = self.lambda_cyc, self.lambda_id
+        terms = {
+            "loss_GAN": ({(5, 4): .5, (6, 4): .5}, 0.0, (0, 0)),
+            "loss_cycle": ({(0, 0): .5, (1, 0): .5}, 0.0, (0, 0)),
+            "loss_id": ({(2, 0): .5, (3, 0): .5}, 0.0, (0, 0)),
+            "loss_grad_cycle": ({(0, 1): .5, (0, 2): .5, (1, 1): .5, (1, 2): .5}, 0.0, (0, 0)),
+            "loss_grad_id": ({(2, 1): .5, (2, 2): .5, (3, 1): .5, (3, 2): .5}, 0.0, (0, 0)),
+            "loss_ssim": ({(0, 3): -.5, (1, 3): -.5}, 1.0, (0, 0)),
+            "loss_contrast_attention": ({(4, 4): 1.0}, 0.0, (0, 0)),
+            "loss_contrast_region": ({}, 0.0, (1, 0)),
+            "loss_contrast_edge": ({}, 0.0, (0, 1)),
+        }
+        lam = {"loss_GAN": 1.0, "loss_cycle": lc, "loss_id": li, "loss_grad_cycle": LAMBDA_GRAD,
+               "loss_grad_id": LAMBDA_GRAD_ID, "loss_ssim": LAMBDA_SSIM, "loss_contrast_attention": LAMBDA_CA,
+               "loss_contrast_region": LAMBDA_CR, "loss_contrast_edge": LAMBDA_CE}
+        bias, coef, coefx = [], [], []
+        for name in _G_TERMS:
+            row, b, cx = [0.0] * (5 * njobs), 0.0, [0.0] * 4
+            parts = terms.items() if name == "loss_G" else [(name, terms[name])]
+            for tn, (cf, bb, (x0, x1)) in parts:
+                w = lam[tn] if name == "loss_G" else 1.0
+                for (j, q), c in cf.items():
+                    row[5 * j + q] += w * c
+                b += w * bb
+                cx[0] += w * x0
+                cx[1] += w * x1
+            bias.append(b)
+            coef.append(row)
+            coefx.append(cx)
+        return bias, coef, coefx
+
+    def _train_step_explicit(self, real_A, real_B, masks=None):
+        """trainer.py:463-525 as an explicit schedule: the Generator / Discriminator forward and
+        backward functions of modules/hip/networks.py called directly, every loss term of the G
+        step (L1, gradient, SSIM, contrast attention, the GAN MSEs) by one fused loss launch that
+        also writes each plane's combined d(loss_G)/d(plane) (modules/hip/ops.py gen_loss_fused),
+        the batch-coupled ContrastRegion / ContrastEdge phases first (their gradients enter the
+        fused launch as addends), and the input gradients of planes used twice summed by
+        in-place adds.  Same math and values as _train_step_autograd."""
+        from .hip import networks as net
+        from .hip import ops
+        from .hip.lib import GL_CA, GL_GRAD, GL_L1, GL_MSEC, GL_SSIM
+        from .losses import _global
+        N = real_A.shape[0]
+        G_AB, G_BA, D_A, D_B = self.models
+        nb, cb = G_AB.num_residual_blocks, G_AB.use_cbam
+        real_A, real_B = real_A.contiguous(), real_B.contiguous()
+        mk = (lambda k: torch.cat([masks] * k)) if masks is not None else (lambda k: None)
+        pAB = dict(zip(G_AB._keys, [p for _, p in G_AB.named_parameters()]))
+        pBA = dict(zip(G_BA._keys, [p for _, p in G_BA.named_parameters()]))
+        pDA = [p for _, p in D_A.named_parameters()]
+        pDB = [p for _, p in D_B.named_parameters()]
+
+        # --- Generator step (trainer.py:463-514) ---
+        ops.range_arena_reset(self.device)  # this step's range records: one zeroing launch
+        self.optimizer_G.zero_grad()
+        with torch.no_grad():
+            ab, S_ab = net.generator_forward(pAB, torch.cat([real_A, real_B]), mk(2), nb, cb, True)
+            fake_B, id_B = ab[:N], ab[N:]
+            ba, S_ba = net.generator_forward(pBA, torch.cat([real_B, real_A, fake_B]), mk(3), nb, cb, True)
+            fake_A, id_A, rec_A = ba[:N], ba[N:2 * N], ba[2 * N:]
+            dB, S_dB = net.discriminator_forward(pDB, fake_B, True)
+            dA, S_dA = net.discriminator_forward(pDA, fake_A, True)
+            rec_B, S_rb = net.generator_forward(pAB, fake_A, masks, nb, cb, True)
+            S_ab["out"], S_ba["out"], S_rb["out"] = ab, ba, rec_B
+            # batch-coupled terms (trainer.py:126-128, 170-180): their own phases, value + gradient
+            cr_m, ce_m = self.criterion_contrast_region, self.criterion_contrast_edge
+            if _global(cr_m.global_stats):
+                cr_v, cr_g = ops.loss_contrast_region_global(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight,
+                                                             parallel.allreduce_sum_, parallel.world())
+            else:
+                cr_v, cr_g = ops.loss_contrast_region(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight)
+            if _global(ce_m.global_stats):
+                ce_v, ce_g = ops.loss_contrast_edge_global(fake_B, real_B, parallel.allreduce_sum_, parallel.world())
+            else:
+                ce_v, ce_g = ops.loss_contrast_edge(fake_B, real_B)
+            # every other term: one fused launch, writing d(loss_G)/d(plane) for each plane
+            d_ab, d_ba, d_rb = torch.empty_like(ab), torch.empty_like(ba), torch.empty_like(rec_B)
+            d_dB, d_dA = torch.empty_like(dB), torch.empty_like(dA)
+            lc, li = self.lambda_cyc, self.lambda_id
+            rec = dict(flags=GL_L1 | GL_GRAD | GL_SSIM, c_l1=lc / 2, c_grad=LAMBDA_GRAD / 2, c_ssim=-LAMBDA_SSIM / 2)
+            idt = dict(flags=GL_L1 | GL_GRAD, c_l1=li / 2, c_grad=LAMBDA_GRAD_ID / 2)
+            ca_m = self.criterion_contrast_attention
+            assert ca_m.blur_kernel == 7, "fused loss: 7x7 contrast-attention box"
+            jobs = [dict(pred=rec_A, target=real_A, grad=d_ba[2 * N:], **rec),
+                    dict(pred=rec_B, target=real_B, grad=d_rb, **rec),
+                    dict(pred=id_A, target=real_A, grad=d_ba[N:2 * N], **idt),
+                    dict(pred=id_B, target=real_B, grad=d_ab[N:], **idt),
+                    dict(pred=fake_B, target=real_B, source=real_A, grad=d_ab[:N], flags=GL_CA, c_ca=LAMBDA_CA,
+                         add0=cr_g, c_add0=LAMBDA_CR, add1=ce_g, c_add1=LAMBDA_CE),
+                    dict(pred=dB, grad=d_dB, flags=GL_MSEC, c_mse=0.5, t_const=1.0),
+                    dict(pred=dA, grad=d_dA, flags=GL_MSEC, c_mse=0.5, t_const=1.0)]
+            vals = ops.gen_loss_fused(jobs, self._g_loss_recipe(len(jobs)), extra=(cr_v, ce_v),
+                                      ssim_data_range=self.criterion_ssim.data_range,
+                                      ca=(ca_m.sigma, ca_m.min_weight, ca_m.max_weight))
+            del cr_g, ce_g
+            # backward: D input gradients (no D parameter gradients in the G step), then the three
+            # Generator calls in reverse; planes with two consumers get the second by an add
+            dxB, _ = net.discriminator_backward(S_dB, d_dB, True, False)
+            ops.scale_add_(d_ab[:N], dxB.reshape(d_ab[:N].shape))
+            dxA, _ = net.discriminator_backward(S_dA, d_dA, True, False)
+            del S_dB, S_dA
+            dx_rb, _ = net.generator_backward(S_rb, d_rb, True, 1, 0, pAB)
+            torch.add(dxA.reshape(d_ba[:N].shape), dx_rb.reshape(d_ba[:N].shape), out=d_ba[:N])
+            del S_rb, dxA, dx_rb
+            dx_ba, _ = net.generator_backward(S_ba, d_ba, True, 1, 2 * N, pBA, slice_only=True)
+            ops.scale_add_(d_ab[:N], dx_ba.reshape(d_ab[:N].shape))
+            del S_ba, dx_ba
+            net.generator_backward(S_ab, d_ab, False, 1, 0, pAB)
+            del S_ab
+        parallel.allreduce_mean_(self.optimizer_G.flat_g)  # replica mean of the G gradient (one all-reduce)
+        self.optimizer_G.step()
+        out = {k: vals[i] for i, k in enumerate(_G_TERMS)}
+
+        # --- Discriminator steps (trainer.py:517-525), real and fake batched ---
+        for name, D, params, real, fake in (("loss_D_A", D_A, pDA, real_A, fake_A),
+                                            ("loss_D_B", D_B, pDB, real_B, fake_B)):
+            opt = self.optimizer_D_A if D is D_A else self.optimizer_D_B
+            opt.zero_grad()
+            with torch.no_grad():
+                o, S = net.discriminator_forward(params, torch.cat([real, fake]), True)
+                d_o = torch.empty_like(o)
+                jobs = [dict(pred=o[:N], grad=d_o[:N], flags=GL_MSEC, c_mse=0.5, t_const=1.0),
+                        dict(pred=o[N:], grad=d_o[N:], flags=GL_MSEC, c_mse=0.5, t_const=0.0)]
+                v = ops.gen_loss_fused(jobs, ([0.0], [[0, 0, 0, 0, .5, 0, 0, 0, 0, .5]], [[0.0] * 4]))
+                net.discriminator_backward(S, d_o, False, True, dict(enumerate(params)))
+            parallel.allreduce_mean_(opt.flat_g)
+            opt.step()
+            out[name] = v[0]
+        return out
+
+    def _train_step_autograd(self, real_A, real_B, masks=None):
+        """The same step on the autograd Functions (modules/hip/networks.py) and loss modules."""
         N = real_A.shape[0]
         G_AB, G_BA, D_A, D_B = self.models
         mk = (lambda k: torch.cat([masks] * k)) if masks is not None else (lambda k: None)

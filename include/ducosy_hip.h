@@ -155,6 +155,46 @@ int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind
 int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                        int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream);
 
+/* Fused G-step loss planes (the north star's fused cycle / identity / SSIM / gradient /
+ * contrast-loss kernel; replaces the per-term calls of modules/trainer.py:469-512).  One job per
+ * (pred, target) plane set of n_img single-channel H x W planes; flags select its terms:
+ *   DCS_GL_L1 nn.L1Loss, DCS_GL_GRAD GradientLoss (trainer.py:22-40), DCS_GL_SSIM
+ *   pytorch_msssim.SSIM (11-tap sigma 1.5 valid gaussian, size_average), DCS_GL_CA
+ *   ContrastAttentionLoss with a 7x7 box (trainer.py:43-86; needs source), DCS_GL_MSEC
+ *   nn.MSELoss against the constant t_const (target unused).
+ * grad (optional) receives c_l1 d(L1)/dpred + c_grad d(Grad)/dpred + c_ssim d(SSIM)/dpred +
+ * c_ca d(CA)/dpred + c_mse d(MSE)/dpred + c_add0 add0 + c_add1 add1 in one write per pixel
+ * (add0 / add1: optional planes of the same shape, e.g. the batch-coupled terms' gradients).
+ * Term values (means) val[5 j + q], q = 0 L1, 1 gradient-loss x part, 2 y part, 3 SSIM, 4 CA or
+ * MSE, are composed into out[o] = bias[o] + sum_k coef[o * 5 njobs + k] val[k]
+ *                                 + sum_x coefx[o * 4 + x] extra[x][0]  (o < nout <= 12)
+ * (extra: up to 4 device scalars, NULL entries skipped).  Two launches; deterministic. */
+#define DCS_GL_L1 1
+#define DCS_GL_GRAD 2
+#define DCS_GL_SSIM 4
+#define DCS_GL_CA 8
+#define DCS_GL_MSEC 16
+typedef struct dcs_gl_job {
+    const float* pred;
+    const float* target;
+    const float* source;
+    const float* add0;
+    const float* add1;
+    float* grad;
+    int32_t n_img, H, W, flags;
+    float c_l1, c_grad, c_ssim, c_ca, c_mse, t_const, c_add0, c_add1;
+} dcs_gl_job;
+size_t dcs_gen_loss_fused_ws(const dcs_gl_job* jobs, int njobs);
+int dcs_gen_loss_fused(const dcs_gl_job* jobs, int njobs, float ssim_data_range, float ca_sigma, float ca_min_w,
+                       float ca_max_w, const float* bias, const float* coef, const float* coefx,
+                       const float* const* extra, int nout, float* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Range-record arena: records (DCS_RANGE_PARTS floats each) inside [base, base + bytes) are zeroed
+ * by the caller, in bulk, before each reuse of the arena; the producers that fold a record's maxima
+ * then skip their own per-record memset.  Host-side registry of the calling process. */
+int dcs_range_arena_register(const void* base, size_t bytes);
+int dcs_range_arena_unregister(const void* base);
+
 /* Partial maxima of |act(x * scale[n][c] + shift[n][c])| (or |x| when act == DCS_ACT_NONE and
  * scale == NULL) over an NHWC tensor of n_img images of `per_img` elements, C channels
  * innermost: DCS_RANGE_PARTS floats into parts, whose max bounds every value (the rng_a / rng_b
@@ -445,6 +485,9 @@ int dcs_anatomical_masks(const float* hu, const uint8_t* lung_in, int N, int H, 
 int dcs_scale_add(float* y, const float* x, float a, int64_t n, void* stream); /* y += a*x */
 /* out = x * (*s) with s a device scalar (loss backward without a host sync) */
 int dcs_scale_dev(const float* x, const float* s, float* out, int64_t n, void* stream);
+/* dst[i][k] += src[i][k], k < n[i], for count tensors in one launch (host arrays of device
+ * pointers; chunks of 64 tensors per launch). */
+int dcs_multi_add(int count, const float* const* src, float* const* dst, const int64_t* n, void* stream);
 /* dy = da * act'(y): relu/lrelu given the pre-activation y; tanh given the output y */
 int dcs_act_backward(const float* da, const float* y, float* dy, int64_t n, int act, float* rng,
                      void* stream);

@@ -76,3 +76,29 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(lib, "LIB_PATH", "/nonexistent/libducosy_hip.so")
     with pytest.raises(lib.HipLibraryError):
         lib.load()
+
+
+def test_gl_job_layout_matches_c(tmp_path):
+    """offsetof/sizeof of dcs_gl_job (the fused loss kernel's job record) == lib.GLJob."""
+    from modules.hip.lib import GLJob
+    names = [f for f, _ in GLJob._fields_]
+    src = tmp_path / "gl.c"
+    body = "\n".join(f'  printf("{n} %zu\\n", offsetof(dcs_gl_job, {n}));' for n in names)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "ducosy_hip.h"\nint main(void){\n'
+                   + body + '\n  printf("sizeof %zu\\n", sizeof(dcs_gl_job));\n  return 0;\n}\n')
+    exe = tmp_path / "gl"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                        check=True).stdout.split("\n") if line)
+    for n in names:
+        assert int(got[n]) == getattr(GLJob, n).offset, n
+    assert int(got["sizeof"]) == ctypes.sizeof(GLJob)
+
+
+def test_integration_md_export_count():
+    """INTEGRATION.md states the number of extern "C" entry points the library exports."""
+    from modules.hip import lib
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"The library exports (\d+) `extern \"C\"` functions", text)
+    assert m, "INTEGRATION.md: export count sentence missing"
+    assert int(m.group(1)) == len(lib.exported_symbols())

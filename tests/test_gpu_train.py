@@ -162,3 +162,39 @@ def test_pack_cache_follows_weight_updates():
     p4 = g.pack_fwd(w)
     assert p4 is not p3 and not torch.equal(p4, p3)
     assert g.pack_dgrad(w) is g.pack_dgrad(w)
+
+
+def test_explicit_step_matches_autograd_step():
+    """CycleGANSystem's explicit step schedule (fused loss launch, direct backward calls) equals the
+    autograd step over the same kernels: loss values and every parameter after two steps."""
+    from modules import trainer
+    n, hw, nb, cin, seed = 2, 64, 1, 3, 611
+    seeds = prng.step_model_seeds(seed)
+    res = {}
+    for mode in (False, True):
+        prev = trainer._EXPLICIT_STEP
+        trainer._EXPLICIT_STEP = mode
+        try:
+            s = _system(cin, nb, seeds)
+            outs = []
+            for i in range(2):
+                rA = torch.from_numpy(prng.uniform(seed, f"A{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+                rB = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+                mk = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, hw, hw), 0.3)).to(DEV)
+                outs.append({k: float(v) for k, v in s.train_step(rA, rB, mk).items()})
+            params = {f"{t}.{k}": p.detach().clone() for t, m in zip(("GA", "GB", "DA", "DB"), s.models)
+                      for k, p in m.named_parameters()}
+            res[mode] = (outs, params)
+        finally:
+            trainer._EXPLICIT_STEP = prev
+    (oa, pa), (oe, pe) = res[False], res[True]
+    for i in range(2):
+        for k in oa[i]:
+            assert abs(oe[i][k] - oa[i][k]) <= 1e-5 * max(abs(oa[i][k]), 1e-2), (i, k, oe[i][k], oa[i][k])
+    # Adam's first updates are ~lr * sign(g): an entry whose gradient is decided by rounding may
+    # move the other way, so the typical entry must agree and every entry stay within 2 lr / step
+    lr = 2e-4
+    for k in pa:
+        d = (pe[k] - pa[k]).abs().flatten()
+        assert d.median().item() <= 1e-6 and d.max().item() <= 2 * lr * 2 + 1e-6, (k, d.max().item())
+
