@@ -19,6 +19,9 @@
 #include "conv_common.hpp"
 #include <type_traits>
 
+#ifndef DCS_WIN_GLDS
+#define DCS_WIN_GLDS 0  // A/B: B k-tiles staged by LDS-DMA (global_load_lds_dwordx4); measured neutral (profiles/r03s)
+#endif
 #ifndef DCS_WIN_SPREAD
 #define DCS_WIN_SPREAD 0  // 1: window staging spread over the slice's k-tiles (no VGPR spills, but 3-5 % slower: profiles/r03g)
 #endif
@@ -323,6 +326,31 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         bg[i] = pl * 0x40000000 + (n0 + row) * K + c6 * 8;  // bit 30: the lo plane
         bl[i] = wb_off(0, pl, c6 >> 1, row, c6 & 1);
     }
+#if DCS_WIN_GLDS
+    // LDS-DMA staging of B: a k-tile is 24 chunks of 1 KB (plane, tx slot, 32-row block); wave w
+    // issues chunks 3w .. 3w+2, each one global_load_lds_dwordx4 whose LDS image is lane-linear
+    // (lane L -> 16 bytes at chunk base + 16 L = row L/2, half position L%2).  The XOR swizzle of
+    // wb_off goes on the source side: lane L fetches the half h = (L%2) ^ bit 3 of its row.
+    int gsrc[3], gdst[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int c = wid * 3 + i, pl = c / 12, rem = c - pl * 12, tx = rem >> 2, rb = rem & 3;
+        const int row = rb * 32 + (lane >> 1), h = (lane & 1) ^ ((row >> 3) & 1);
+        gsrc[i] = pl * 0x40000000 + (n0 + row) * K + tx * 16 + h * 8;
+        gdst[i] = __builtin_amdgcn_readfirstlane((pl * 3 + tx) * WIN_SLOT + rb * 32 * 16);
+    }
+    auto b_glds = [&](int t, int buf) {
+        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
+        const int kb = s_ * 144 + ty_ * 48;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const _Float16* w = ((gsrc[i] >> 30) ? wl : wh) + (gsrc[i] & 0x3fffffff) + kb;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(w),
+                                             (__attribute__((address_space(3))) void*)(Bs + buf * 6 * WIN_SLOT + gdst[i]),
+                                             16, 0, 0);
+        }
+    };
+#endif
     uint4 br0, br1, br2;  // named (an array here was promoted to LDS)
     auto b_ld = [&](int i, int kb) {
         const int g = bg[i] & 0x3fffffff;
@@ -370,10 +398,15 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     win_load(0);
     win_store(0, 0);
 #endif
+#if DCS_WIN_GLDS
+    b_glds(0, 0);
+    __syncthreads();  // (drains the DMA: vmcnt(0) before the barrier)
+#else
     b_load(0);
     b_store(0);
     __syncthreads();
     b_load(1);
+#endif
 
     // every global load below is unconditional (indices clamped at the end): a load under a branch
     // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer, which here
@@ -382,9 +415,20 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     for (int s = 0; s < nslice; ++s) {
         const int wbuf = s & 1;
         if (!DCS_WIN_SPREAD) win_load(s + 1 < nslice ? s + 1 : s);
+#if DCS_WIN_GLDS
+        // keep the next slice's window loads at the top of the slice: with the DMA staging every
+        // barrier waits vmcnt(0), so loads sunk to the end of a k-tile would expose their latency
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) {
             const int tt = 3 * s + ty, bbuf = tt & 1;
+#if DCS_WIN_GLDS
+            // B tile tt + 1 into the other buffer (free: every wave passed the barrier after reading
+            // tile tt - 1 there); landed by the barrier that ends this k-tile.  Past the end: a repeat
+            // into a buffer nobody reads again
+            b_glds(tt + 1 < last ? tt + 1 : last, bbuf ^ 1);
+#endif
 #if DCS_WIN_SPREAD
             win_load_q(s + 1 < nslice ? s + 1 : s, ty);
 #endif
@@ -416,8 +460,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             }
             // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2 (past the end:
             // a repeat into a buffer nobody reads again)
+#if !DCS_WIN_GLDS
             b_store(bbuf ^ 1);
             b_load(tt + 2 < last ? tt + 2 : last);
+#endif
 #if DCS_WIN_SPREAD
             win_store_q(wbuf ^ 1, ty, s + 1 < nslice ? s + 1 : s);
 #else
