@@ -177,6 +177,9 @@ constexpr int NT = 256;
 #ifndef DCS_H3_BM256_TAG0
 #define DCS_H3_BM256_TAG0 0  // fp16 modes: 256 x 128 tiles for the non-residual 128-column rows passes
 #endif
+#ifndef DCS_WGRAD_X6_V4
+#define DCS_WGRAD_X6_V4 1  // fp16 modes: 4-channel-source weight gradients (stem, PatchGAN layer 0) on the x6 kernel
+#endif
 #ifndef DCS_TAG3
 #define DCS_TAG3 1  // PatchGAN layers 1-3: rows / x6 weight-gradient instances with the IN + LeakyReLU gather fixed
 #endif
@@ -2535,7 +2538,9 @@ typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
 
 // MMA == MMA_BF16P (the half-precision mode): the three planes hold three consecutive 16-pixel
 // sub-tiles converted to bf16 (48 pixels per barrier, one product each, one accumulation level).
-template <int TAG, int MMA = MMA_BF16X6>
+// V4: 4-channel NHWC source (the packed stem image + masks, PatchGAN layer 0): a thread's 8
+// columns are channels 0-3 of two consecutive taps, one float4 gather each
+template <int TAG, int MMA = MMA_BF16X6, bool V4 = false>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
     const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws, int kt_per_split,
@@ -2592,7 +2597,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
     const int nb0 = n0 + cc;
     const bool bcol_ok = nb0 < Ktot;
     int bady = 0, badx = 0, bchan = 0;
-    if (bcol_ok) {  // the 8 columns share one tap (Cs % 16 == 0)
+    int bady1 = 0, badx1 = 0;  // V4: the second tap of the thread's columns
+    bool bok1 = false;
+    if constexpr (V4) {
+        if (bcol_ok) {
+            int bt;
+            tap_decode(d, g, nb0 >> 2, bady, badx, bt);
+            bok1 = (nb0 >> 2) + 1 < g.ntaps;
+            if (bok1) tap_decode(d, g, (nb0 >> 2) + 1, bady1, badx1, bt);
+        }
+    } else if (bcol_ok) {  // the 8 columns share one tap (Cs % 16 == 0)
         const int j = nb0 / d.Cs;
         bchan = nb0 - j * d.Cs;
         int bt;
@@ -2638,8 +2652,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_x6_kernel(
         const bool xok = map_coord_sel(vx, Wv, d.up, d.pad_mode, sx);
         const bool ok = pok && bcol_ok && yok && xok;
         const int off = ok ? (pn * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w + bchan) * 4 : OOB_OFF;
+        if constexpr (V4) {
+            const int vy1 = d.parity == 2 ? pqy + bady1 : pqy * d.stride - d.pt + bady1;
+            const int vx1 = d.parity == 2 ? pqx + badx1 : pqx * d.stride - d.pl + badx1;
+            int sy1, sx1;
+            const bool ok1 = pok && bok1 && map_coord_sel(vy1, Hv, d.up, d.pad_mode, sy1) &&
+                             map_coord_sel(vx1, Wv, d.up, d.pad_mode, sx1);
+            rb[2 * sub] = buf_load4(rsrc, off);
+            rb[2 * sub + 1] = buf_load4(rsrc, ok1 ? (pn * (int)d.s_n + sy1 * (int)d.s_h + sx1 * (int)d.s_w) * 4 : OOB_OFF);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) rb[2 * sub + i] = buf_load4(rsrc, off + 16 * i);
+            for (int i = 0; i < 2; ++i) rb[2 * sub + i] = buf_load4(rsrc, off + 16 * i);
+        }
         pro[sub] = (d.pro_act != DCS_ACT_NONE && ok) ? pn * d.Cs + bchan : -1;
         // next k-tile: at most one row wrap (the dispatch requires Mx >= BKP), as selects so the
         // tile body stays one basic block
@@ -2997,6 +3021,17 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
         else
             hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
+    } else if (DCS_WGRAD_X6_V4 && (d.mma == MMA_F16X3 || d.mma == MMA_F16) && v4 && d.Cs == 4 && !d.parity && dy_small &&
+               d.pro_act == DCS_ACT_NONE && (p.BM == 128 || d.Co == 64) && class_geom(d, 0).Mx >= 16) {
+        // 4-channel sources (stem, PatchGAN layer 0) on the fp16 x6 pipeline: two taps per thread's 8 columns
+        const bool plain = DCS_TAG2 && d.pad_mode == DCS_PAD_ZERO && d.up == 1;
+        if (d.mma == MMA_F16X3) {
+            if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        } else {
+            if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+        }
     } else if (d.mma != MMA_F32 && vec && dy_small && (p.BM == 128 || (d.Co == 64 && DCS_WGRAD_X6_CO64 && (d.mma == MMA_F16X3 || d.mma == MMA_F16))) &&
                d.parity != 1 && class_geom(d, 0).Mx >= 16 && DCS_WGRAD_X6) {  // one row wrap per tile
         // 16-pixel tiles: twice the tile count per split, the same pixel ranges and slabs.  (The

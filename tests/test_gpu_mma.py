@@ -147,3 +147,25 @@ def test_modes_deterministic(ops, mode):
         for y, dx in outs[1:]:
             assert torch.equal(y, outs[0][0]), (mode, case)
             assert torch.equal(dx, outs[0][1]), (mode, case)
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("case", [(3, 64, 7, 1, (3, 3, 3, 3), "reflect", 1, 40), (1, 64, 4, 2, (1, 1, 1, 1), "zero", 1, 48)],
+                         ids=["stem", "d0"])
+def test_wgrad_4ch_source_vs_fp64(ops, mode, case):
+    """Weight gradients over the packed 4-channel NHWC source (the stem's image + masks, PatchGAN
+    layer 0) on the fp16 x6 kernel (conv_wgrad_x6_kernel<., ., V4>) against float64."""
+    g, H = _geom(case)
+    N = 2
+    x = rnd((N, g.cin, H, H + 1), 51, "x").double()
+    w = torch.from_numpy(prng.normal(52, "w", (g.cout, g.cin, g.k, g.k), 0, 0.05)).double()
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, g)
+    R = torch.from_numpy(prng.normal(53, "R", tuple(yr.shape))).float().double()
+    (yr * R).sum().backward()
+    ops.set_mma(mode)
+    x4 = ops.pack_nhwc4(x.float().to(DEV)[:, :1].contiguous(), x.float().to(DEV)[:, 1:].contiguous()
+                        if g.cin > 1 else None)
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dw = g.wgrad(Rd, ops.Src.nhwc(x4))
+    assert _relmax(dw, wr.grad) <= TOL[mode]
