@@ -180,6 +180,9 @@ constexpr int NT = 256;
 #ifndef DCS_WGRAD_X6_V4
 #define DCS_WGRAD_X6_V4 1  // fp16 modes: 4-channel-source weight gradients (stem, PatchGAN layer 0) on the x6 kernel
 #endif
+#ifndef DCS_TAG4
+#define DCS_TAG4 1  // the Generator stem's rows instance: per-row reflected offset tables, compile-time 7x7 x 4
+#endif
 #ifndef DCS_TAG3
 #define DCS_TAG3 1  // PatchGAN layers 1-3: rows / x6 weight-gradient instances with the IN + LeakyReLU gather fixed
 #endif
@@ -605,6 +608,10 @@ __device__ __forceinline__ dcs_conv_desc specialise(dcs_conv_desc d) {
         d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
         d.pad_mode = DCS_PAD_ZERO; d.up = 1;
     }
+    if constexpr (TAG == 4) {  // the Generator stem: 7x7 reflect-padded conv over the packed NHWC x 4 image
+        d.KH = 7; d.KW = 7; d.Cs = 4; d.csplit = 4; d.s_c = 1; d.stride = 1; d.up = 1; d.parity = 0;
+        d.pad_mode = DCS_PAD_REFLECT; d.pro_act = DCS_ACT_NONE; d.epi_act = DCS_ACT_NONE;
+    }
     if constexpr (TAG == 3) {  // the PatchGAN layers 1-3: the gather applies IN + LeakyReLU of the
         // previous layer (compile-time activation), zero padding, no upsampling, no epilogue activation
         d.pro_act = DCS_ACT_LRELU; d.epi_act = DCS_ACT_NONE;
@@ -774,6 +781,11 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     // spans, staged once, so the affine at the LDS store reads LDS instead of issuing global
     // loads that would wait behind the prefetched gathers
     constexpr bool PRO_LDS = X6F && (TAG == 0 || TAG == 3);
+    // TAG 4 (stem): the reflected source row / column offsets of each A row's 7 kernel rows and 7
+    // kernel columns, computed once per workgroup (14 coordinate maps per row instead of 2 per tap
+    // per k-tile); a tap's gather offset is one row entry + one column entry
+    constexpr bool STEMT = TAG == 4 && VEC == 2;
+    __shared__ int stab[STEMT ? 2 * BM * 7 : 1];
     constexpr int PRO_CMAX = 512;
     __shared__ __attribute__((aligned(16))) float prol[PRO_LDS ? 4 * PRO_CMAX : 4];
 
@@ -800,6 +812,21 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     const RowInfo ri = row_info(d, g, (int)(m0 + arow), fold);
     const bool rvalid = ri.out_off >= 0;
     if ((tid & 1) == 0) rowoff[arow] = ri.out_off;
+    if constexpr (STEMT) {  // thread pair of a row: even lane the 7 row offsets, odd lane the 7 column offsets
+        const int Hv0 = d.Hs * d.up, Wv0 = d.Ws * d.up;
+#pragma unroll
+        for (int t7 = 0; t7 < 7; ++t7) {
+            int c;
+            if ((tid & 1) == 0) {
+                map_coord(ri.by + t7, Hv0, d.up, d.pad_mode, c);
+                stab[arow * 7 + t7] = c * (int)d.s_h;
+            } else {
+                map_coord(ri.bx + t7, Wv0, d.up, d.pad_mode, c);
+                stab[BM * 7 + arow * 7 + t7] = c * (int)d.s_w;
+            }
+        }
+        __syncthreads();
+    }
     // B loader: one output channel row, BKPT consecutive k
     const int brow = tid / BTPR, bkq = (tid % BTPR) * ((MMA == MMA_BF16P || NSUB > 1) ? 16 / BTPR : BKPT);
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
@@ -954,7 +981,17 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     auto load_a = [&](int kt, auto& dst, int (&pa)[NSUB]) {
 #pragma unroll
         for (int q = 0; q < NSUB; ++q) pa[q] = -1;
-        if (VEC == 2) {  // Cs == 4: taps aj .. aj+ACH-1, one float4 each (no prologue)
+        if (STEMT) {  // the stem: 49 taps, reflected offsets from the per-row table, branch-free
+#pragma unroll
+            for (int e = 0; e < ACH; ++e) {
+                const int j = aj + e;
+                const int ty = j / 7, tx = j - (j / 7) * 7;
+                const bool ok = rvalid && j < 49;
+                const int o = ok ? (ri.n * (int)d.s_n + stab[arow * 7 + ty] + stab[BM * 7 + arow * 7 + tx]) * 4 : OOB_OFF;
+                dst[e] = buf_load4(arsrc, ok ? o : OOB_OFF);
+            }
+            aj += BKT / 4;
+        } else if (VEC == 2) {  // Cs == 4: taps aj .. aj+ACH-1, one float4 each (no prologue)
 #pragma unroll
             for (int e = 0; e < ACH; ++e) dst[e] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (rvalid) {
@@ -2418,9 +2455,12 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     }
     if (v4 && x6f && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
         const int gxx = gx;
+        const bool stem = DCS_TAG4 && d.KH == 7 && d.KW == 7 && d.Cs == 4 && d.stride == 1 && d.up == 1 && !d.parity &&
+                          d.pad_mode == DCS_PAD_REFLECT && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
         if (BN == 128 && plain) { DCS_ROWS_X6F(128, 128, 2, 2, grid) }
         else if (BN == 128) { DCS_ROWS_X6F(128, 128, 2, 0, grid) }
         else if (plain) { DCS_ROWS_X6F(128, 64, 2, 2, grid) }
+        else if (stem) { DCS_ROWS_X6F(128, 64, 2, 4, grid) }
         else { DCS_ROWS_X6F(128, 64, 2, 0, grid) }
         return check_launch("conv_rows");
     }

@@ -1,0 +1,14 @@
+# 256-row TAG-0 tiles (variant t256): op / model / mma tests on it, kbench A/B of all layers, bench A/B
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+V=${1:-uw}
+DUCOSY_HIP_LIB=$R/ducosy-gan_amd/lib/libducosy_hip_$V.so timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_train.py tests/test_gpu_fullsize.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_tests.log 2>&1 || { echo TESTS FAILED; grep -E "FAILED|^E  " gpurun_out/t_tests.log | head -30; tail -3 gpurun_out/t_tests.log; exit 1; }
+tail -1 gpurun_out/t_tests.log
+bash scripts/gpu_kab.sh "stem" f16x3 16 $V && bash scripts/gpu_kab.sh "stem" f16x3 16 $V || exit 1
+for it in 1 2; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/t_bench_A_$it.log 2>&1 || { echo BENCH A FAILED; exit 1; }
+  echo "A: $(tail -1 gpurun_out/t_bench_A_$it.log | cut -c100-200)"
+  DUCOSY_HIP_LIB=$R/ducosy-gan_amd/lib/libducosy_hip_$V.so timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/t_bench_B_$it.log 2>&1 || { echo BENCH B FAILED; exit 1; }
+  echo "B: $(tail -1 gpurun_out/t_bench_B_$it.log | cut -c100-200)"
+done
