@@ -891,6 +891,7 @@ __global__ __launch_bounds__(256) void gl_planes_kernel(GLArgsK a, double* __res
 // out[o] = bias[o] + sum_k coef[o][k] * val[k] + sum_x coef_x[o][x] * extra[x][0]
 // val[5 j + q]: q = 0 L1 mean, 1 gradient-loss x mean, 2 y mean, 3 SSIM mean, 4 CA / MSE mean
 constexpr int GL_MAXOUT = 12, GL_NEXTRA = 4;
+constexpr int GL_FINAL_WAVES = 8;
 struct GLRecipeK {
     float bias[GL_MAXOUT];
     float coef[GL_MAXOUT][GL_MAXJOB * 5];
@@ -899,17 +900,25 @@ struct GLRecipeK {
     int nout;
 };
 __global__ void gl_final_kernel(GLArgsK a, GLRecipeK rc, const double* __restrict__ part, float* __restrict__ out) {
+    // one wave per job (jobs w, w + 8, ...); each lane sums the five terms of its blocks in a
+    // fixed order, then a fixed-shape wave reduction: deterministic, 5 independent load streams
     __shared__ float val[GL_MAXJOB * 5];
-    for (int j = 0; j < a.njobs; ++j) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (int j = wv; j < a.njobs; j += GL_FINAL_WAVES) {
         const int H = a.j[j].H, W = a.j[j].W;
         const int b0 = a.j[j].blk0, nb = a.j[j].nimg * a.j[j].tiles;
         const double ni = a.j[j].nimg;
         const double nrm[5] = {ni * H * W, ni * H * (W - 1), ni * (H - 1) * W, ni * (H - 10) * (W - 10), ni * H * W};
+        double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int b = ln; b < nb; b += 64) {
+            const double* pp = part + (long long)(b0 + b) * 8;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) s[q] += pp[q];
+        }
+#pragma unroll
         for (int q = 0; q < 5; ++q) {
-            double s = 0.0;
-            for (int b = threadIdx.x; b < nb; b += 64) s += part[(long long)(b0 + b) * 8 + q];
-            s = wave_sum_d(s);
-            if (threadIdx.x == 0) val[5 * j + q] = nrm[q] > 0 ? (float)(s / nrm[q]) : 0.f;
+            const double t = wave_sum_d(s[q]);
+            if (ln == 0) val[5 * j + q] = nrm[q] > 0 ? (float)(t / nrm[q]) : 0.f;
         }
     }
     __syncthreads();
@@ -1266,7 +1275,7 @@ extern "C" int dcs_gen_loss_fused(const dcs_gl_job* jobs, int njobs, float ssim_
             for (int x = 0; x < GL_NEXTRA; ++x) rc.coefx[o][x] = coefx ? coefx[o * GL_NEXTRA + x] : 0.f;
         }
         for (int x = 0; x < GL_NEXTRA; ++x) rc.extra[x] = extra ? extra[x] : nullptr;
-        hipLaunchKernelGGL(gl_final_kernel, dim3(1), dim3(64), 0, s, a, rc, part, out);
+        hipLaunchKernelGGL(gl_final_kernel, dim3(1), dim3(64 * GL_FINAL_WAVES), 0, s, a, rc, part, out);
     }
     return check_launch("gen_loss_fused");
 }
