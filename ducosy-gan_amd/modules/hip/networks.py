@@ -82,11 +82,12 @@ _GRAD_ACC = os.environ.get("DUCOSY_GRAD_ACC", "1") == "1"
 
 class _GradSink:
     """Parameter gradients of one backward pass.  A parameter whose ``.grad`` the fused optimizer has
-    just zeroed (modules/optim.py FusedAdam.zero_grad marks it ``_dcs_fresh``) receives its gradient
-    in place: the producing kernel writes straight into ``.grad`` and autograd gets None, so there is
-    no AccumulateGrad add and no zero fill.  Any other parameter gets its gradient back through
-    autograd as usual (the second batched G_A2B call of a step, plain ``.backward()`` without the
-    fused optimizer: same values, same ``.grad`` contents as accumulation gives)."""
+    just zeroed (modules/optim.py FusedAdam.zero_grad stamps it ``_dcs_fresh`` with the .grad's address
+    and version counter) receives its gradient in place while the stamp still matches: the producing
+    kernel writes straight into ``.grad`` and autograd gets None, so there is no AccumulateGrad add and
+    no zero fill.  Any other parameter (the second batched G_A2B call of a step, a .grad some torch op
+    wrote to since the zeroing, plain ``.backward()`` without the fused optimizer) gets its gradient
+    added: to scratch and one multi-tensor add, or back through autograd."""
 
     def __init__(self, params):
         self.params = params or {}
@@ -98,8 +99,9 @@ class _GradSink:
         g = None if (p is None or not _GRAD_SINK) else p.grad
         if g is None or not g.is_contiguous() or g.dtype != torch.float32:
             return None
-        if getattr(p, "_dcs_fresh", False):
-            p._dcs_fresh = False
+        stamp = getattr(p, "_dcs_fresh", None)
+        p._dcs_fresh = None
+        if stamp is not None and stamp == (g.data_ptr(), g._version):
             return g if view is None else g.view(view)
         if not _GRAD_ACC:
             return None

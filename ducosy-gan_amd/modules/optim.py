@@ -45,11 +45,17 @@ class FusedAdam(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = True):
         """Zero the flat gradient buffer (the per-parameter grads stay views of it).  Each parameter is
-        marked fresh: the fused networks' backward (modules/hip/networks.py _GradSink) then writes its
-        first gradient straight into the zeroed .grad instead of handing it to AccumulateGrad."""
+        marked fresh with a stamp (storage address, version counter) of its zeroed .grad: the fused
+        networks' backward (modules/hip/networks.py _GradSink) writes its first gradient straight into
+        that .grad instead of handing it to AccumulateGrad, but only while the stamp still matches.
+        Any torch in-place write to the flat buffer (AccumulateGrad's add of an ordinary autograd
+        contribution, a user regulariser) bumps the version counter the views share, and a replaced
+        .grad changes the address: the parameter is then no longer fresh and its fused contribution
+        is added, not written over."""
         self.flat_g.zero_()
+        v = self.flat_g._version
         for p in self.param_groups[0]["params"]:
-            p._dcs_fresh = True
+            p._dcs_fresh = (p.grad.data_ptr(), v) if p.grad is not None else None
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -5,10 +5,10 @@ scatters every G/D call over 8 GPUs, re-broadcasts all parameters per call and r
 gradients to cuda:0.  Here each rank owns full replicas of G_A2B, G_B2A, D_A, D_B and its own
 batch shard; per optimizer step the optimizer's flat gradient buffer (FusedAdam.flat_g: 91.6 MB
 for the G pair, 11.05 MB per D at cin 3) is averaged over the replicas by ONE stream-ordered
-all-reduce after the backward (``GradBuckets`` with overlap off, the default).  Launching bucket
-all-reduces from inside the backward (``DUCOSY_GRAD_OVERLAP=1``) would put RCCL's kernels on their
-own queue beside the backward's, on shared compute-unit pairs: the condition of the unexplained
-two-queue hazard (Config 5), for at most ~1 ms of a 300+ ms step.  Initial weights
+all-reduce after the backward, stream-ordered on the compute stream.  The exchange is not
+overlapped with the backward: RCCL's kernels on a queue of their own beside the backward's would
+share compute-unit pairs with it, the condition of the two-queue hazard (Config 5),
+for at most ~1 ms of a 250 ms step.  Initial weights
 are broadcast from the group's first rank once; ``replicas_identical`` checks after a run that
 every replica still holds the same parameters (bench.py reports it).
 
@@ -129,86 +129,6 @@ def shard(n_total: int, r: int = None, w: int = None):
     w = world() if w is None else w
     per = n_total // w
     return r * per, (r + 1) * per
-
-
-_OVERLAP = os.environ.get("DUCOSY_GRAD_OVERLAP", "0") == "1"
-
-
-class GradBuckets:
-    """All-reduce-mean of one flat gradient buffer.  Default (``overlap`` False): ``arm()`` does
-    nothing and ``finish()`` runs one stream-ordered all-reduce of the whole buffer after the
-    backward.  With ``overlap`` (DUCOSY_GRAD_OVERLAP=1, experimental): in buckets, each launched
-    (async) as soon as the backward has finished accumulating every parameter of the bucket, so
-    the exchange of the early buckets overlaps the rest of the backward.
-
-    buckets: list of lists of parameters whose ``.grad`` are views of ``flat`` (FusedAdam
-    layout); each bucket must be one contiguous span of ``flat``.  Autograd accumulates a leaf
-    once per backward however many graph branches reach it (the branches are summed first), so
-    a bucket is complete after one post-accumulate hook per member.  ``arm()`` before the
-    backward, ``finish()`` after it (waits for every bucket and applies 1/world); ``early``
-    counts the buckets launched from inside the backward.  With one replica both are no-ops."""
-
-    def __init__(self, flat: torch.Tensor, buckets, overlap: bool = None):
-        self.flat = flat
-        self.overlap = _OVERLAP if overlap is None else bool(overlap)
-        self.spans, self.members = [], []
-        base = flat.data_ptr()
-        esz = flat.element_size()
-        for b in buckets:
-            offs = [((p.grad.data_ptr() - base) // esz, p.numel()) for p in b]
-            lo = min(o for o, _ in offs)
-            hi = max(o + n for o, n in offs)
-            if sum(n for _, n in offs) != hi - lo:
-                raise ValueError("GradBuckets: a bucket must be one contiguous span of the flat buffer")
-            self.spans.append((lo, hi))
-            self.members.append(b)
-        self._handles = []
-        self._works = []
-        self._left = None
-        self.early = 0
-
-    def disarm(self):
-        """Remove the hooks of an earlier arm() (also after a backward that raised)."""
-        for h in self._handles:
-            h.remove()
-        self._handles = []
-
-    def arm(self):
-        self.disarm()
-        if world() == 1 or not self.overlap:
-            return
-        self._works = [None] * len(self.spans)
-        self._left = [len(b) for b in self.members]
-        self.early = 0
-        for bi, b in enumerate(self.members):
-            for p in b:
-                self._handles.append(p.register_post_accumulate_grad_hook(self._hook(bi)))
-
-    def _hook(self, bi):
-        def fn(_p):
-            self._left[bi] -= 1
-            if self._left[bi] == 0:
-                lo, hi = self.spans[bi]
-                self._works[bi] = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_GROUP,
-                                                  async_op=True)
-                self.early += 1
-        return fn
-
-    def finish(self):
-        w = world()
-        if w == 1:
-            return
-        if not self.overlap:
-            allreduce_mean_(self.flat)
-            return
-        self.disarm()
-        for bi, wk in enumerate(self._works):
-            lo, hi = self.spans[bi]
-            if wk is None:  # a member received no gradient this step: reduce the bucket now
-                dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=_GROUP)
-            else:
-                wk.wait()
-        _scale_(self.flat, 1.0 / w)
 
 
 def replica_checksums(flats) -> torch.Tensor:

@@ -87,12 +87,10 @@ class CycleGANSystem:
         # identical initial replicas on every rank
         for opt in self.optimizers:
             parallel.broadcast_(opt.flat_p, 0)
-        # G gradient exchange: one all-reduce after the backward by default; with
-        # DUCOSY_GRAD_OVERLAP=1 two buckets (G_B2A's half is final once its one backward call has
-        # run and goes out while the G_A2B backward of the batched [real_A; real_B] call is
-        # still computing)
-        self._g_sync = parallel.GradBuckets(self.optimizer_G.flat_g,
-                                            [list(self.G_A2B.parameters()), list(self.G_B2A.parameters())])
+        # the broadcast wrote every parameter through the flat buffer, behind the parameters' own
+        # version counters: no packed weight built before it may be reused
+        from .hip import ops
+        ops.bump_weights_epoch()
 
     @property
     def models(self):
@@ -150,6 +148,47 @@ class CycleGANSystem:
             coefx.append(cx)
         return bias, coef, coefx
 
+    def g_step_losses(self, planes, grads):
+        """loss_G of trainer.py:469-512 and its terms from the step's planes, plus d(loss_G)/d(plane).
+
+        planes: real_A, real_B, rec_A, rec_B, id_A, id_B, fake_B [N,1,H,W] and dB = D_B(fake_B),
+        dA = D_A(fake_A) [N,1,H/16,W/16]; grads: an output tensor for each plane except the two real
+        ones (written, not added to).  The batch-coupled ContrastRegion / ContrastEdge terms
+        (trainer.py:126-128, 170-180) run their own phases first; every other term is one fused
+        launch (ops.gen_loss_fused) that takes their gradients as addends of fake_B's plane.
+        Returns a device vector of _G_TERMS values."""
+        from .hip import ops
+        from .hip.lib import GL_CA, GL_GRAD, GL_L1, GL_MSEC, GL_SSIM
+        from .losses import _global
+        P = planes
+        real_A, real_B, fake_B = P["real_A"], P["real_B"], P["fake_B"]
+        cr_m, ce_m = self.criterion_contrast_region, self.criterion_contrast_edge
+        if _global(cr_m.global_stats):
+            cr_v, cr_g = ops.loss_contrast_region_global(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight,
+                                                         parallel.allreduce_sum_, parallel.world())
+        else:
+            cr_v, cr_g = ops.loss_contrast_region(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight)
+        if _global(ce_m.global_stats):
+            ce_v, ce_g = ops.loss_contrast_edge_global(fake_B, real_B, parallel.allreduce_sum_, parallel.world())
+        else:
+            ce_v, ce_g = ops.loss_contrast_edge(fake_B, real_B)
+        lc, li = self.lambda_cyc, self.lambda_id
+        rec = dict(flags=GL_L1 | GL_GRAD | GL_SSIM, c_l1=lc / 2, c_grad=LAMBDA_GRAD / 2, c_ssim=-LAMBDA_SSIM / 2)
+        idt = dict(flags=GL_L1 | GL_GRAD, c_l1=li / 2, c_grad=LAMBDA_GRAD_ID / 2)
+        ca_m = self.criterion_contrast_attention
+        assert ca_m.blur_kernel == 7, "fused loss: 7x7 contrast-attention box"
+        jobs = [dict(pred=P["rec_A"], target=real_A, grad=grads["rec_A"], **rec),
+                dict(pred=P["rec_B"], target=real_B, grad=grads["rec_B"], **rec),
+                dict(pred=P["id_A"], target=real_A, grad=grads["id_A"], **idt),
+                dict(pred=P["id_B"], target=real_B, grad=grads["id_B"], **idt),
+                dict(pred=fake_B, target=real_B, source=real_A, grad=grads["fake_B"], flags=GL_CA, c_ca=LAMBDA_CA,
+                     add0=cr_g, c_add0=LAMBDA_CR, add1=ce_g, c_add1=LAMBDA_CE),
+                dict(pred=P["dB"], grad=grads["dB"], flags=GL_MSEC, c_mse=0.5, t_const=1.0),
+                dict(pred=P["dA"], grad=grads["dA"], flags=GL_MSEC, c_mse=0.5, t_const=1.0)]
+        return ops.gen_loss_fused(jobs, self._g_loss_recipe(len(jobs)), extra=(cr_v, ce_v),
+                                  ssim_data_range=self.criterion_ssim.data_range,
+                                  ca=(ca_m.sigma, ca_m.min_weight, ca_m.max_weight))
+
     def _train_step_explicit(self, real_A, real_B, masks=None):
         """trainer.py:463-525 as an explicit schedule: the Generator / Discriminator forward and
         backward functions of modules/hip/networks.py called directly, every loss term of the G
@@ -160,8 +199,7 @@ class CycleGANSystem:
         in-place adds.  Same math and values as _train_step_autograd."""
         from .hip import networks as net
         from .hip import ops
-        from .hip.lib import GL_CA, GL_GRAD, GL_L1, GL_MSEC, GL_SSIM
-        from .losses import _global
+        from .hip.lib import GL_MSEC
         N = real_A.shape[0]
         G_AB, G_BA, D_A, D_B = self.models
         nb, cb = G_AB.num_residual_blocks, G_AB.use_cbam
@@ -184,37 +222,14 @@ class CycleGANSystem:
             dA, S_dA = net.discriminator_forward(pDA, fake_A, True)
             rec_B, S_rb = net.generator_forward(pAB, fake_A, masks, nb, cb, True)
             S_ab["out"], S_ba["out"], S_rb["out"] = ab, ba, rec_B
-            # batch-coupled terms (trainer.py:126-128, 170-180): their own phases, value + gradient
-            cr_m, ce_m = self.criterion_contrast_region, self.criterion_contrast_edge
-            if _global(cr_m.global_stats):
-                cr_v, cr_g = ops.loss_contrast_region_global(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight,
-                                                             parallel.allreduce_sum_, parallel.world())
-            else:
-                cr_v, cr_g = ops.loss_contrast_region(fake_B, real_B, real_A, cr_m.threshold, cr_m.weight)
-            if _global(ce_m.global_stats):
-                ce_v, ce_g = ops.loss_contrast_edge_global(fake_B, real_B, parallel.allreduce_sum_, parallel.world())
-            else:
-                ce_v, ce_g = ops.loss_contrast_edge(fake_B, real_B)
-            # every other term: one fused launch, writing d(loss_G)/d(plane) for each plane
+            # every loss term of loss_G, and d(loss_G)/d(plane) written into each plane's slice
             d_ab, d_ba, d_rb = torch.empty_like(ab), torch.empty_like(ba), torch.empty_like(rec_B)
             d_dB, d_dA = torch.empty_like(dB), torch.empty_like(dA)
-            lc, li = self.lambda_cyc, self.lambda_id
-            rec = dict(flags=GL_L1 | GL_GRAD | GL_SSIM, c_l1=lc / 2, c_grad=LAMBDA_GRAD / 2, c_ssim=-LAMBDA_SSIM / 2)
-            idt = dict(flags=GL_L1 | GL_GRAD, c_l1=li / 2, c_grad=LAMBDA_GRAD_ID / 2)
-            ca_m = self.criterion_contrast_attention
-            assert ca_m.blur_kernel == 7, "fused loss: 7x7 contrast-attention box"
-            jobs = [dict(pred=rec_A, target=real_A, grad=d_ba[2 * N:], **rec),
-                    dict(pred=rec_B, target=real_B, grad=d_rb, **rec),
-                    dict(pred=id_A, target=real_A, grad=d_ba[N:2 * N], **idt),
-                    dict(pred=id_B, target=real_B, grad=d_ab[N:], **idt),
-                    dict(pred=fake_B, target=real_B, source=real_A, grad=d_ab[:N], flags=GL_CA, c_ca=LAMBDA_CA,
-                         add0=cr_g, c_add0=LAMBDA_CR, add1=ce_g, c_add1=LAMBDA_CE),
-                    dict(pred=dB, grad=d_dB, flags=GL_MSEC, c_mse=0.5, t_const=1.0),
-                    dict(pred=dA, grad=d_dA, flags=GL_MSEC, c_mse=0.5, t_const=1.0)]
-            vals = ops.gen_loss_fused(jobs, self._g_loss_recipe(len(jobs)), extra=(cr_v, ce_v),
-                                      ssim_data_range=self.criterion_ssim.data_range,
-                                      ca=(ca_m.sigma, ca_m.min_weight, ca_m.max_weight))
-            del cr_g, ce_g
+            vals = self.g_step_losses(
+                dict(real_A=real_A, real_B=real_B, rec_A=rec_A, rec_B=rec_B, id_A=id_A, id_B=id_B, fake_B=fake_B,
+                     dB=dB, dA=dA),
+                dict(rec_A=d_ba[2 * N:], rec_B=d_rb, id_A=d_ba[N:2 * N], id_B=d_ab[N:], fake_B=d_ab[:N],
+                     dB=d_dB, dA=d_dA))
             # backward: D input gradients (no D parameter gradients in the G step), then the three
             # Generator calls in reverse; planes with two consumers get the second by an add
             dxB, _ = net.discriminator_backward(S_dB, d_dB, True, False)
@@ -281,12 +296,8 @@ class CycleGANSystem:
         loss_G = (loss_GAN + self.lambda_cyc * loss_cycle + self.lambda_id * loss_id
                   + LAMBDA_GRAD * loss_grad_cycle + LAMBDA_GRAD_ID * loss_grad_id + LAMBDA_SSIM * loss_ssim
                   + LAMBDA_CA * loss_ca + LAMBDA_CR * loss_cr + LAMBDA_CE * loss_ce)
-        self._g_sync.arm()
-        try:
-            loss_G.backward()
-        finally:
-            self._g_sync.disarm()  # no hook outlives a backward that raised
-        self._g_sync.finish()  # replica mean of the G gradient
+        loss_G.backward()
+        parallel.allreduce_mean_(self.optimizer_G.flat_g)  # replica mean of the G gradient
         self.optimizer_G.step()
 
         # --- Discriminator steps (trainer.py:517-525), real and fake batched ---
@@ -326,81 +337,26 @@ class CycleGANSystem:
 class ConcurrentCycleGANs:
     """Several CycleGANSystems trained in the same process (BASELINE config 5: the soft-tissue
     (cin 3) and lung (cin 2) models; the reference trains them one after the other,
-    train.py:27-38).
+    train.py:27-38): each step runs the systems one after the other on the caller's stream.
 
-    schedule "serial" (default, the recommended one): the systems step one after the other on the
-    caller's stream.
-    schedule "concurrent" (EXPERIMENTAL; warns on construction): one HIP stream per system, each confined to its own contiguous,
-    pair-aligned share of the compute units (dcs_stream_create_cu_mask); the kernels of one model
-    fill the gaps of the other (small normalisation / loss / Adam launches, split-K reductions,
-    launch latency).  Workspaces are per stream (ops.workspace).  The CU partition is what makes
-    it exact: when the two streams share compute-unit pairs, a model's numbers sometimes leave
-    its sequential run (Config 5: 30/74 repetitions on shared CUs, 10/32 with the
-    models on alternating CUs, 0/74 on disjoint halves, 0/32 on interleaved 8-CU blocks).  With
-    the partition each model equals its own sequential run bit for bit in every operand mode
-    (tests/test_gpu_concurrent.py), but the partition avoids a hazard whose mechanism is
-    inferred, not proven, so the schedule stays experimental.  On 8 GPUs the config-5 schedule is "groups" (bench.py
-    --dual-schedule groups, modules/parallel.py): each model on its own half of the ranks."""
+    A two-stream schedule (one HIP stream per model, each on its own compute-unit partition) was
+    built and measured in rounds 1-3: 1.8 % faster than this one (32.77 vs 32.19 img/s, f16x3) and
+    exact only with pair-aligned CU partitions, because streams whose waves share a compute-unit
+    pair sometimes gave wrong results (Config 5).  It is not part of the product.
+    On 8 GPUs config 5 runs as split GPU groups (bench.py --dual-schedule groups,
+    modules/parallel.py split_groups): each model on its own half of the ranks."""
 
     def __init__(self, systems, device, schedule="serial"):
-        if schedule not in ("concurrent", "serial"):
-            raise ValueError("schedule must be 'concurrent' or 'serial'")
+        if schedule != "serial":
+            raise ValueError("ConcurrentCycleGANs: the only schedule is 'serial' (DESIGN.md §3, Config 5)")
         self.systems = list(systems)
         self.device = torch.device(device)
         self.schedule = schedule
-        if schedule == "concurrent":
-            import warnings
-            warnings.warn("ConcurrentCycleGANs(schedule='concurrent') is experimental: it relies on CU-partitioned "
-                          "streams to avoid a cross-stream hazard (DESIGN.md §3); 'serial' is the recommended "
-                          "schedule", RuntimeWarning, stacklevel=2)
-        self.streams = [self._cu_stream(i, len(self.systems)) for i in range(len(self.systems))] \
-            if schedule == "concurrent" else []
-
-    # CU-mask streams live for the whole process, one per (device, partition): the caching
-    # allocator keeps blocks tagged with a stream after the runner that used it is gone, so the
-    # streams are never destroyed, and repeated runners reuse them
-    _CU_STREAMS = {}
-
-    def _cu_stream(self, i, n):
-        import ctypes
-        from .hip import lib
-        key = (self.device.index, i, n)
-        if key not in ConcurrentCycleGANs._CU_STREAMS:
-            with torch.cuda.device(self.device):
-                ncu = lib.load().dcs_device_cu_count()
-                if ncu < 2 * n:
-                    raise RuntimeError(f"concurrent schedule: {ncu} compute units for {n} streams")
-                lo, hi = (i * ncu // n) & ~1, ((i + 1) * ncu // n) & ~1 if i + 1 < n else ncu
-                words = (ncu + 31) // 32
-                mask = (ctypes.c_uint32 * words)()
-                for cu in range(lo, hi):
-                    mask[cu // 32] |= 1 << (cu % 32)
-                raw = ctypes.c_void_p()
-                lib.call("dcs_stream_create_cu_mask", mask, words, ctypes.byref(raw))
-            ConcurrentCycleGANs._CU_STREAMS[key] = torch.cuda.ExternalStream(raw.value, device=self.device)
-        return ConcurrentCycleGANs._CU_STREAMS[key]
 
     def train_step(self, batches):
         """batches: one (real_A, real_B, masks) per system.  Returns one loss dict per system
-        (device tensors, ready once the streams are synchronised with the caller's)."""
-        if self.schedule == "serial":
-            return [sysm.train_step(*b) for sysm, b in zip(self.systems, batches)]
-        cur = torch.cuda.current_stream(self.device)
-        # one event for the inputs: the CU-mask streams are blocking streams, so a command on a
-        # legacy-null caller stream between the two models' launches would serialise them
-        ready = torch.cuda.Event()
-        ready.record(cur)
-        out = []
-        for sysm, st, b in zip(self.systems, self.streams, batches):
-            st.wait_event(ready)
-            with torch.cuda.stream(st):
-                for t in b:
-                    if t is not None:
-                        t.record_stream(st)
-                out.append(sysm.train_step(*b))
-        for st in self.streams:
-            cur.wait_stream(st)
-        return out
+        (device tensors)."""
+        return [sysm.train_step(*b) for sysm, b in zip(self.systems, batches)]
 
 
 # -------------------------------------------------------------------------------------------

@@ -262,6 +262,33 @@ LAMBDA_GRAD, LAMBDA_GRAD_ID, LAMBDA_SSIM = 5.0, 2.5, 2.0          # trainer.py:4
 LAMBDA_CA, LAMBDA_CR, LAMBDA_CE = 2.0, 1.5, 1.0                    # trainer.py:500-502
 
 
+def g_loss_terms(real_A, real_B, rec_A, rec_B, id_A, id_B, fake_B, dB, dA, lambda_cyc=10.0,
+                 lambda_id=5.0, loss_GAN=None) -> Dict[str, torch.Tensor]:
+    """loss_G of modules/trainer.py:469-512 and its nine terms from the step's planes (id, cycle
+    and fake images [N,1,H,W]; dB = D_B(fake_B), dA = D_A(fake_A) [N,1,H/16,W/16]).  loss_id is
+    trainer.py:474-476, loss_GAN :477-480 (labels of ones, :459), loss_cycle :485-487, the
+    gradient terms :490-492, SSIM :494-496, the contrast terms :498-502 (instantiated :356-358).
+    ``loss_GAN`` given: use it instead of the MSE of dB / dA."""
+    loss_id = (l1(id_A, real_A) + l1(id_B, real_B)) / 2
+    if loss_GAN is None:
+        loss_GAN = (mse(dB, torch.ones_like(dB)) + mse(dA, torch.ones_like(dA))) / 2
+    loss_cycle = (l1(rec_A, real_A) + l1(rec_B, real_B)) / 2
+    loss_grad_cycle = (gradient_loss(rec_A, real_A) + gradient_loss(rec_B, real_B)) / 2
+    loss_grad_id = (gradient_loss(id_A, real_A) + gradient_loss(id_B, real_B)) / 2
+    loss_ssim = 1 - (ssim(rec_A, real_A) + ssim(rec_B, real_B)) / 2
+    loss_ca = contrast_attention_loss(fake_B, real_B, real_A, 0.15, 1.0, 3.0, 7)
+    loss_cr = contrast_region_loss(fake_B, real_B, real_A, 0.15, 1.5)
+    loss_ce = contrast_edge_loss(fake_B, real_B, real_A)
+    loss_G = (loss_GAN + lambda_cyc * loss_cycle + lambda_id * loss_id
+              + LAMBDA_GRAD * loss_grad_cycle + LAMBDA_GRAD_ID * loss_grad_id
+              + LAMBDA_SSIM * loss_ssim + LAMBDA_CA * loss_ca + LAMBDA_CR * loss_cr
+              + LAMBDA_CE * loss_ce)
+    return {"loss_G": loss_G, "loss_GAN": loss_GAN, "loss_cycle": loss_cycle, "loss_id": loss_id,
+            "loss_grad_cycle": loss_grad_cycle, "loss_grad_id": loss_grad_id, "loss_ssim": loss_ssim,
+            "loss_contrast_attention": loss_ca, "loss_contrast_region": loss_cr,
+            "loss_contrast_edge": loss_ce}
+
+
 class OracleCycleGAN:
     """Four parameter dicts + three torch.optim.Adam, exactly as trainer.py:327-367 builds them."""
 
@@ -293,21 +320,12 @@ class OracleCycleGAN:
         self.opt_G.zero_grad()
         fake_B, fake_A = self.G(self.G_AB, rA_in), self.G(self.G_BA, rB_in)
         id_A, id_B = self.G(self.G_BA, rA_in), self.G(self.G_AB, rB_in)
-        loss_id = (l1(id_A, real_A) + l1(id_B, real_B)) / 2
         loss_GAN = (mse(discriminator_forward(self.D_B, fake_B), valid)
                     + mse(discriminator_forward(self.D_A, fake_A), valid)) / 2
         rec_A, rec_B = self.G(self.G_BA, cat(fake_B)), self.G(self.G_AB, cat(fake_A))
-        loss_cycle = (l1(rec_A, real_A) + l1(rec_B, real_B)) / 2
-        loss_grad_cycle = (gradient_loss(rec_A, real_A) + gradient_loss(rec_B, real_B)) / 2
-        loss_grad_id = (gradient_loss(id_A, real_A) + gradient_loss(id_B, real_B)) / 2
-        loss_ssim = 1 - (ssim(rec_A, real_A) + ssim(rec_B, real_B)) / 2
-        loss_ca = contrast_attention_loss(fake_B, real_B, real_A, 0.15, 1.0, 3.0, 7)
-        loss_cr = contrast_region_loss(fake_B, real_B, real_A, 0.15, 1.5)
-        loss_ce = contrast_edge_loss(fake_B, real_B, real_A)
-        loss_G = (loss_GAN + self.lambda_cyc * loss_cycle + self.lambda_id * loss_id
-                  + LAMBDA_GRAD * loss_grad_cycle + LAMBDA_GRAD_ID * loss_grad_id
-                  + LAMBDA_SSIM * loss_ssim + LAMBDA_CA * loss_ca + LAMBDA_CR * loss_cr
-                  + LAMBDA_CE * loss_ce)
+        T = g_loss_terms(real_A, real_B, rec_A, rec_B, id_A, id_B, fake_B, None, None,
+                         self.lambda_cyc, self.lambda_id, loss_GAN=loss_GAN)
+        loss_G = T["loss_G"]
         loss_G.backward()
         self.opt_G.step()
 
@@ -321,12 +339,9 @@ class OracleCycleGAN:
                     + mse(discriminator_forward(self.D_B, fake_B.detach()), fake)) / 2
         loss_D_B.backward()
         self.opt_DB.step()
-        f = lambda t: float(t.detach())
-        return {"loss_G": f(loss_G), "loss_GAN": f(loss_GAN), "loss_cycle": f(loss_cycle),
-                "loss_id": f(loss_id), "loss_grad_cycle": f(loss_grad_cycle),
-                "loss_grad_id": f(loss_grad_id), "loss_ssim": f(loss_ssim),
-                "loss_contrast_attention": f(loss_ca), "loss_contrast_region": f(loss_cr),
-                "loss_contrast_edge": f(loss_ce), "loss_D_A": f(loss_D_A), "loss_D_B": f(loss_D_B)}
+        out = {k: float(v.detach()) for k, v in T.items()}
+        out.update(loss_D_A=float(loss_D_A.detach()), loss_D_B=float(loss_D_B.detach()))
+        return out
 
 
 def lr_lambda(epoch: int, epochs: int, decay_epoch: int) -> float:

@@ -4,10 +4,9 @@
   0-1, lung model on ranks 2-3): inside each group the all-reduce-mean of the shard gradients
   equals that model's full-batch gradient (oracle Generator, per-sample losses), and the
   rank-0 broadcast gives each group its own first rank's weights;
-* world 2: GradBuckets (trainer.py's G exchange) equals one all-reduce-mean of the whole flat
-  buffer, with a parameter reached by two graph branches (as G_A2B's weights are) and one
-  reached once: by default after the backward (no bucket goes out from inside it), and with
-  overlap on both buckets go out from inside the backward; a second arm() does not stack hooks;
+* world 2: trainer.py's G exchange (parallel.allreduce_mean_ of FusedAdam's flat gradient after
+  the backward) gives every rank the replica mean, with a parameter reached by two graph
+  branches (as G_A2B's weights are) and one reached once;
 * world 2: parallel.replicas_identical (bench.py's "replicas_identical") is True for equal
   replicas and False when one replica differs by one ulp in one element.
 """
@@ -75,7 +74,7 @@ def _groups_worker(rank, world, port, q):
         raise
 
 
-def _buckets_worker(rank, world, port, q, overlap):
+def _flat_mean_worker(rank, world, port, q):
     _setup(rank, world, port)
     from modules import parallel
     try:
@@ -84,24 +83,19 @@ def _buckets_worker(rank, world, port, q, overlap):
         a = torch.nn.Parameter(torch.arange(4.0))
         b = torch.nn.Parameter(torch.arange(6.0) - 2)
         a.grad, b.grad = flat[:4].view(4), flat[4:].view(6)
-        sync = parallel.GradBuckets(flat, [[a], [b]], overlap=overlap)
         x = torch.tensor(float(rank + 1))
-        sync.arm()
-        sync.arm()  # re-arming replaces the hooks (a stale set would reduce buckets early)
         # a is used by two graph branches that reach it separately (two accumulations)
         la = (a * x).sum()
         lb = (a * a * x).sum() + (b.square() * x).sum()
         torch.autograd.backward([la, lb])
-        early = sync.early
-        sync.finish()
-        sums = [sum(r + 1.0 for r in range(world))]
-        xm = sums[0] / world
+        parallel.allreduce_mean_(flat)
+        xm = sum(r + 1.0 for r in range(world)) / world
         want = torch.cat([xm * (1 + 2 * torch.arange(4.0)), xm * 2 * (torch.arange(6.0) - 2)])
-        q.put((rank, float((flat - want).abs().max()), early))
+        q.put((rank, float((flat - want).abs().max())))
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
     except Exception as e:
-        q.put((-1, repr(e), 0))
+        q.put((-1, repr(e)))
         raise
 
 
@@ -145,13 +139,10 @@ def test_split_groups_world4():
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("overlap", [False, True])
-def test_grad_buckets_world2(overlap):
-    res = _run(_buckets_worker, 2, 2, overlap)
+def test_flat_grad_mean_world2():
+    res = _run(_flat_mean_worker, 2, 2)
     for r in res:
-        assert r[0] >= 0, r
-        # overlap: both buckets launched from inside the backward; default: none (one all-reduce after it)
-        assert r[1] < 1e-6 and r[2] == (2 if overlap else 0), r
+        assert r[0] >= 0 and r[1] < 1e-6, r
 
 
 @pytest.mark.timeout(300)

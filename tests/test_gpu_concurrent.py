@@ -1,12 +1,23 @@
-"""Concurrent training of two CycleGANs on two HIP streams (BASELINE config 5: soft-tissue cin 3
-and lung cin 2 models; modules/trainer.py ConcurrentCycleGANs) gives each model exactly the
-losses and weights of a sequential run: the kernels are deterministic and every stream has its
-own workspace."""
+"""BASELINE config 5 on one GPU: the soft-tissue (cin 3) and lung (cin 2) CycleGANs trained in one
+process (modules/trainer.py ConcurrentCycleGANs, serial schedule; the reference trains them one
+after the other, train.py:27-38).
+
+* each model gets exactly the losses and weights of its own run, in the default operand mode and
+  in config 5's fp16 MFMA mode (the kernels are deterministic; the models share only workspaces);
+* in the fp16 mode both models of the pair hold the fp16 bar of tests/test_gpu_train.py (5e-3 on
+  step-0 losses, the 1e-2 envelope after): the soft-tissue model against the reference-generated
+  step fixture (tests/golden/steps_64.npz), the lung model against the oracle (no reference
+  fixture has a cin-2 step)."""
+import os
+
+import numpy as np
 import pytest
 import torch
 
+from conftest import GOLDEN
 from oracle import prng
-from test_gpu_train import _system
+from oracle import ref_torch as orc
+from test_gpu_train import _sd, _system
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -19,55 +30,62 @@ def _batch(seed, i, n, hw, cin):
     return rA, rB, mk
 
 
-# fresh repetitions of the concurrent run: with the two streams sharing compute-unit pairs, 6-45 %
-# of such repetitions left the sequential numbers in bf16x6 (scripts/conc_cumask.py,
-# profiles/r02e_hazard_cumask.md); the CU-partitioned streams of ConcurrentCycleGANs never did
-@pytest.mark.parametrize("mode,reps", [("f32", 1), ("bf16x6", 2), ("f16x3", 4)])
-def test_concurrent_equals_sequential(mode, reps):
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+def test_serial_schedule_equals_independent_runs(mode):
+    """The serial schedule (both models on the caller's stream) gives each model exactly the numbers
+    of its own run."""
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
-    n, hw, nb, steps = 2, 64, 2, 3
-    cfg = [(3, 801), (2, 802)]
+    n, hw, nb, steps = 2, 64, 2, 2
+    cfg = [(3, 811), (2, 812)]
     prev = ops.get_mma()
     ops.set_mma(mode)
-    side = torch.cuda.Stream()  # the caller's stream: the legacy null stream stays idle
     try:
-        with torch.cuda.stream(side):
-            batches = [[_batch(s, i, n, hw, c) for i in range(steps)] for c, s in cfg]
-            seq = [_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg]
-            want = [[{k: float(v) for k, v in m.train_step(*batches[j][i]).items()} for i in range(steps)]
-                    for j, m in enumerate(seq)]
-            for rep in range(reps):
-                run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV,
-                                          schedule="concurrent")
-                torch.cuda.synchronize()
-                got = [[], []]
-                for i in range(steps):
-                    outs = run.train_step([batches[j][i] for j in range(len(cfg))])
-                    torch.cuda.synchronize()
-                    for j, o in enumerate(outs):
-                        got[j].append({k: float(v) for k, v in o.items()})
-                assert got == want, f"repetition {rep}"
-                for a, b in zip(seq, run.systems):
-                    assert torch.equal(a.optimizer_G.flat_p, b.optimizer_G.flat_p)
-                    assert torch.equal(a.optimizer_D_A.flat_p, b.optimizer_D_A.flat_p)
+        want = []
+        for c, s in cfg:
+            m = _system(c, nb, prng.step_model_seeds(s))
+            want.append([{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()}
+                         for i in range(steps)])
+        run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV)
+        got = [[], []]
+        for i in range(steps):
+            for j, o in enumerate(run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])):
+                got[j].append({k: float(v) for k, v in o.items()})
+        assert got == want
     finally:
         ops.set_mma(prev)
 
 
-def test_serial_schedule_equals_independent_runs():
-    """The serial schedule (both models on the caller's stream, default operand mode) gives each
-    model exactly the numbers of its own run."""
+def test_dual_f16_vs_reference():
+    from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
-    n, hw, nb, steps = 2, 64, 2, 2
-    cfg = [(3, 811), (2, 812)]
-    want = []
-    for c, s in cfg:
-        m = _system(c, nb, prng.step_model_seeds(s))
-        want.append([{k: float(v) for k, v in m.train_step(*_batch(s, i, n, hw, c)).items()} for i in range(steps)])
-    run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV, schedule="serial")
-    got = [[], []]
-    for i in range(steps):
-        for j, o in enumerate(run.train_step([_batch(s, i, n, hw, c) for c, s in cfg])):
-            got[j].append({k: float(v) for k, v in o.items()})
-    assert got == want
+    z = np.load(os.path.join(GOLDEN, "steps_64.npz"))
+    n, hw, nb, cin, steps, seed = [int(v) for v in z["meta"]]
+    lung_seed = 813
+    ls = prng.step_model_seeds(lung_seed)
+    gs, ds = orc.generator_param_shapes(2, nb, True), orc.discriminator_param_shapes(1)
+    oracle = orc.OracleCycleGAN(_sd(gs, ls["G_A2B"]), _sd(gs, ls["G_B2A"]), _sd(ds, ls["D_A"]),
+                                _sd(ds, ls["D_B"]), nb)
+    prev = ops.get_mma()
+    ops.set_mma("f16")
+    try:
+        run = ConcurrentCycleGANs([_system(cin, nb, prng.step_model_seeds(seed)),
+                                   _system(2, nb, ls)], DEV)
+        lung0 = None
+        for i in range(steps):
+            soft = _batch(seed, i, n, hw, cin)
+            lung = _batch(lung_seed, i, n, hw, 2)
+            want_lung = oracle.step(*(t.cpu() for t in lung))
+            lung0 = lung0 or want_lung
+            out_soft, out_lung = ({k: float(v) for k, v in o.items()} for o in run.train_step([soft, lung]))
+            tol = 5e-3 if i == 0 else 1e-2
+            for k, v in out_soft.items():
+                ref = float(z[k][i])
+                scale = ref if i == 0 else max(abs(ref), abs(float(z[k][0])))
+                assert abs(v - ref) <= tol * max(abs(scale), 1e-2), ("soft", i, k, v, ref)
+            for k, v in out_lung.items():
+                ref = want_lung[k]
+                scale = max(abs(ref), abs(lung0[k]))  # a term may shrink to a near-cancellation
+                assert abs(v - ref) <= tol * max(scale, 1e-2), ("lung", i, k, v, ref)
+    finally:
+        ops.set_mma(prev)

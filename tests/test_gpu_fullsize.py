@@ -9,8 +9,13 @@ the CPU oracle (oracle/ref_torch.py, pinned to the reference by the golden fixtu
   * BASELINE config 3's loss kernels at bs 8 on planes the HIP Generator produced: every loss term
     of trainer.py:469-512 and its d/dpred, including the batch-coupled ContrastRegion mean / std
     (trainer.py:126-128) and ContrastEdge mean / std / top-10 % at k = 209,715 (trainer.py:170-180);
-  * BASELINE config 3: two full training steps of one slice (every loss term within 1e-3 at step 0,
-    whose losses are pure forward, 2e-3 after one Adam update);
+  * BASELINE config 3's production loss path at bs 8: CycleGANSystem.g_step_losses (the
+    ContrastRegion / ContrastEdge phases and the fused loss launch with the trainer's seven-job
+    recipe) on planes from the HIP networks, every composed value of loss_G and each plane's combined
+    d(loss_G)/d(plane) against oracle autograd of loss_G (trainer.py:469-512) restricted to the planes;
+  * BASELINE config 3 (soft tissue, cin 3) and the lung model of config 5 (cin 2, CBAM): two full
+    training steps of one slice (every loss term within 1e-3 at step 0, whose losses are pure
+    forward, 2e-3 after one Adam update);
   * at bs 8: the default operand mode is bit-reproducible and within 1e-4 of the exact-f32 path on
     every loss term (both are fp32-class; the difference is accumulation order)."""
 import pytest
@@ -25,10 +30,10 @@ DEV = "cuda"
 HW, NB, CIN = 512, 9, 3
 
 
-def _inputs(seed, i, n):
+def _inputs(seed, i, n, cin=CIN):
     a = torch.from_numpy(prng.uniform(seed, f"A{i}", (n, 1, HW, HW), -1, 1))
     b = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, HW, HW), -1, 1))
-    m = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, CIN - 1, HW, HW), 0.3))
+    m = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, HW, HW), 0.3))
     return a, b, m
 
 
@@ -138,18 +143,49 @@ def test_fullsize_losses_bs8_vs_oracle():
     print("config 3 losses at bs 8, 512x512 (value rel, grad rel L2):", res)
 
 
-def test_fullsize_steps_match_oracle():
+def test_fullsize_g_step_losses_bs8_vs_oracle():
+    """The production G-step loss path at BASELINE config 3's batch (bs 8, 512 x 512): values of
+    loss_G and its nine terms within 1e-5 relative, d(loss_G)/d(plane) of the seven loss planes
+    within relative L2 1e-4, against oracle autograd of trainer.py:469-512 on the same planes."""
+    from modules import trainer
+    torch.set_num_threads(16)
+    n, seed = 8, 915
+    s = _system(CIN, NB, prng.step_model_seeds(seed))
+    a, b, m = (x.to(DEV) for x in _inputs(seed, 0, n))
+    with torch.no_grad():  # the reference's calls, trainer.py:466-481
+        fake_B, fake_A = s.G_A2B(a, m), s.G_B2A(b, m)
+        id_A, id_B = s.G_B2A(a, m), s.G_A2B(b, m)
+        rec_A, rec_B = s.G_B2A(fake_B, m), s.G_A2B(fake_A, m)
+        dB, dA = s.D_B(fake_B), s.D_A(fake_A)
+    planes = dict(real_A=a, real_B=b, rec_A=rec_A, rec_B=rec_B, id_A=id_A, id_B=id_B, fake_B=fake_B, dB=dB, dA=dA)
+    grads = {k: torch.empty_like(v) for k, v in planes.items() if not k.startswith("real")}
+    vals = s.g_step_losses(planes, grads).double().cpu()
+    cpu = {k: v.cpu().clone().requires_grad_(not k.startswith("real")) for k, v in planes.items()}
+    T = orc.g_loss_terms(cpu["real_A"], cpu["real_B"], cpu["rec_A"], cpu["rec_B"], cpu["id_A"], cpu["id_B"],
+                         cpu["fake_B"], cpu["dB"], cpu["dA"], s.lambda_cyc, s.lambda_id)
+    T["loss_G"].backward()
+    ev = {k: _rel(float(vals[i]), float(T[k])) for i, k in enumerate(trainer._G_TERMS)}
+    eg = {k: _rel_l2(grads[k].cpu(), cpu[k].grad) for k in grads}
+    print("g_step_losses at bs 8, 512x512: value rel", max(ev.values()), "grad rel L2", eg)
+    assert max(ev.values()) <= 1e-5, ev
+    assert max(eg.values()) <= 1e-4, eg
+
+
+@pytest.mark.parametrize("cin", [3, 2])
+def test_fullsize_steps_match_oracle(cin):
+    """Two training steps at 512 x 512, bs 1, 9 blocks, CBAM: the soft-tissue model (cin 3,
+    BASELINE config 3) and the lung model of config 5 (cin 2: image + lung mask)."""
     from modules.hip import ops
-    seed = 901
+    seed = 901 if cin == 3 else 903
     seeds = prng.step_model_seeds(seed)
     torch.set_num_threads(16)
-    gs, ds = orc.generator_param_shapes(CIN, NB, True), orc.discriminator_param_shapes(1)
+    gs, ds = orc.generator_param_shapes(cin, NB, True), orc.discriminator_param_shapes(1)
     oracle = orc.OracleCycleGAN(_sd(gs, seeds["G_A2B"]), _sd(gs, seeds["G_B2A"]), _sd(ds, seeds["D_A"]),
                                 _sd(ds, seeds["D_B"]), NB)
-    gpu = _system(CIN, NB, seeds)
+    gpu = _system(cin, NB, seeds)
     worst = {}
     for i in range(2):
-        a, b, m = _inputs(seed, i, 1)
+        a, b, m = _inputs(seed, i, 1, cin)
         want = oracle.step(a, b, m)
         got = {k: float(v) for k, v in gpu.train_step(a.to(DEV), b.to(DEV), m.to(DEV)).items()}
         # step 1 follows one Adam update (measured 2.9e-4; the CPU reference itself moves ~2e-4 on the
@@ -158,8 +194,8 @@ def test_fullsize_steps_match_oracle():
         for k, ref in want.items():
             e = _rel(got[k], float(ref))
             worst[(i, k)] = e
-            assert e <= tol, (ops.get_mma(), i, k, got[k], float(ref), e)
-    print("fullsize vs oracle, worst relative error per step:",
+            assert e <= tol, (ops.get_mma(), cin, i, k, got[k], float(ref), e)
+    print(f"fullsize cin {cin} vs oracle, worst relative error per step:",
           {i: max(v for (j, _), v in worst.items() if j == i) for i in range(2)})
 
 

@@ -3,8 +3,8 @@
 Every tensor the product code allocates through torch.empty / empty_like / zeros / zeros_like /
 ones on the device (kernel outputs, padded dgrad buffers, split-K partial slabs, the per-stream
 workspaces) is carved out of a larger buffer whose 4 KiB on either side is filled with a canary
-byte.  One step of two CycleGANs on two HIP streams (config 5's concurrent schedule) and one
-single-stream step run with every allocation guarded, in f32 and bf16x6;
+byte.  One step of the two CycleGANs of config 5 (serial schedule) runs with every allocation guarded,
+in the f16x3, f16 and bf16x6 operand modes;
 afterwards every guard band must still hold the canary: no kernel stores outside the extent its
 host code allocated for it (the two-stream audit).
 """
@@ -90,8 +90,8 @@ class _Guarded:
         return bad
 
 
-@pytest.mark.parametrize("schedule,mode", [("concurrent", "f32"), ("concurrent", "f16x3"), ("serial", "f16x3"), ("serial", "bf16x6")])
-def test_no_store_outside_allocations(schedule, mode):
+@pytest.mark.parametrize("mode", ["f16x3", "f16", "bf16x6"])
+def test_no_store_outside_allocations(mode):
     from modules.hip import ops
     from modules.trainer import ConcurrentCycleGANs
     n, hw, nb = 2, 64, 2
@@ -100,7 +100,7 @@ def test_no_store_outside_allocations(schedule, mode):
     ops.set_mma(mode)
     saved_ws = dict(ops._WS)
     try:
-        run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV, schedule=schedule)
+        run = ConcurrentCycleGANs([_system(c, nb, prng.step_model_seeds(s)) for c, s in cfg], DEV)
         batches = [_batch(s, 0, n, hw, c) for c, s in cfg]
         torch.cuda.synchronize()
         ops._WS.clear()  # workspaces are re-created (guarded) inside the step

@@ -198,3 +198,29 @@ def test_explicit_step_matches_autograd_step():
         d = (pe[k] - pa[k]).abs().flatten()
         assert d.median().item() <= 1e-6 and d.max().item() <= 2 * lr * 2 + 1e-6, (k, d.max().item())
 
+
+
+def test_fused_grad_adds_to_an_autograd_contribution():
+    """A parameter whose freshly zeroed .grad received an ordinary autograd contribution first (here
+    an L2 penalty, accumulated in place by AccumulateGrad) keeps it: the fused Discriminator
+    backward adds its own gradient instead of writing over the buffer (modules/optim.py zero_grad's
+    stamp, modules/hip/networks.py _GradSink).  Reference: plain accumulation without FusedAdam."""
+    from modules.model import Discriminator
+    from modules.optim import FusedAdam
+    torch.manual_seed(5)
+    x = torch.rand(2, 1, 64, 64, device=DEV)
+    sd = Discriminator().state_dict()
+    grads = []
+    for fused in (True, False):
+        D = Discriminator().to(DEV)
+        D.load_state_dict(sd)
+        if fused:
+            FusedAdam(D.parameters(), lr=2e-4).zero_grad()
+        w = D.model[2].weight
+        (w.square().sum() * 0.5).backward()  # first: AccumulateGrad in place (fused) / fresh .grad
+        D(x).square().mean().backward()       # then the fused backward's contribution
+        grads.append({k: p.grad.detach().clone() for k, p in D.named_parameters()})
+    for k in grads[1]:
+        assert torch.allclose(grads[0][k], grads[1][k], rtol=1e-5, atol=1e-7), k
+    # the penalty's share is there: dL/dw = w + d(D loss)/dw, not the D loss gradient alone
+    assert not torch.allclose(grads[0]["model.2.weight"] - sd["model.2.weight"].to(DEV), grads[0]["model.2.weight"])
