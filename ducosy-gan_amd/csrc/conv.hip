@@ -132,9 +132,6 @@ constexpr int NT = 256;
 #ifndef DCS_X6_V4
 #define DCS_X6_V4 1  // bf16x6 rows also for the 4-channel NHWC gather (stem, PatchGAN layer 0)
 #endif
-#ifndef DCS_ROWS_F32
-#define DCS_ROWS_F32 0  // A/B only: the rows pass ignores the bf16 operand modes (exact f32)
-#endif
 #ifndef DCS_X6_PIPE
 #define DCS_X6_PIPE 1  // bf16x6 rows: global loads two k-tiles ahead (two register sets)
 #endif
@@ -173,9 +170,6 @@ constexpr int NT = 256;
 #endif
 #ifndef DCS_H3_NSUB
 #define DCS_H3_NSUB 2  // f16x3 rows, 128-column tiles: 16-k sub-tiles per barrier (64-column tiles: 1)
-#endif
-#ifndef DCS_H3_BM256_TAG0
-#define DCS_H3_BM256_TAG0 0  // fp16 modes: 256 x 128 tiles for the non-residual 128-column rows passes
 #endif
 #ifndef DCS_WGRAD_X6_V4
 #define DCS_WGRAD_X6_V4 1  // fp16 modes: 4-channel-source weight gradients (stem, PatchGAN layer 0) on the x6 kernel
@@ -1833,196 +1827,6 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// wgrad pass on the bf16 MFMA (dcs_conv_desc.mma = BF16 / BF16X3): regular rows (parity 0),
-// vectorisable sources (Cs % 16 == 0), 128 x 128 tiles.  dW[co][n] = sum_p dy[p][co] x[p][n]
-// with the pixels p as the GEMM reduction.  The bf16 MFMA wants each lane's fragment to be 8
-// consecutive k (here: pixels) of one row, so LDS keeps both operands row-major with the
-// pixels contiguous ([row][32 px (+32 lo) + pad]) and every fragment is one ds_read_b128.
-// Loader: thread (pair q = tid & 63, group g = tid >> 6) reads rows 2q and 2q+1 (one float2)
-// at the 8 consecutive pixels 8g .. 8g+7 of the k-tile and writes them as two bf16x8 rows:
-// no transpose.  The pixel walk is wave-uniform (g is the wave index).
-// ---------------------------------------------------------------------------------------
-template <int MMA, bool UNI>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_mma16_kernel(
-    const dcs_conv_desc din, const float* __restrict__ dy, const float* __restrict__ src,
-    const float* __restrict__ psc, const float* __restrict__ psh, float* __restrict__ ws,
-    int kt_per_split, int gn, int gm) {
-    constexpr int BM = 128, BN = 128, WM = 64, WN = 64, IM = 2, JN = 2, KT2 = 4;
-    constexpr int LDE = lde_bf16<MMA>();
-    __shared__ __attribute__((aligned(16))) __bf16 Ah[2][BM][LDE];
-    __shared__ __attribute__((aligned(16))) __bf16 Bh[2][BN][LDE];
-    const dcs_conv_desc d = din;
-
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int ntile = L % gn;
-    const int mtile = (L / gn) % gm;
-    const int split = L / (gn * gm);
-    const int My = d.Ho, Mx = d.Wo, per = My * Mx;
-    const long long P = (long long)per * d.N;
-    const int Ktot = d.KH * d.KW * d.Cs;
-    const int m0 = mtile * BM, n0 = ntile * BN;
-    const long long nkt_all = (P + BK - 1) / BK;
-    const long long kt_beg = (long long)split * kt_per_split;
-    long long kt_end = kt_beg + kt_per_split;
-    if (kt_end > nkt_all) kt_end = nkt_all;
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    const int q = lane;                                          // row pair
-    const int grp = __builtin_amdgcn_readfirstlane(wid);         // pixel group (wave-uniform)
-    const int am = m0 + 2 * q;                                   // dy channels am, am+1
-    const bool a_ok = am < d.Co;                                 // Co % 4 == 0: both or none
-    const int bn = n0 + 2 * q;                                   // columns bn, bn+1 (same tap)
-    const bool b_ok = bn < Ktot;
-    // UNI (Cs % 128 == 0): the tile's 128 columns share one tap, so the tap and the whole
-    // pixel -> source-coordinate walk below are wave-uniform (scalar); the lane only adds its
-    // channel offset.  Otherwise each lane decodes its own tap.
-    int ady = 0, adx = 0, bchan = 0;
-    if (UNI) {
-        const int j = n0 / d.Cs;
-        bchan = n0 - j * d.Cs + 2 * q;
-        ady = j / d.KW;
-        adx = j - ady * d.KW;
-    } else if (b_ok) {
-        const int j = bn / d.Cs;
-        bchan = bn - j * d.Cs;
-        ady = j / d.KW;
-        adx = j - ady * d.KW;
-    }
-    const int Hv = d.Hs * d.up, Wv = d.Ws * d.up;
-
-    // wave-uniform pixel state of this wave's first pixel in the NEXT k-tile to load
-    int pn = 0, pqy = 0, pqx = 0;
-    {
-        const long long p = kt_beg * BK + 8 * grp;
-        if (p < P) {
-            pn = (int)(p / per);
-            const int rem = (int)(p - (long long)pn * per);
-            pqy = rem / Mx;
-            pqx = rem - pqy * Mx;
-        }
-    }
-    float2 ra[8], rb[8];
-    // branch-free loads through buffer descriptors (OOB offset -> zeros); the host keeps dy and
-    // the source below 2 GiB
-    const __amdgpu_buffer_rsrc_t rdy = src_rsrc(dy), rsrc = src_rsrc(src);
-    auto load = [&](long long kt) {
-        const long long p0 = kt * BK + 8 * grp;
-        int n = pn, qy = pqy, qx = pqx;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const bool pok = p0 + j < P;
-            ra[j] = buf_load2(rdy, (pok && a_ok) ? (int)(((p0 + j) * d.Co + am) * 4) : OOB_OFF);
-            int sy, sx;
-            const bool yok = map_coord_sel(qy * d.stride - d.pt + ady, Hv, d.up, d.pad_mode, sy);
-            const bool xok = map_coord_sel(qx * d.stride - d.pl + adx, Wv, d.up, d.pad_mode, sx);
-            const int base = n * (int)d.s_n + sy * (int)d.s_h + sx * (int)d.s_w;
-            const int so = UNI ? __builtin_amdgcn_readfirstlane(base) : base;
-            const bool ok = pok && b_ok && yok && xok;
-            float2 v = buf_load2(rsrc, ok ? (so + bchan) * 4 : OOB_OFF);
-            if (d.pro_act != DCS_ACT_NONE && ok) {
-                const long long o = (long long)n * d.Cs + bchan;
-                v.x = act_apply(fmaf(v.x, psc[o], psh[o]), d.pro_act);
-                v.y = act_apply(fmaf(v.y, psc[o + 1], psh[o + 1]), d.pro_act);
-            }
-            rb[j] = v;
-            if (++qx == Mx) { qx = 0; if (++qy == My) { qy = 0; ++n; } }
-        }
-        // advance the wave's start by one k-tile (32 pixels)
-        pqx += BK;
-        while (pqx >= Mx) { pqx -= Mx; if (++pqy == My) { pqy = 0; ++pn; } }
-    };
-    // two rows (x, y halves of the float2s) of 8 pixels -> bf16 hi (+ lo) rows
-    auto put2 = [&](const float2 (&r)[8], __bf16 (*T)[LDE], int row) {
-        const float4 x0 = make_float4(r[0].x, r[1].x, r[2].x, r[3].x), x1 = make_float4(r[4].x, r[5].x, r[6].x, r[7].x);
-        const float4 y0 = make_float4(r[0].y, r[1].y, r[2].y, r[3].y), y1 = make_float4(r[4].y, r[5].y, r[6].y, r[7].y);
-        bf16x8 h, l;
-        split8<MMA>(x0, x1, h, l);
-        *reinterpret_cast<bf16x8*>(&T[row][8 * grp]) = h;
-        if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(&T[row][32 + 8 * grp]) = l;
-        split8<MMA>(y0, y1, h, l);
-        *reinterpret_cast<bf16x8*>(&T[row + 1][8 * grp]) = h;
-        if constexpr (MMA == MMA_BF16X3) *reinterpret_cast<bf16x8*>(&T[row + 1][32 + 8 * grp]) = l;
-    };
-    auto store = [&](int buf) {
-        put2(ra, Ah[buf], 2 * q);
-        put2(rb, Bh[buf], 2 * q);
-    };
-
-    floatx16 acc[IM][JN], t[IM][JN];
-#pragma unroll
-    for (int i = 0; i < IM; ++i)
-#pragma unroll
-        for (int j = 0; j < JN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
-
-    if (kt_beg < kt_end) {
-        load(kt_beg);
-        store(0);
-    }
-    __syncthreads();
-    const int l32 = lane & 31, kh = (lane >> 5) * 8;
-    for (long long kt = kt_beg; kt < kt_end; ++kt) {
-        const int cur = (int)((kt - kt_beg) & 1);
-        auto step = [&](int st) {
-            bf16x8 ah[IM], bh[JN], al[IM], bl[JN];
-#pragma unroll
-            for (int i = 0; i < IM; ++i) {
-                const __bf16* a = &Ah[cur][wm * WM + i * 32 + l32][16 * st + kh];
-                ah[i] = *reinterpret_cast<const bf16x8*>(a);
-                if constexpr (MMA == MMA_BF16X3) al[i] = *reinterpret_cast<const bf16x8*>(a + 32);
-            }
-#pragma unroll
-            for (int j = 0; j < JN; ++j) {
-                const __bf16* b = &Bh[cur][wn * WN + j * 32 + l32][16 * st + kh];
-                bh[j] = *reinterpret_cast<const bf16x8*>(b);
-                if constexpr (MMA == MMA_BF16X3) bl[j] = *reinterpret_cast<const bf16x8*>(b + 32);
-            }
-#pragma unroll
-            for (int i = 0; i < IM; ++i)
-#pragma unroll
-                for (int j = 0; j < JN; ++j) {
-                    if constexpr (MMA == MMA_BF16X3) {
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t[i][j], 0, 0, 0);
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t[i][j], 0, 0, 0);
-                    }
-                    t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t[i][j], 0, 0, 0);
-                }
-        };
-        step(0);
-        if (kt + 1 < kt_end) load(kt + 1);
-        step(1);
-        const long long rel = kt - kt_beg;
-        if ((rel % KT2) == KT2 - 1 || kt + 1 == kt_end) {
-#pragma unroll
-            for (int i = 0; i < IM; ++i)
-#pragma unroll
-                for (int j = 0; j < JN; ++j) {
-                    acc[i][j] += t[i][j];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
-                }
-        }
-        if (kt + 1 < kt_end) store(cur ^ 1);
-        __syncthreads();
-    }
-
-    float* slab = ws + (long long)split * d.Co * Ktot;
-#pragma unroll
-    for (int j = 0; j < JN; ++j) {
-        const int col = n0 + wn * WN + j * 32 + l32;
-        if (col >= Ktot) continue;
-#pragma unroll
-        for (int i = 0; i < IM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (row < d.Co) slab[(long long)row * Ktot + col] = acc[i][j][r];
-            }
-    }
-}
 
 // dw[co][ci][ty][tx] = sum_s ws[s][co][(ty*KW+tx)*Cs + ci].  Threads walk the slabs in
 // their own (co, tap, ci) order so the nsplit reads per output are coalesced; each output is
@@ -2414,7 +2218,6 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
                        d.up == 1;
     const bool lrelu = DCS_TAG3 && d.pro_act == DCS_ACT_LRELU && d.epi_act == DCS_ACT_NONE && d.pad_mode == DCS_PAD_ZERO &&
                        d.up == 1;  // TAG 2 instances
-    const ClassGeom g0 = class_geom(d, 0);
 #define DCS_ROWS_X6F(BM_, BN_, VEC_, TAG_, G)                                                                          \
     if (d.mma == MMA_F16X3)                                                                                          \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_F16X3>), G, dim3(2 * BM_), 0, s, d, src, src2, \
@@ -2425,7 +2228,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
     else                                                                                                             \
         hipLaunchKernelGGL((conv_rows_kernel<BM_, BN_, VEC_, TAG_, MMA_BF16X6>), G, dim3(2 * BM_), 0, s, d, src, src2, \
                            wpack, bias, psc, psh, out, gxx, gy, parts, fold_arg);
-    if (vec && x6f && (BN == 128 || DCS_X6_BN64) && !DCS_ROWS_F32) {  // x6 / f16x3: 128- or 64-column tiles
+    if (vec && x6f && (BN == 128 || DCS_X6_BN64)) {  // x6 / f16x3: 128- or 64-column tiles
         // 256-row tiles where they divide the pixels evenly (the forward over whole 128 x 128
         // images); the 130 x 130 padded data gradient keeps 128-row tiles (measured: its partial
         // last dispatch round and zero-padded border rows make the big tile 7 % slower there)
@@ -2436,15 +2239,6 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
             DCS_ROWS_X6F(256, 128, 1, 1, grid2)
             if (bm_used) *bm_used = 256;
         } else if (BN == 128 && res) { DCS_ROWS_X6F(128, 128, 1, 1, grid) }
-        else if (BN == 128 && DCS_H3_BM256_TAG0 && d.mma != MMA_BF16X6 && fold == 0 && Mmax % 256 == 0 &&
-                 (!parts || ((long long)g0.My * g0.Mx) % 256 == 0)) {
-            // fp16 modes: 256-row tiles for the other 128-column layers (half the weight-tile
-            // traffic per output; these passes stream their fp32 operands from L2)
-            gxx = (int)cdiv(Mmax, 256);
-            const dim3 grid2((unsigned)(gxx * gy * ncls));
-            DCS_ROWS_X6F(256, 128, 1, 0, grid2)
-            if (bm_used) *bm_used = 256;
-        }
         else if (BN == 128 && plain) { DCS_ROWS_X6F(128, 128, 1, 2, grid) }
         else if (BN == 128 && lrelu) { DCS_ROWS_X6F(128, 128, 1, 3, grid) }
         else if (BN == 128) { DCS_ROWS_X6F(128, 128, 1, 0, grid) }
@@ -2453,7 +2247,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         else { DCS_ROWS_X6F(128, 64, 1, 0, grid) }
         return check_launch("conv_rows");
     }
-    if (v4 && x6f && DCS_X6_V4 && !DCS_ROWS_F32) {  // 4-channel stem / PatchGAN layer 0
+    if (v4 && x6f && DCS_X6_V4) {  // 4-channel stem / PatchGAN layer 0
         const int gxx = gx;
         const bool stem = DCS_TAG4 && d.KH == 7 && d.KW == 7 && d.Cs == 4 && d.stride == 1 && d.up == 1 && !d.parity &&
                           d.pad_mode == DCS_PAD_REFLECT && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
@@ -2465,7 +2259,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         return check_launch("conv_rows");
     }
 #undef DCS_ROWS_X6F
-    if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && DCS_BF16P_ROWS && !DCS_ROWS_F32 && d.ldb % 48 == 0) {
+    if (vec && d.mma == MMA_BF16 && res && BN == 128 && DCS_BF16P && DCS_BF16P_ROWS && d.ldb % 48 == 0) {
         // residual convs in the half-precision mode: the x6 pipeline, 48 k per barrier; 256-row
         // tiles where they divide the pixels (the forward)
         if (DCS_BF16P_BM256 && Mmax % 256 == 0 && (!parts || ((long long)d.Ho * d.Wo) % 256 == 0)) {
@@ -2479,7 +2273,7 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
         }
         return check_launch("conv_rows");
     }
-    const bool mma_ok = vec && !DCS_ROWS_F32 && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
+    const bool mma_ok = vec && (d.mma == MMA_BF16X3 || (d.mma == MMA_BF16 && d.Cs % 64 == 0 && d.ldb % 64 == 0));
     if (mma_ok) {  // bf16 operand modes (vectorised gathers; else exact f32)
 #define DCS_ROWS_MMA(M)                                                                                              \
     if (BN == 128 && res) hipLaunchKernelGGL((conv_rows_kernel<128, 128, 1, 1, M>), grid, dim3(NT), 0, s, d, src, src2, wpack, bias, psc, psh, out, gx, gy, parts, fold_arg); \
@@ -2997,8 +2791,7 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
 namespace dcs {
 bool wgrad_win_check(const dcs_conv_desc& d);
 size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
-int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh, float* ws,
-                     hipStream_t s);
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
 }  // namespace dcs
 
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
@@ -3031,8 +2824,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
     hipStream_t s = as_stream(stream);
     float* w = reinterpret_cast<float*>(ws);
     if (DCS_WGRAD_WIN && wgrad_win_check(d)) {  // f16x3 residual geometry: the rolling-window kernel
-        if (d.pro_act != DCS_ACT_NONE && (!psc || !psh)) return fail(DCS_E_INVALID, "conv_wgrad: missing prologue");
-        const int ns = wgrad_win_launch(d, dy, x, psc, psh, w, s);
+        const int ns = wgrad_win_launch(d, dy, x, w, s);
         if (ns < 0) return -ns;
         const long long total = (long long)d.Co * 9 * d.Cs;
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
@@ -3043,25 +2835,9 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
                      d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;
     const bool v4 = !vec && vec4_ok(dp, x) && d.pro_act == DCS_ACT_NONE && !d.parity;
     const bool dy_small = (long long)d.N * d.Ho * d.Wo * d.Co * 4 < (long long)OOB_OFF - 64;
-    // The bf16 weight-gradient kernel measured slower than the exact f32 one at every layer
-    // (res 2.1-2.5 ms vs 1.75 ms: its 8-pixel walk per thread is VALU bound), so the bf16 and
-    // bf16x3 modes run the bf16x6 weight gradient (fp32-class and faster than f32) unless
-    // DCS_WGRAD_MMA16 is defined (kept for the A/B record).
-#ifdef DCS_WGRAD_MMA16
-    if (d.mma != MMA_F32 && vec && dy_small && p.BM == 128 && p.BN == 128 && !d.parity) {
-#else
-    if (false && dy_small) {
-#endif
-        const bool uni = d.Cs % 128 == 0;
-        if (d.mma == MMA_BF16 && uni)
-            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-        else if (d.mma == MMA_BF16)
-            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-        else if (uni)
-            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, true>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-        else
-            hipLaunchKernelGGL((conv_wgrad_mma16_kernel<MMA_BF16X3, false>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, p.kt_per_split, gn, gm);
-    } else if (DCS_WGRAD_X6_V4 && (d.mma == MMA_F16X3 || d.mma == MMA_F16) && v4 && d.Cs == 4 && !d.parity && dy_small &&
+    // (the bf16 and bf16x3 modes run the bf16x6 weight gradient: a bf16 MFMA weight gradient measured
+    // slower than the exact f32 one at every layer, its 8-pixel walk per thread VALU bound)
+    if (DCS_WGRAD_X6_V4 && (d.mma == MMA_F16X3 || d.mma == MMA_F16) && v4 && d.Cs == 4 && !d.parity && dy_small &&
                d.pro_act == DCS_ACT_NONE && (p.BM == 128 || d.Co == 64) && class_geom(d, 0).Mx >= 16) {
         // 4-channel sources (stem, PatchGAN layer 0) on the fp16 x6 pipeline: two taps per thread's 8 columns
         const bool plain = DCS_TAG2 && d.pad_mode == DCS_PAD_ZERO && d.up == 1;

@@ -103,34 +103,6 @@ __global__ __launch_bounds__(512) void range_parts_kernel(const float* __restric
 extern "C" const char* dcs_last_error(void) { return g_last_error.c_str(); }
 extern "C" int dcs_version(void) { return 1; }
 
-extern "C" int dcs_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream) {
-    if (!cu_mask || words <= 0 || !stream) return fail(DCS_E_INVALID, "stream_create_cu_mask: bad arguments");
-    hipStream_t s = nullptr;
-    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, cu_mask);
-    if (e != hipSuccess) {
-        set_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
-        return (int)e;
-    }
-    *stream = reinterpret_cast<void*>(s);
-    return DCS_OK;
-}
-
-extern "C" int dcs_stream_destroy(void* stream) {
-    const hipError_t e = hipStreamDestroy(as_stream(stream));
-    if (e != hipSuccess) {
-        set_error(std::string("hipStreamDestroy: ") + hipGetErrorString(e));
-        return (int)e;
-    }
-    return DCS_OK;
-}
-
-extern "C" int dcs_device_cu_count(void) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-    return n;
-}
-
 extern "C" int dcs_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                              float beta2, float eps, float bias_c1, float bias_c2, void* stream) {
     if (!p || !g || !m || !v || n < 0) return fail(DCS_E_INVALID, "adam: bad arguments");
@@ -297,32 +269,6 @@ extern "C" int dcs_channel_sum(const float* x, int64_t P, int C, float* out, voi
     hipLaunchKernelGGL(channel_sum_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
                        reinterpret_cast<const float*>(ws), C, nch, out);
     return check_launch("channel_sum_final");
-}
-
-// range record of relu(x * scale + shift) from the InstanceNorm statistics (dcs_range_from_in_stats):
-// with scale > 0 the largest value of a (image, channel) plane is relu(xmax * scale + shift), so
-// part i is the max over the planes j = i (mod DCS_RANGE_PARTS) of that value -- the same number the
-// materialising dcs_in_apply would have recorded, without a pass over the tensor
-__global__ __launch_bounds__(256) void range_from_in_stats_kernel(const float* __restrict__ sc,
-                                                                  const float* __restrict__ sh,
-                                                                  const float* __restrict__ xmax, int n,
-                                                                  float* __restrict__ parts) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= DCS_RANGE_PARTS) return;
-    float m = 0.f;
-    for (int j = i; j < n; j += DCS_RANGE_PARTS) m = fmaxf(m, act_apply(fmaf(xmax[j], sc[j], sh[j]), DCS_ACT_RELU));
-    parts[i] = m;
-}
-
-extern "C" int dcs_range_from_in_stats(const float* scale, const float* shift, const float* xmax, int n, int act,
-                                       float* parts, void* stream) {
-    if (!scale || !shift || !xmax || !parts || n <= 0)
-        return fail(DCS_E_INVALID, "range_from_in_stats: bad arguments");
-    if (act != DCS_ACT_RELU)
-        return fail(DCS_E_INVALID, "range_from_in_stats: DCS_ACT_RELU only (the bound needs scale > 0 and a floor at 0)");
-    hipLaunchKernelGGL(range_from_in_stats_kernel, dim3((DCS_RANGE_PARTS + 255) / 256), dim3(256), 0, as_stream(stream),
-                       scale, shift, xmax, n, parts);
-    return check_launch("range_from_in_stats");
 }
 
 extern "C" int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale, const float* shift,

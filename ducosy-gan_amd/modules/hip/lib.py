@@ -55,18 +55,13 @@ DP = POINTER(ConvDesc)
 SIGNATURES = {
     "dcs_last_error": (c_char_p, []),
     "dcs_version": (c_int, []),
-    "dcs_stream_create_cu_mask": (c_int, [P, c_int, P]),
-    "dcs_stream_destroy": (c_int, [P]),
-    "dcs_device_cu_count": (c_int, []),
     "dcs_pack_weights": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "dcs_pack_weights_r": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     "dcs_range_parts": (c_int, [P, c_int, c_int64, c_int, P, P, c_int, P, P]),
-    "dcs_range_from_in_stats": (c_int, [P, P, P, c_int, c_int, P, P]),
     "dcs_pack_weights_h3_scratch_size": (c_size_t, []),
     "dcs_pack_weights_h3": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "dcs_conv3_win_ok": (c_int, [DP, c_int]),
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
-    "dcs_conv3_win_in_stats_pro": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_conv_dgrad_reflect_win": (c_int, [DP, P, P, P, P, P, P, P, P, P]),
     "dcs_conv_dgrad_reflect_win_inbwd_parts_size": (c_size_t, [DP]),
     "dcs_conv_dgrad_reflect_win_inbwd": (c_int, [DP, P, P, P, P, P, P, P, P, P, P, c_int, P, c_size_t, P, P]),

@@ -63,12 +63,6 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
     return n
 
 
-# IN + ReLU of the residual blocks' first conv applied in the window kernels' staging (fp16 modes) with
-# DUCOSY_FUSE_PRO=1.  Off: measured 1.3 ms/step slower than in_apply (profiles/r03h: the prologue adds
-# 75 us to each conv2 forward and 30 us to each weight gradient, more than the 80 us in_apply pass saves)
-_FUSE_PRO = os.environ.get("DUCOSY_FUSE_PRO", "0") == "1"
-
-
 # the InstanceNorm backward's partial sums of each residual block's first IN fused into the data
 # gradient that produces its input gradient (window path); "0" = separate partial-sum pass (A/B)
 _FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
@@ -135,22 +129,17 @@ class _GradSink:
 
 
 class _Block:
-    __slots__ = ("x", "y1", "s1", "a1", "pro1", "y2", "s2", "cb")
+    __slots__ = ("x", "y1", "s1", "a1", "y2", "s2", "cb")
 
 
 def _res_block_forward(L, W, b, x, use_cbam, keep):
-    """One ResidualBlock[WithCBAM] (modules/model.py:56-87) on NHWC x.  In the fp16 operand modes
-    the IN + ReLU between the two convs is applied in the window kernels' staging (conv2's forward
-    and weight gradient; its range record from the IN statistics), never materialised."""
+    """One ResidualBlock[WithCBAM] (modules/model.py:56-87) on NHWC x.  The IN + ReLU between the
+    two convs is materialised once (in_apply) for conv2's forward and weight gradient: applying it
+    in the window kernels' staging instead measured 1.3 ms per step slower (profiles/r03h)."""
     res = L["res"]
-    fused = _FUSE_PRO and res.win_fits(x.shape[1], x.shape[2])
-    y1, s1 = res.forward_in_stats(Src.nhwc(x), W["pk"][f"r{b}.c1.w"], want_max=fused)
-    if fused:
-        a1, pro1 = None, (s1.scale, s1.shift, ACT_RELU, ops.range_from_stats(s1, ACT_RELU))
-        y2, s2 = res.forward_in_stats(Src.nhwc(y1), W["pk"][f"r{b}.c2.w"], pro=pro1, want_max=use_cbam)
-    else:
-        a1, pro1 = ops.in_apply(y1, s1, ACT_RELU), None
-        y2, s2 = res.forward_in_stats(Src.nhwc(a1), W["pk"][f"r{b}.c2.w"], want_max=use_cbam)
+    y1, s1 = res.forward_in_stats(Src.nhwc(x), W["pk"][f"r{b}.c1.w"])
+    a1 = ops.in_apply(y1, s1, ACT_RELU)
+    y2, s2 = res.forward_in_stats(Src.nhwc(a1), W["pk"][f"r{b}.c2.w"], want_max=use_cbam)
     cb = None
     if use_cbam:
         w1, w2, wsa = W[f"r{b}.fc1"], W[f"r{b}.fc2"], W[f"r{b}.sa"]
@@ -162,7 +151,7 @@ def _res_block_forward(L, W, b, x, use_cbam, keep):
     blk = None
     if keep:
         blk = _Block()
-        blk.x, blk.y1, blk.s1, blk.a1, blk.pro1, blk.y2, blk.s2, blk.cb = x, y1, s1, a1, pro1, y2, s2, cb
+        blk.x, blk.y1, blk.s1, blk.a1, blk.y2, blk.s2, blk.cb = x, y1, s1, a1, y2, s2, cb
     return out, blk
 
 
@@ -181,10 +170,7 @@ def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
     else:
         dy2 = ops.in_act_backward(dout, blk.y2, blk.s2, ACT_AFFINE)
     H, Wd = blk.x.shape[1], blk.x.shape[2]
-    if blk.a1 is None:  # IN + ReLU applied in the window staging
-        grads.put(f"r{b}.c2.w", lambda o: res.wgrad(dy2, Src.nhwc(blk.y1), pro=blk.pro1, out=o))
-    else:
-        grads.put(f"r{b}.c2.w", lambda o: res.wgrad(dy2, Src.nhwc(blk.a1), out=o))
+    grads.put(f"r{b}.c2.w", lambda o: res.wgrad(dy2, Src.nhwc(blk.a1), out=o))
     if _FUSE_IBW:  # IN1's backward partial sums from the data gradient's epilogue (window path)
         da1, parts, nch = res.dgrad(dy2, res.pack_dgrad(W[f"r{b}.c2.w"]), H, Wd, inbwd=(blk.y1, blk.s1, ACT_RELU))
         if parts is not None:

@@ -155,10 +155,7 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
     """DCS_RANGE_PARTS partial maxima of |t| (or of |act(t * scale + shift)| with a per-(image,
     channel) prologue) for an NHWC tensor: the f16x3 kernels reduce them to the operand's power-of-two
     scale.  Cached on the tensor object per (version, prologue), so the forward, data-gradient and
-    weight-gradient passes over one activation or gradient compute it once.  A prologue tuple with a
-    4th element carries its record already (range_from_stats): no pass over t."""
-    if pro is not None and len(pro) > 3 and pro[3] is not None:
-        return pro[3]
+    weight-gradient passes over one activation or gradient compute it once."""
     cached = getattr(t, "_dcs_rng", None)
     if cached is not None and cached[0] == t._version and cached[1] is (pro[0] if pro else None) \
             and cached[2] == (pro[2] if pro else ACT_NONE) and _rng_valid(cached):
@@ -168,16 +165,6 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
     lib.call("dcs_range_parts", _p(t), N, t.numel() // N, C, _p(pro[0]) if pro else None,
              _p(pro[1]) if pro else None, pro[2] if pro else ACT_NONE, _p(parts), _stream())
     t._dcs_rng = (t._version, pro[0] if pro else None, pro[2] if pro else ACT_NONE, parts)
-    return parts
-
-
-def range_from_stats(st: "INStats", act: int) -> torch.Tensor:
-    """Range record of relu(x * scale + shift) from the InstanceNorm statistics (needs st.xmax: the
-    forward_in_stats(..., want_max=True) of x), for a window pass that applies the IN + ReLU in its
-    prologue (dcs_range_from_in_stats)."""
-    parts = torch.empty(lib.RANGE_PARTS, device=st.scale.device, dtype=torch.float32)
-    lib.call("dcs_range_from_in_stats", _p(st.scale), _p(st.shift), _p(st.xmax), st.scale.numel(), act, _p(parts),
-             _stream())
     return parts
 
 
@@ -379,12 +366,6 @@ class ConvGeom:
         return (_WIN and _h3() and self.k == 3 and self.stride == 1 and self.up == 1
                 and self.pads == (1, 1, 1, 1) and self.cin % 16 == 0 and self.cout % 128 == 0)
 
-    def win_fits(self, H: int, W: int) -> bool:
-        """The window forward covers an H x W image (csrc/conv_win.hip win_check: whole rows per
-        256-pixel tile).  Passes with a source prologue need it: the rows-pass fallback of the residual
-        geometry runs the prologue-free slice-major kernel its weights are packed for."""
-        return self.win and W <= 128 and 256 % W == 0 and H % (256 // W) == 0
-
     def _attach_h3(self, wpack: torch.Tensor, w: torch.Tensor, flip: int) -> torch.Tensor:
         ncols = self.cin if flip else self.cout
         K = 9 * (self.cout if flip else self.cin)
@@ -508,7 +489,7 @@ class ConvGeom:
             _set_mma(d, s.t, pro, _wrng(wpack))
         h3 = getattr(wpack, "_dcs_h3", None)
         if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
-            return self._win_in_stats(s, d, h3, nb, want_max, pro)
+            return self._win_in_stats(s, d, h3, nb, want_max)
         if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
@@ -532,18 +513,16 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
-    def _win_in_stats(self, s: Src, d, h3, nb, want_max, pro=None):
-        """Forward + IN statistics on the f16x3 window kernel (csrc/conv_win.hip), with the source
-        prologue ``pro`` applied at staging."""
+    def _win_in_stats(self, s: Src, d, h3, nb, want_max):
+        """Forward + IN statistics on the f16x3 window kernel (csrc/conv_win.hip)."""
         dev = s.t.device
         Ho, Wo = self.out_hw(s.H, s.W)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
         parts = workspace(nb, dev)
         nchunk = ctypes.c_int(0)
         e0 = PROBE.begin() if _is_res_geom(self) else None
-        lib.call("dcs_conv3_win_in_stats_pro", ctypes.byref(d), _p(s.t), _p(pro[0]) if pro else None,
-                 _p(pro[1]) if pro else None, _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out), _p(parts), parts.numel(),
-                 ctypes.byref(nchunk), _stream())
+        lib.call("dcs_conv3_win_in_stats", ctypes.byref(d), _p(s.t), _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out),
+                 _p(parts), parts.numel(), ctypes.byref(nchunk), _stream())
         PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
         C = self.cout
         scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
@@ -569,8 +548,8 @@ class ConvGeom:
         h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
         if h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
-            lib.call("dcs_conv3_win_in_stats_pro", ctypes.byref(d), _p(s.t), _p(pro[0]) if pro else None,
-                     _p(pro[1]) if pro else None, _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out), None, 0, None, _stream())
+            lib.call("dcs_conv3_win_in_stats", ctypes.byref(d), _p(s.t), _p(h3[0]), _p(h3[1]), _p(h3[2]), _p(out),
+                     None, 0, None, _stream())
         else:
             lib.call(fn, ctypes.byref(d), _p(s.t), _p(s.t2), _p(wpack), _p(bias),
                      _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _stream())

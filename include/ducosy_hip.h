@@ -124,16 +124,6 @@ typedef struct dcs_conv_desc {
 const char* dcs_last_error(void);
 int dcs_version(void);
 
-/* A HIP stream whose kernels may only occupy the compute units set in cu_mask (words 32-bit
- * words, bit i = CU i; hipExtStreamCreateWithCUMask).  The two-stream schedule of BASELINE
- * config 5 runs each model on its own CU partition (modules/trainer.py ConcurrentCycleGANs;
- * DESIGN.md §3, Config 5: streams sharing a CU pair gave wrong results); the reference trains
- * its two models one after the other (train.py:27-38), so this has no reference counterpart.
- * The stream is created blocking: it synchronises with the legacy null stream. */
-int dcs_stream_create_cu_mask(const uint32_t* cu_mask, int words, void** stream);
-int dcs_stream_destroy(void* stream);
-/* number of compute units of the current device */
-int dcs_device_cu_count(void);
 
 /* ---- convolution family (modules/model.py:61-63,74-79,94-112,122-129 → aten conv) ---- */
 
@@ -201,12 +191,6 @@ int dcs_range_arena_unregister(const void* base);
  * of an F16X3 pass).  per_img % 4 == 0, C % 4 == 0 with a prologue. */
 int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const float* scale,
                     const float* shift, int act, float* parts, void* stream);
-/* The same record for relu(x * scale + shift) from the InstanceNorm statistics alone (n = images x
- * channels entries of scale / shift / xmax, the per-plane max of x from dcs_in_stats_finish):
- * relu(xmax * scale + shift) bounds every value of the plane (scale > 0).  act must be
- * DCS_ACT_RELU.  Lets an F16X3 pass apply the IN + ReLU in its prologue without a range pass. */
-int dcs_range_from_in_stats(const float* scale, const float* shift, const float* xmax, int n, int act,
-                            float* parts, void* stream);
 
 /* ---- f16x3 window convolution: the residual-block 3x3 convs (modules/model.py:72-80) ----
  * A workgroup owns 256 consecutive pixels of one image (256 / W whole rows) x 128 output channels
@@ -235,13 +219,6 @@ int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, int ncols, 
 int dcs_conv3_win_ok(const dcs_conv_desc* d, int dgrad);
 int dcs_conv3_win_in_stats(const dcs_conv_desc* d, const float* src, const void* w_hi, const void* w_lo,
                            const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream);
-/* The forward with a source prologue (d->pro_act = DCS_ACT_AFFINE / _RELU / _LRELU): the window stages
- * act(src * pro_scale[n][c] + pro_shift[n][c]) -- the InstanceNorm apply + ReLU between the two convs of a
- * residual block (modules/model.py:74-78), never materialised; d->rng_a bounds the prologue's output
- * (dcs_range_from_in_stats).  dcs_conv_wgrad takes the same prologue on its window path. */
-int dcs_conv3_win_in_stats_pro(const dcs_conv_desc* d, const float* src, const float* pro_scale, const float* pro_shift,
-                               const void* w_hi, const void* w_lo, const int* wexp, float* out, void* parts,
-                               size_t parts_bytes, int* nchunk, void* stream);
 int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* d, const float* dy, const float* wpack, const void* w_hi,
                                const void* w_lo, const int* wexp, const float* addend, float* dx, float* ring,
                                void* stream);

@@ -19,6 +19,13 @@
 #include "conv_common.hpp"
 #include <type_traits>
 
+#ifndef DCS_WIN_GLDS
+#define DCS_WIN_GLDS 0  // A/B: B k-tiles staged by LDS-DMA (global_load_lds_dwordx4); measured neutral (profiles/r03s)
+#endif
+#ifndef DCS_WIN_SPREAD
+#define DCS_WIN_SPREAD 0  // 1: window staging spread over the slice's k-tiles (no VGPR spills, but 3-5 % slower: profiles/r03g)
+#endif
+
 namespace dcs {
 namespace {
 
@@ -35,7 +42,10 @@ struct WinArgs {
     int R, tiles;        // image rows per tile (256 / W), tiles per image (H / R)
     int gy;              // column tiles (Co / 128)
     int rng_n;           // partial maxima of the source range record
+    int pro_act;         // DCS_ACT_*: InstanceNorm apply (+ act) of the source at staging, per (image, channel)
 };
+
+constexpr int WIN_PRO_CMAX = 512;  // source channels the staged prologue covers
 
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 
@@ -175,8 +185,9 @@ __device__ __forceinline__ void win_ibw(const floatx16 (&acc)[2][2], const float
 }
 
 // NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only);
+// PRO: the source prologue (a separate instance: the prologue-free passes keep their register budget);
 // IBW: the InstanceNorm-backward partial sums of the output (data gradients without addend)
-template <int NP, bool IBW>
+template <int NP, bool PRO, bool IBW>
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
                                                                  const _Float16* __restrict__ wh,
                                                                  const _Float16* __restrict__ wl,
@@ -184,8 +195,12 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                                                                  const int* __restrict__ wexp,
                                                                  const float* __restrict__ addend,
                                                                  float* __restrict__ out, Part* __restrict__ parts,
-                                                                 IbwArgs ib) {
+                                                                 const float* __restrict__ psc,
+                                                                 const float* __restrict__ psh, IbwArgs ib) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT];
+    // the source prologue's scale / shift of this tile's image (the window kernels' tiles never
+    // straddle images), read at staging from LDS so the staging issues no global load of its own
+    __shared__ __attribute__((aligned(16))) float prl[PRO ? 2 * WIN_PRO_CMAX : 4];
     _Float16* const Wn = smem;                               // [2][2][WIN_PIX][16]
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;        // [2][6][WIN_SLOT]
 
@@ -207,6 +222,23 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int ea = f16x3_exp(rng, a.rng_n);
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
     const float asc = __builtin_ldexpf(1.f, ea);
+    if constexpr (PRO) {
+        for (int i = tid; i < C; i += WIN_NT) {
+            prl[i] = psc[(long long)n * C + i];
+            prl[WIN_PRO_CMAX + i] = psh[(long long)n * C + i];
+        }
+        __syncthreads();
+    }
+    // prologue of one staged unit (8 channels c0 .. c0 + 7 of a real source pixel)
+    auto pro8 = [&](float4& v0, float4& v1, int c0) {
+        const float4 s0 = *reinterpret_cast<const float4*>(prl + c0), s1 = *reinterpret_cast<const float4*>(prl + c0 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(prl + WIN_PRO_CMAX + c0);
+        const float4 b1 = *reinterpret_cast<const float4*>(prl + WIN_PRO_CMAX + c0 + 4);
+        v0.x = act_apply(fmaf(v0.x, s0.x, b0.x), a.pro_act); v0.y = act_apply(fmaf(v0.y, s0.y, b0.y), a.pro_act);
+        v0.z = act_apply(fmaf(v0.z, s0.z, b0.z), a.pro_act); v0.w = act_apply(fmaf(v0.w, s0.w, b0.w), a.pro_act);
+        v1.x = act_apply(fmaf(v1.x, s1.x, b1.x), a.pro_act); v1.y = act_apply(fmaf(v1.y, s1.y, b1.y), a.pro_act);
+        v1.z = act_apply(fmaf(v1.z, s1.z, b1.z), a.pro_act); v1.w = act_apply(fmaf(v1.w, s1.w, b1.w), a.pro_act);
+    };
 
     // window staging units of this thread: (pixel, 8-channel half); the byte offset of the unit's
     // source channel 0 (OOB_OFF-style sentinel -1 for zero padding / past the window)
@@ -230,7 +262,32 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         }
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
-    float4 wr_[WIN_UNITS][2];
+#if DCS_WIN_SPREAD
+    // the next slice's window is staged one unit per k-tile (unit q in k-tile ty = q): 8 VGPRs in
+    // flight instead of 24 held across the slice
+    float4 wq[2];
+    auto win_load_q = [&](int s, int q) {
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+        __builtin_memcpy(&wq[0], &v0, 16);
+        __builtin_memcpy(&wq[1], &v1, 16);
+    };
+    auto win_store_q = [&](int buf, int q, int cur_slice) {
+        const int u = tid + q * WIN_NT;
+        const int wpix = u >> 1, h = u & 1;
+        if (wpix < npix) {
+            if (PRO && uoff[q] >= 0) pro8(wq[0], wq[1], cur_slice * 16 + 8 * h);
+            f16x8 hi, lo;
+            split8h(wq[0], wq[1], asc, hi, lo);
+            *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
+        }
+    };
+    static_assert(WIN_UNITS == 3, "one window unit per k-tile of a slice");
+#endif
+    float4 wr_[DCS_WIN_SPREAD ? 1 : WIN_UNITS][2];
     auto win_load = [&](int s) {
 #pragma unroll
         for (int q = 0; q < WIN_UNITS; ++q) {
@@ -242,12 +299,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             __builtin_memcpy(&wr_[q][1], &v1, 16);
         }
     };
-    auto win_store = [&](int buf) {
+    auto win_store = [&](int buf, int cur_slice) {
 #pragma unroll
         for (int q = 0; q < WIN_UNITS; ++q) {
             const int u = tid + q * WIN_NT;
             const int wpix = u >> 1, h = u & 1;
             if (wpix < npix) {
+                if (PRO && uoff[q] >= 0) pro8(wr_[q][0], wr_[q][1], cur_slice * 16 + 8 * h);
                 f16x8 hi, lo;
                 split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
@@ -268,6 +326,31 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         bg[i] = pl * 0x40000000 + (n0 + row) * K + c6 * 8;  // bit 30: the lo plane
         bl[i] = wb_off(0, pl, c6 >> 1, row, c6 & 1);
     }
+#if DCS_WIN_GLDS
+    // LDS-DMA staging of B: a k-tile is 24 chunks of 1 KB (plane, tx slot, 32-row block); wave w
+    // issues chunks 3w .. 3w+2, each one global_load_lds_dwordx4 whose LDS image is lane-linear
+    // (lane L -> 16 bytes at chunk base + 16 L = row L/2, half position L%2).  The XOR swizzle of
+    // wb_off goes on the source side: lane L fetches the half h = (L%2) ^ bit 3 of its row.
+    int gsrc[3], gdst[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int c = wid * 3 + i, pl = c / 12, rem = c - pl * 12, tx = rem >> 2, rb = rem & 3;
+        const int row = rb * 32 + (lane >> 1), h = (lane & 1) ^ ((row >> 3) & 1);
+        gsrc[i] = pl * 0x40000000 + (n0 + row) * K + tx * 16 + h * 8;
+        gdst[i] = __builtin_amdgcn_readfirstlane((pl * 3 + tx) * WIN_SLOT + rb * 32 * 16);
+    }
+    auto b_glds = [&](int t, int buf) {
+        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
+        const int kb = s_ * 144 + ty_ * 48;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const _Float16* w = ((gsrc[i] >> 30) ? wl : wh) + (gsrc[i] & 0x3fffffff) + kb;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(w),
+                                             (__attribute__((address_space(3))) void*)(Bs + buf * 6 * WIN_SLOT + gdst[i]),
+                                             16, 0, 0);
+        }
+    };
+#endif
     uint4 br0, br1, br2;  // named (an array here was promoted to LDS)
     auto b_ld = [&](int i, int kb) {
         const int g = bg[i] & 0x3fffffff;
@@ -305,12 +388,25 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
     // prologue: window of slice 0, B tile 0; B tile 1 in flight
+#if DCS_WIN_SPREAD
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        win_load_q(0, q);
+        win_store_q(0, q, 0);
+    }
+#else
     win_load(0);
-    win_store(0);
+    win_store(0, 0);
+#endif
+#if DCS_WIN_GLDS
+    b_glds(0, 0);
+    __syncthreads();  // (drains the DMA: vmcnt(0) before the barrier)
+#else
     b_load(0);
     b_store(0);
     __syncthreads();
     b_load(1);
+#endif
 
     // every global load below is unconditional (indices clamped at the end): a load under a branch
     // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer, which here
@@ -318,10 +414,24 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int last = 3 * nslice - 1;
     for (int s = 0; s < nslice; ++s) {
         const int wbuf = s & 1;
-        win_load(s + 1 < nslice ? s + 1 : s);
+        if (!DCS_WIN_SPREAD) win_load(s + 1 < nslice ? s + 1 : s);
+#if DCS_WIN_GLDS
+        // keep the next slice's window loads at the top of the slice: with the DMA staging every
+        // barrier waits vmcnt(0), so loads sunk to the end of a k-tile would expose their latency
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) {
             const int tt = 3 * s + ty, bbuf = tt & 1;
+#if DCS_WIN_GLDS
+            // B tile tt + 1 into the other buffer (free: every wave passed the barrier after reading
+            // tile tt - 1 there); landed by the barrier that ends this k-tile.  Past the end: a repeat
+            // into a buffer nobody reads again
+            b_glds(tt + 1 < last ? tt + 1 : last, bbuf ^ 1);
+#endif
+#if DCS_WIN_SPREAD
+            win_load_q(s + 1 < nslice ? s + 1 : s, ty);
+#endif
 #pragma unroll
             for (int tx = 0; tx < 3; ++tx) {
                 f16x8 ah[2], al[2], bh[2], bl[2];
@@ -350,9 +460,15 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             }
             // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2 (past the end:
             // a repeat into a buffer nobody reads again)
+#if !DCS_WIN_GLDS
             b_store(bbuf ^ 1);
             b_load(tt + 2 < last ? tt + 2 : last);
-            if (ty == 2) win_store(wbuf ^ 1);
+#endif
+#if DCS_WIN_SPREAD
+            win_store_q(wbuf ^ 1, ty, s + 1 < nslice ? s + 1 : s);
+#else
+            if (ty == 2) win_store(wbuf ^ 1, s + 1 < nslice ? s + 1 : s);
+#endif
             __syncthreads();
         }
         // close the slice's accumulation chain (144 k)
@@ -409,6 +525,359 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         float yv[2][2][16];
         win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm, wn, lane);
         win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(smem));
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// conv3_win2_kernel: the same tile and K order as conv3_win_h3_kernel, with the LDS traffic laid out
+// so that every MFMA fragment of the next sub-tile is read while the current sub-tile's MFMAs run.
+//   * window pixel records of W2_PITCH bytes: [hi 16 ch][lo 16 ch][16 B pad] (80 B; f16: [hi][pad],
+//     48 B).  A 16-lane ds_read_b128 group reads 16 consecutive pixels' 16-byte pieces: at a 20- (12-)
+//     dword pitch their start banks are 16 distinct multiples of 4 for ANY pixel shift, so the nine
+//     taps' reads are conflict-free with the shift as an immediate offset (the first kernel's XOR
+//     swizzle depends on the pixel and cost two VALU per fragment read).
+//   * B k-tiles by LDS-DMA (global_load_lds_dwordx4, swizzle on the source side) into three
+//     buffers: tile t lives in buffer t % 3 = ty (compile-time), its DMA issued at the start of tile
+//     t - 2.  So at any time two tiles are readable: the current one and the next, and the next
+//     tile's first fragments are read during the current tile's last sub-tile.  No VGPRs stage B.
+//   * the window of slice s + 1 is loaded to registers at the start of tile 3s (units 0, 1) and
+//     3s + 1 (unit 2, 16 threads), split and stored at the end of that tile, visible from tile 3s + 2,
+//     whose last sub-tile reads the first fragments of slice s + 1.
+//   * fragments double-buffered in registers (F: being multiplied, G: being read); per sub-tile the
+//     8 (f16: 4) reads of the next one go out before its 12 (4) MFMAs.
+// One barrier per k-tile, with every wave's LDS-DMA and loads of the tile retired before it.
+// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(0): every VMEM op of this wave (its LDS-DMA included) and every
+// LDS op retired
+#define W2_DRAIN() __builtin_amdgcn_s_waitcnt(0x0070)
+constexpr int W2_SLOTB = WIN_SLOT * 2;       // bytes per B plane-slot
+constexpr int W2_BBUF = 6 * W2_SLOTB;        // bytes per B buffer
+template <int NP> constexpr int w2_pitch() { return NP == 3 ? 80 : 48; }  // bytes per window pixel
+template <int NP> constexpr int w2_lds_bytes() { return 2 * WIN_PIX * w2_pitch<NP>() + 3 * W2_BBUF + 64 * 48; }  // + pad slots
+
+// one global_load_lds_dwordx4 (lane L's 16 bytes to LDS byte address lds + 16 L), written as inline
+// asm: beside a compiler-emitted LDS-DMA, hipcc waits lgkmcnt(0) before every MFMA that uses a
+// ds_read result (it cannot order the DMA's LDS writes against the reads), which serialises the
+// fragment prefetch.  The asm DMA is invisible to its counters: the kernel retires it itself
+// (W2_DRAIN before the barrier that precedes every read of the buffer).
+__device__ __forceinline__ void w2_glds(const void* g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// KO (timing probes only, results wrong): bit 0 no fragment reads in the loop, bit 1 no staging (DMA,
+// window) in the loop, bit 2 no barriers / drains in the loop
+template <int NP, bool IBW, int KO = 0>
+__global__ __launch_bounds__(WIN_NT, 1) void conv3_win2_kernel(WinArgs a, const float* __restrict__ src,
+                                                               const _Float16* __restrict__ wh,
+                                                               const _Float16* __restrict__ wl,
+                                                               const float* __restrict__ rng,
+                                                               const int* __restrict__ wexp,
+                                                               const float* __restrict__ addend,
+                                                               float* __restrict__ out, Part* __restrict__ parts,
+                                                               IbwArgs ib) {
+    constexpr int PB = w2_pitch<NP>();
+    constexpr int WBUF = WIN_PIX * PB;  // bytes per window buffer
+    __shared__ __attribute__((aligned(16))) char lds[w2_lds_bytes<NP>()];
+    char* const Wn = lds;                 // [2][WIN_PIX][PB]
+    char* const Bs = lds + 2 * WBUF;      // [3][6][WIN_SLOT halves]
+
+    const int T = gridDim.x;
+    const int L = xcd_remap(blockIdx.x, T);
+    const int ntile = L % a.gy, mt = L / a.gy;
+    const int n = mt / a.tiles, tile = mt - n * a.tiles;
+    const int n0 = ntile * WIN_BN;
+    const int y0 = tile * a.R;
+    const int W = a.W, WP = a.W + 2, C = a.C;
+    const int K = 9 * C;
+    const int nslice = C / 16;
+    const int npix = (a.R + 2) * WP;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int l32 = lane & 31, kh = lane >> 5;
+
+    const int ea = f16x3_exp(rng, a.rng_n);
+    const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
+    const float asc = __builtin_ldexpf(1.f, ea);
+
+    // ---- window staging: units (pixel, 8-channel half); byte offset of channel 0 (or -1) ----
+    int uoff[WIN_UNITS];
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        const int u = tid + q * WIN_NT;
+        const int wpix = u >> 1, h = u & 1;
+        uoff[q] = -1;
+        if (wpix < npix) {
+            const int wr = wpix / WP, wc = wpix - (wpix / WP) * WP;
+            int sy = y0 - 1 + wr, sx = wc - 1;
+            bool ok = true;
+            if (a.reflect) {
+                sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
+                sx = sx < 0 ? -sx : (sx >= W ? 2 * W - 2 - sx : sx);
+            } else {
+                ok = sy >= 0 && sy < a.H && sx >= 0 && sx < W;
+            }
+            if (ok) uoff[q] = (((n * a.H + sy) * W + sx) * C + 8 * h) * 4;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    float4 wr_[WIN_UNITS][2];
+    auto win_load = [&](int s, int q) {
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+        __builtin_memcpy(&wr_[q][0], &v0, 16);
+        __builtin_memcpy(&wr_[q][1], &v1, 16);
+    };
+    // branch-free: a unit past the window writes its lane's pad slot after the B buffers (a store under
+    // a branch lets the compiler sink the unit's loads down to it, exposing their latency; one slot
+    // for every lane would be a 64-way write conflict)
+    int wso[WIN_UNITS];
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        const int u = tid + q * WIN_NT;
+        wso[q] = (u >> 1) < npix ? (u >> 1) * PB + 16 * (u & 1) : -1;
+    }
+    auto win_store = [&](int buf, int q) {
+        f16x8 hi, lo;
+        split8h_s(wr_[q][0], wr_[q][1], asc, hi, lo);
+        char* p = wso[q] < 0 ? Wn + 2 * WBUF + 3 * W2_BBUF + 48 * lane : Wn + buf * WBUF + wso[q];
+        *reinterpret_cast<f16x8*>(p) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(p + 32) = lo;
+    };
+
+    // ---- B by LDS-DMA: a k-tile is 2 (f16: 1) planes x 3 tx x 4 row blocks of 1 KB; wave w issues
+    // chunks w, w + 8, w + 16 (f16: w, w + 8 below 12).  Lane L of a chunk: row rb * 32 + L / 2,
+    // 16-byte half (L % 2) ^ bit 3 of the row (the read side's swizzle, applied at the source; bit 3
+    // of the row is bit 4 of L).
+    constexpr int NCH = NP == 3 ? 24 : 12;
+    constexpr int CPW = (NCH + 7) / 8;
+    const int glane = (lane >> 1) * K + 8 * ((lane & 1) ^ ((lane >> 4) & 1));  // halves
+    const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)Bs;
+    auto b_dma = [&](int t, int buf) {
+        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
+        const int kb = s_ * 144 + ty_ * 48;
+#pragma unroll
+        for (int i = 0; i < CPW; ++i) {
+            const int c = wid + 8 * i;
+            if (c < NCH) {  // wave-uniform
+                const int pl = c / 12, rem = c - pl * 12, tx = rem >> 2, rb = rem & 3;
+                const _Float16* w = (pl ? wl : wh) + (long long)(n0 + rb * 32) * K + tx * 16 + kb + glane;
+                w2_glds(w, __builtin_amdgcn_readfirstlane(bs_lds + buf * W2_BBUF + (pl * 3 + tx) * W2_SLOTB + rb * 1024));
+            }
+        }
+    };
+
+    // ---- fragment addresses (bytes) ----
+    int abase[2], bbase[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = wm * 64 + i * 32 + l32;
+        abase[i] = ((q / W) * WP + (q - (q / W) * W)) * PB + 16 * kh;
+        const int row = wn * 64 + i * 32 + l32;
+        bbase[i] = row * 32 + 16 * (kh ^ ((row >> 3) & 1));
+    }
+    // A fragments (2 pixel blocks x hi / lo) double-buffered; B fragments (per column block j)
+    // refilled right after the MFMAs that used them
+    struct AF {
+        f16x8 h[2], l[2];
+    };
+    struct BF {
+        f16x8 h, l;
+    };
+    auto rdA = [&](AF& f, int wb, int ty, auto tx_c) {
+        constexpr int TX = decltype(tx_c)::value;
+        const int ao = wb * WBUF + ty * WP * PB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const char* pa = Wn + ((KO & 32) ? 16 * i : abase[i]) + ao + TX * PB;  // KO & 32: broadcast probe
+            f.h[i] = *reinterpret_cast<const f16x8*>(pa);
+            if constexpr (NP == 3) f.l[i] = *reinterpret_cast<const f16x8*>(pa + 32);
+        }
+    };
+    auto rdB = [&](BF& f, int j, auto bbuf_c, auto tx_c) {
+        constexpr int BBUF = decltype(bbuf_c)::value, TX = decltype(tx_c)::value;
+        const char* pb = Bs + BBUF * W2_BBUF + ((KO & 64) ? 16 * j : bbase[j]) + TX * W2_SLOTB;  // KO & 64: broadcast probe
+        f.h = *reinterpret_cast<const f16x8*>(pb);
+        if constexpr (NP == 3) f.l = *reinterpret_cast<const f16x8*>(pb + 3 * W2_SLOTB);
+    };
+
+    floatx16 acc[2][2], t[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
+
+    const floatx16 zero16 = {};
+    // FIRST: the slice's first sub-tile starts each inner chain from zero (no zeroing moves)
+    auto mma_j = [&](const AF& a_, const BF& b_, int j, auto first_c) {
+        constexpr bool FIRST = decltype(first_c)::value;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            floatx16 c = FIRST ? zero16 : t[i][j];
+            if constexpr (NP == 3) {
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_.l[i], b_.h, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_.h[i], b_.l, c, 0, 0, 0);
+            }
+            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_.h[i], b_.h, c, 0, 0, 0);
+        }
+    };
+    constexpr int RA = NP == 3 ? 4 : 2, RB = NP == 3 ? 2 : 1, MJ = NP == 3 ? 6 : 2;
+    AF A0, A1;
+    BF B0, B1;
+    // one sub-tile: the next sub-tile's A fragments, the MFMAs of column block 0, its next B
+    // fragments, the MFMAs of column block 1, its next B fragments (the scheduler is pinned to that
+    // order: every read has 6 MFMAs (f16: 2) or more between its issue and its use)
+    BF B0n, B1n;  // KO & 16: B double-buffered too (probe)
+    auto sub = [&](AF& cur, AF& nxt, int wb_n, int ty_n, auto bbuf_c, auto tx_c, auto first_c) {
+        if constexpr (KO & 16) {
+            rdA(nxt, wb_n, ty_n, tx_c);
+            rdB(B0n, 0, bbuf_c, tx_c);
+            rdB(B1n, 1, bbuf_c, tx_c);
+            mma_j(cur, B0, 0, first_c);
+            mma_j(cur, B1, 1, first_c);
+            B0 = B0n;
+            B1 = B1n;
+            __builtin_amdgcn_sched_group_barrier(0x100, NP == 3 ? 8 : 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2 * (NP == 3 ? 6 : 2), 0);
+            return;
+        }
+        if constexpr (!(KO & 1)) rdA(nxt, wb_n, ty_n, tx_c);
+        mma_j(cur, B0, 0, first_c);
+        if constexpr (!(KO & 1)) rdB(B0, 0, bbuf_c, tx_c);
+        mma_j(cur, B1, 1, first_c);
+        if constexpr (!(KO & 1)) rdB(B1, 1, bbuf_c, tx_c);
+        __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, MJ, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, RB, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MJ, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, RB, 0);
+    };
+
+    // prologue: window of slice 0, B tiles 0 and 1; fragments of (tile 0, tx 0)
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) win_load(0, q);
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) win_store(0, q);
+    b_dma(0, 0);
+    b_dma(1, 1);
+    W2_DRAIN();
+    __syncthreads();
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using T1 = std::true_type;
+    using F0 = std::false_type;
+    rdA(A0, 0, 0, I0{});
+    rdB(B0, 0, I0{}, I0{});
+    rdB(B1, 1, I0{}, I0{});
+
+    const int last = 3 * nslice - 1;
+    for (int s = 0; s < nslice; ++s) {
+        const int wb = s & 1, ns = s + 1 < nslice ? s + 1 : s;
+        // ---- tile 3s (ty 0, B buffer 0) ----
+        if constexpr (!(KO & 2)) {
+            b_dma(3 * s + 2 < last ? 3 * s + 2 : last, 2);
+            win_load(ns, 0);
+            win_load(ns, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the window loads stay at the tile start
+        sub(A0, A1, wb, 0, I0{}, I1{}, T1{});
+        sub(A1, A0, wb, 0, I0{}, I2{}, F0{});
+        sub(A0, A1, wb, 1, I1{}, I0{}, F0{});
+        __builtin_amdgcn_sched_barrier(0);  // the split stays after the tile's MFMAs (its loads' latency covered)
+        if constexpr (!(KO & 2)) {
+            win_store(wb ^ 1, 0);
+            win_store(wb ^ 1, 1);
+        }
+        if constexpr (!(KO & 4)) {
+            W2_DRAIN();  // the tile's DMA and loads retired before the barrier
+            __syncthreads();
+        }
+        // ---- tile 3s + 1 (ty 1, B buffer 1) ----
+        if constexpr (!(KO & 2)) {
+            b_dma(3 * s + 3 < last ? 3 * s + 3 : last, 0);
+            if constexpr (WIN_UNITS > 2) win_load(ns, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sub(A1, A0, wb, 1, I1{}, I1{}, F0{});
+        sub(A0, A1, wb, 1, I1{}, I2{}, F0{});
+        sub(A1, A0, wb, 2, I2{}, I0{}, F0{});
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (WIN_UNITS > 2 && !(KO & 2)) win_store(wb ^ 1, 2);
+        if constexpr (!(KO & 4)) {
+            W2_DRAIN();
+            __syncthreads();
+        }
+        // ---- tile 3s + 2 (ty 2, B buffer 2); its last sub-tile reads slice s + 1's first ----
+        if constexpr (!(KO & 2)) b_dma(3 * s + 4 < last ? 3 * s + 4 : last, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        sub(A0, A1, wb, 2, I2{}, I1{}, F0{});
+        sub(A1, A0, wb, 2, I2{}, I2{}, F0{});
+        sub(A0, A1, wb ^ 1, 0, I0{}, I0{}, F0{});
+        A0 = A1;
+        // close the slice's accumulation chain (144 k)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_fmaf(1.f, t[i][j][r], acc[i][j][r]);
+        if constexpr (!(KO & 4)) {
+            W2_DRAIN();
+            __syncthreads();
+        }
+    }
+
+    // epilogue: undo the operand scales, + addend, NHWC store, IN statistics (the loop's last barrier
+    // freed the LDS)
+    const int eab = -(ea + eb);
+    const int p0 = y0 * W;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+    const long long obase = (long long)n * a.H * W * a.Co;
+    auto ooff = [&](int i, int j, int r) {
+        const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 32 + l32;
+    };
+    if (addend) {
+        floatx16 ad[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ad[i][j][r] = addend[ooff(i, j, r)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r] + ad[i][j][r];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r];
+    }
+    if (parts) win_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(lds), parts,
+                         (long long)n * a.tiles + tile);
+    if constexpr (IBW) {
+        float yv[2][2][16];
+        win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm, wn, lane);
+        win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(lds));
     }
 }
 
@@ -486,6 +955,7 @@ struct WWArgs {
     int strips, rchunks, rows_per;  // 64-pixel strips per row, row chunks per strip, rows per chunk
     int gco, gci;        // 64-channel tiles of co / ci
     int rng_a_n, rng_b_n;
+    int pro_act;         // DCS_ACT_*: InstanceNorm apply (+ act) of the source at staging, per (image, channel)
 };
 
 __device__ __forceinline__ int ww_swz(int pix) { return ((pix >> 1) & 1) << 2; }
@@ -504,8 +974,11 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                                                                  const float* __restrict__ src,
                                                                  const float* __restrict__ rnga,
                                                                  const float* __restrict__ rngb,
-                                                                 float* __restrict__ ws) {
+                                                                 float* __restrict__ ws,
+                                                                 const float* __restrict__ psc,
+                                                                 const float* __restrict__ psh) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
+    __shared__ __attribute__((aligned(16))) float prl[2 * 64];  // source prologue of this tile's 64 channels
     _Float16* const Xr = smem;                 // [4][2][66][64]
     _Float16* const Dy = smem + 4 * WW_XROW;   // [2][2][64][64]
 
@@ -525,6 +998,19 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 
     const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
     const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+    if (a.pro_act != DCS_ACT_NONE && tid < 64) {  // made visible by the prologue's barrier below
+        prl[tid] = psc[(long long)n * C + ci0 + tid];
+        prl[64 + tid] = psh[(long long)n * C + ci0 + tid];
+    }
+    auto pro8 = [&](float4& v0, float4& v1, int c0) {
+        const float4 s0 = *reinterpret_cast<const float4*>(prl + c0), s1 = *reinterpret_cast<const float4*>(prl + c0 + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(prl + 64 + c0);
+        const float4 b1 = *reinterpret_cast<const float4*>(prl + 64 + c0 + 4);
+        v0.x = act_apply(fmaf(v0.x, s0.x, b0.x), a.pro_act); v0.y = act_apply(fmaf(v0.y, s0.y, b0.y), a.pro_act);
+        v0.z = act_apply(fmaf(v0.z, s0.z, b0.z), a.pro_act); v0.w = act_apply(fmaf(v0.w, s0.w, b0.w), a.pro_act);
+        v1.x = act_apply(fmaf(v1.x, s1.x, b1.x), a.pro_act); v1.y = act_apply(fmaf(v1.y, s1.y, b1.y), a.pro_act);
+        v1.z = act_apply(fmaf(v1.z, s1.z, b1.z), a.pro_act); v1.w = act_apply(fmaf(v1.w, s1.w, b1.w), a.pro_act);
+    };
 
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
@@ -587,6 +1073,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int q = 0; q < WW_XU; ++q) {
             if (xls[q] >= 0) {
+                if (a.pro_act != DCS_ACT_NONE && xoff[q] >= 0) pro8(xr[q][0], xr[q][1], 8 * ((tid + q * WW_NT) & 7));
                 f16x8 hi, lo;
                 split8h(xr[q][0], xr[q][1], bsc, hi, lo);
                 *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
@@ -619,6 +1106,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
 
+    if (a.pro_act != DCS_ACT_NONE) __syncthreads();  // prl
     // prologue: source rows y_beg-1 .. y_beg+1 into their ring slots, dy row y_beg into buffer 0
 #pragma unroll 1
     for (int r = y_beg - 1; r <= y_beg + 1; ++r) {
@@ -736,7 +1224,8 @@ bool wgrad_win_check(const dcs_conv_desc& d) {
            d.pt == 1 && d.pl == 1 && d.Ho == d.Hs && d.Wo == d.Ws && d.Cs % 64 == 0 && d.Co % 64 == 0 &&
            d.Ws % WW_SW == 0 && d.Hs >= 2 && d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
            d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) &&
-           d.pro_act == DCS_ACT_NONE && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 &&
+           (d.pro_act == DCS_ACT_NONE || d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU ||
+            d.pro_act == DCS_ACT_LRELU) && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 &&
            d.rng_b_n > 0 && d.rng_b_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
            (long long)d.N * d.Hs * d.Ws * d.Co * 4 < 0x7fffff00LL - 64;
 }
@@ -747,7 +1236,8 @@ size_t wgrad_win_workspace_size(const dcs_conv_desc& d) {
 }
 
 // partial slabs into ws (wgrad_win_workspace_size bytes); returns the split count (< 0: error)
-int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s) {
+int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh, float* ws,
+                     hipStream_t s) {
     const WWPlan p = ww_plan(d);
     WWArgs a;
     a.N = d.N; a.H = d.Hs; a.W = d.Ws; a.C = d.Cs; a.Co = d.Co;
@@ -755,11 +1245,14 @@ int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, fl
     a.strips = p.strips; a.rchunks = p.rchunks; a.rows_per = p.rows_per;
     a.gco = d.Co / 64; a.gci = d.Cs / 64;
     a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n;
+    a.pro_act = d.pro_act;
     const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
     if (d.mma == DCS_MMA_F16)
-        hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws,
+                           psc, psh);
     else
-        hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+        hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws,
+                           psc, psh);
     const int e = check_launch("wgrad3_win");
     return e ? -e : p.nsplit;
 }
@@ -772,29 +1265,74 @@ int win_check(const dcs_conv_desc& d, bool fwd) {
                       d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
                       d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs &&
                       d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_a_n > 0 &&
-                      d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL &&
-                      d.pro_act == DCS_ACT_NONE;
+                      d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL;
     if (!geom) return 0;
+    // a source prologue (IN apply + act at staging) on the forward only
+    const bool pro_ok = d.pro_act == DCS_ACT_NONE ||
+                        (fwd && d.Cs <= WIN_PRO_CMAX && (d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU ||
+                                                         d.pro_act == DCS_ACT_LRELU));
+    if (!pro_ok) return 0;
     if (fwd) return d.Ho == d.Hs && d.Wo == d.Ws && d.pt == 1 && d.pl == 1;
     return d.Ho == d.Hs + 2 && d.Wo == d.Ws + 2 && d.pt == 2 && d.pl == 2 && d.pad_mode == DCS_PAD_ZERO;
 }
 
 int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* src, const void* wh, const void* wl,
                const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s,
-               const IbwArgs* ibw = nullptr) {
+               const float* psc = nullptr, const float* psh = nullptr, const IbwArgs* ibw = nullptr) {
     WinArgs a;
     a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
+    a.pro_act = d.pro_act;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
     const IbwArgs ib = ibw ? *ibw : IbwArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-#define DCS_WIN_LAUNCH(NP_, IBW_)                                                                                   \
-    hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                     \
+#define DCS_WIN_LAUNCH(NP_, PRO_, IBW_)                                                                             \
+    hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, PRO_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,              \
+                       reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
+                       out, parts, psc, psh, ib);
+    const bool pro = d.pro_act != DCS_ACT_NONE;
+    static const bool v1 = getenv("DCS_WIN_V1") != nullptr;  // A/B: the first window kernel
+    if (!pro && !v1) {
+#define DCS_WIN2_LAUNCH(NP_, IBW_)                                                                                   \
+    hipLaunchKernelGGL((conv3_win2_kernel<NP_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                       \
                        reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
                        out, parts, ib);
-    if (d.mma == DCS_MMA_F16) {
-        if (ibw) { DCS_WIN_LAUNCH(1, true) } else { DCS_WIN_LAUNCH(1, false) }
+#define DCS_WIN2_KO(KO_)                                                                                              \
+    hipLaunchKernelGGL((conv3_win2_kernel<3, false, KO_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                   \
+                       reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
+                       out, parts, ib);
+        static const int ko = getenv("DCS_WIN2_KO") ? atoi(getenv("DCS_WIN2_KO")) : 0;  // timing probes
+        if (ko && d.mma == DCS_MMA_F16X3 && !ibw) {
+            switch (ko) {
+                case 1: DCS_WIN2_KO(1) break;
+                case 2: DCS_WIN2_KO(2) break;
+                case 3: DCS_WIN2_KO(3) break;
+                case 4: DCS_WIN2_KO(4) break;
+                case 6: DCS_WIN2_KO(6) break;
+                case 18: DCS_WIN2_KO(18) break;
+                case 22: DCS_WIN2_KO(22) break;
+                case 16: DCS_WIN2_KO(16) break;
+                case 34: DCS_WIN2_KO(34) break;
+                case 66: DCS_WIN2_KO(66) break;
+                case 98: DCS_WIN2_KO(98) break;
+                default: DCS_WIN2_KO(7) break;
+            }
+            return check_launch("conv3_win2 KO");
+        }
+#undef DCS_WIN2_KO
+        if (d.mma == DCS_MMA_F16) {
+            if (ibw) { DCS_WIN2_LAUNCH(1, true) } else { DCS_WIN2_LAUNCH(1, false) }
+        } else {
+            if (ibw) { DCS_WIN2_LAUNCH(3, true) } else { DCS_WIN2_LAUNCH(3, false) }
+        }
+#undef DCS_WIN2_LAUNCH
+        return check_launch("conv3_win2");
+    }
+    if (ibw) {
+        if (d.mma == DCS_MMA_F16) { DCS_WIN_LAUNCH(1, false, true) } else { DCS_WIN_LAUNCH(3, false, true) }
+    } else if (d.mma == DCS_MMA_F16) {
+        if (pro) { DCS_WIN_LAUNCH(1, true, false) } else { DCS_WIN_LAUNCH(1, false, false) }
     } else {
-        if (ibw) { DCS_WIN_LAUNCH(3, true) } else { DCS_WIN_LAUNCH(3, false) }
+        if (pro) { DCS_WIN_LAUNCH(3, true, false) } else { DCS_WIN_LAUNCH(3, false, false) }
     }
 #undef DCS_WIN_LAUNCH
     return check_launch("conv3_win");
@@ -835,15 +1373,16 @@ extern "C" int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, 
 
 extern "C" int dcs_conv3_win_ok(const dcs_conv_desc* dp, int dgrad) { return dp ? win_check(*dp, !dgrad) : 0; }
 
-extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
-                                      const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk,
-                                      void* stream) {
+extern "C" int dcs_conv3_win_in_stats_pro(const dcs_conv_desc* dp, const float* src, const float* pro_scale,
+                                          const float* pro_shift, const void* w_hi, const void* w_lo, const int* wexp,
+                                          float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
     if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "conv3_win: null pointer");
     const dcs_conv_desc& d = *dp;
+    if (d.pro_act != DCS_ACT_NONE && (!pro_scale || !pro_shift))
+        return fail(DCS_E_INVALID, "conv3_win: the source prologue needs pro_scale / pro_shift");
     if (!win_check(d, true))
         return fail(DCS_E_INVALID, "conv3_win: needs a 3x3 stride-1 'same' f16x3 conv over contiguous NHWC rows "
-                                   "(W <= 128, 256 % W == 0, H % (256 / W) == 0, Cs % 16 == 0, Co % 128 == 0, "
-                                   "no prologue)");
+                                   "(W <= 128, 256 % W == 0, H % (256 / W) == 0, Cs % 16 == 0, Co % 128 == 0)");
     const int tiles = d.Hs / (256 / d.Ws);
     if (parts) {
         if (!nchunk || parts_bytes < (size_t)d.N * tiles * d.Co * sizeof(Part))
@@ -851,7 +1390,15 @@ extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src,
         *nchunk = tiles;
     }
     return launch_win(d, d.Hs, d.Ws, d.pad_mode == DCS_PAD_REFLECT, src, w_hi, w_lo, wexp, nullptr, out,
-                      reinterpret_cast<Part*>(parts), as_stream(stream));
+                      reinterpret_cast<Part*>(parts), as_stream(stream), pro_scale, pro_shift);
+}
+
+extern "C" int dcs_conv3_win_in_stats(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
+                                      const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk,
+                                      void* stream) {
+    if (dp && dp->pro_act != DCS_ACT_NONE)
+        return fail(DCS_E_INVALID, "conv3_win: a descriptor with a prologue goes through dcs_conv3_win_in_stats_pro");
+    return dcs_conv3_win_in_stats_pro(dp, src, nullptr, nullptr, w_hi, w_lo, wexp, out, parts, parts_bytes, nchunk, stream);
 }
 
 extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* dy, const float* wpack,
@@ -897,7 +1444,7 @@ extern "C" int dcs_conv_dgrad_reflect_win_inbwd(const dcs_conv_desc* dp, const f
     const int tiles = d.Hs * d.Ws / 256;
     const int nch = tiles + IBW_FOLD_CHUNKS;
     const IbwArgs ib{y, scale, shift, reinterpret_cast<Sum2*>(parts), act, nch};
-    int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, nullptr, dx, nullptr, s, &ib);
+    int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, nullptr, dx, nullptr, s, nullptr, nullptr, &ib);
     if (e) return e;
     if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
     *nchunk = nch;

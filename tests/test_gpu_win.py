@@ -171,33 +171,6 @@ def test_win_f16_mode_vs_fp64(ops, N, H, W):
         assert max(errs) <= tol, (mode, errs)
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 16, 64), (1, 8, 128)])
-def test_win_prologue_vs_fp64(ops, N, H, W):
-    """The IN + ReLU prologue in the window staging (dcs_conv3_win_in_stats_pro, the window weight
-    gradient with pro_scale / pro_shift, the range record from the IN statistics by
-    dcs_range_from_in_stats): conv(relu(y * scale + shift)) forward and weight gradient within 1e-5 of
-    float64 on the same fp32 activation."""
-    from modules.hip.lib import ACT_RELU
-    ops.set_mma("f16x3")
-    g = _geom(ops)
-    y = rnd((N, 256, H, W), 101, "y").double()
-    w = torch.from_numpy(prng.normal(102, "w", (256, 256, 3, 3), 0, 0.05)).float().double().requires_grad_(True)
-    yd = y.float().to(DEV).permute(0, 2, 3, 1).contiguous()
-    st = ops.in_stats(yd, want_max=True)
-    a = torch.relu(yd.double() * st.scale.double()[:, None, None, :] + st.shift.double()[:, None, None, :])
-    a = a.permute(0, 3, 1, 2).cpu()
-    ref = F.conv2d(F.pad(a, (1, 1, 1, 1), mode="reflect"), w)
-    R = torch.from_numpy(prng.normal(103, "R", tuple(ref.shape))).float().double()
-    (ref * R).sum().backward()
-    pro = (st.scale, st.shift, ACT_RELU, ops.range_from_stats(st, ACT_RELU))
-    assert g.win_fits(H, W)
-    out, _ = g.forward_in_stats(ops.Src.nhwc(yd), g.pack_fwd(w.detach().float().to(DEV)), pro=pro)
-    assert _relmax(out.permute(0, 3, 1, 2), ref.detach()) <= 1e-5
-    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
-    dw = g.wgrad(Rd, ops.Src.nhwc(yd), pro=pro)
-    assert _relmax(dw, w.grad) <= 1e-5
-
-
 @pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128)])
 def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
     """The InstanceNorm backward of a = relu(IN(y)) with its partial sums fused into the window data
