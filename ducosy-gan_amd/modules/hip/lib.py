@@ -62,6 +62,12 @@ SIGNATURES = {
     "dcs_pack_weights_h3": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "dcs_conv3_win_ok": (c_int, [DP, c_int]),
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
+    "dcs_head_fwd_proj_ok": (c_int, [DP]),
+    "dcs_head_fwd_proj": (c_int, [DP, P, P, P, P, P, P, P, P]),
+    "dcs_head_wgrad_proj_workspace_size": (c_size_t, [DP]),
+    "dcs_head_wgrad_proj": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
+    "dcs_head_dgrad_in_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "dcs_head_dgrad_in": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P, P]),
     "dcs_conv_dgrad_reflect_win": (c_int, [DP, P, P, P, P, P, P, P, P, P]),
     "dcs_conv_dgrad_reflect_win_inbwd_parts_size": (c_size_t, [DP]),
     "dcs_conv_dgrad_reflect_win_inbwd": (c_int, [DP, P, P, P, P, P, P, P, P, P, P, c_int, P, c_size_t, P, P]),

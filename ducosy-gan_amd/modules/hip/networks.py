@@ -217,9 +217,9 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
         blocks.append(blk)
     yu1, su1 = L["up1"].forward_in_stats(Src.nhwc(h), pk["up1.w"])
     au1 = ops.in_apply(yu1, su1, ACT_RELU)
-    yu2, su2 = L["up2"].forward_in_stats(Src.nhwc(au1), pk["up2.w"])
+    yu2, su2 = L["up2"].forward_in_stats(Src.nhwc(au1), pk["up2.w"], want_max=True)
     out = L["head"].forward(Src.nhwc(yu2), pk["head.w"], bias=W["head.b"],
-                            pro=(su2.scale, su2.shift, ACT_RELU), epi_act=ACT_TANH)
+                            pro=(su2.scale, su2.shift, ACT_RELU), epi_act=ACT_TANH, pro_max=su2.xmax)
     out = out.view(N, 1, H, Wd)
     saved = None
     if keep:
@@ -246,11 +246,14 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     grads.put("head.b", lambda o: ops.channel_sum(dpre, out=o))
     su2, su1 = S["su2"], S["su1"]
     grads.put("head.w", lambda o: L["head"].wgrad(dpre, Src.nhwc(S["yu2"]), pro=(su2.scale, su2.shift, ACT_RELU),
-                                                   out=o))
-    da = L["head"].dgrad(dpre, L["head"].pack_dgrad(W["head.w"]), H, Wd)
+                                                   out=o, pro_max=su2.xmax))
+    wk = L["head"].pack_dgrad(W["head.w"])
+    dy = ops.head_dgrad_in(dpre, wk, S["yu2"], su2, ACT_RELU)
+    if dy is None:
+        da = L["head"].dgrad(dpre, wk, H, Wd)
+        dy = ops.in_act_backward(da, S["yu2"], su2, ACT_RELU)
     del dpre
     # up2
-    dy = ops.in_act_backward(da, S["yu2"], su2, ACT_RELU)
     grads.put("up2.w", lambda o: L["up2"].wgrad(dy, Src.nhwc(S["au1"]), out=o))
     da = L["up2"].dgrad(dy, L["up2"].pack_dgrad(W["up2.w"]), H // 2, Wd // 2)
     # up1

@@ -28,6 +28,9 @@ _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3
 # default f16x3: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
 # tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32, also for bf16x6) at half of bf16x6's MFMAs
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
+# the Generator head's forward by tap projection on the MFMA pipe in the fp16 modes
+# (csrc/conv_head.hip); "0" = the exact-f32 VALU kernel (A/B)
+_HEAD_PROJ = os.environ.get("DUCOSY_HEAD_PROJ", "1") == "1"
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -535,13 +538,22 @@ class ConvGeom:
 
     def forward(self, s: Src, wpack: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
-                epi_act: int = ACT_NONE) -> torch.Tensor:
+                epi_act: int = ACT_NONE, pro_max: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``pro_max``: per-(image, channel) max of the source before its prologue (INStats.xmax), for
+        the Generator head's tap-projection kernel in the fp16 modes (csrc/conv_head.hip)."""
         assert s.C == self.cin or (s.C == 4 and self.cin < 4), (s.C, self.cin)
         _check_dev(s.t, s.t2, wpack, bias)
         Ho, Wo = self.out_hw(s.H, s.W)
         pro_act = pro[2] if pro is not None else ACT_NONE
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
+        if self.narrow and _HEAD_PROJ and pro is not None and pro_max is not None and _h3() and s.t2 is None:
+            d.mma = _MMA
+            if lib.query("dcs_head_fwd_proj_ok", ctypes.byref(d)):
+                lib.call("dcs_head_fwd_proj", ctypes.byref(d), _p(s.t), _p(wpack), _p(bias), _p(pro[0]), _p(pro[1]),
+                         _p(pro_max), _p(out), _stream())
+                return out
+            d.mma = _fallback()
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
         if not self.narrow and s.t2 is None:
             _set_mma(d, s.t, pro, _wrng(wpack))
@@ -718,11 +730,22 @@ class ConvGeom:
     # ---- weight gradient ---------------------------------------------------------------
     def wgrad(self, dy: torch.Tensor, s: Src,
               pro: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """dL/dW in torch's OIHW layout."""
+              out: Optional[torch.Tensor] = None, pro_max: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """dL/dW in torch's OIHW layout.  ``pro_max``: as in forward (the head's projection path)."""
         _check_dev(dy, s.t, s.t2)
         pro_act = pro[2] if pro is not None else ACT_NONE
         d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
+        if self.narrow and _HEAD_PROJ and pro is not None and pro_max is not None and _h3() and s.t2 is None \
+                and dy.is_contiguous():
+            m0, d.mma = d.mma, _MMA
+            if lib.query("dcs_head_fwd_proj_ok", ctypes.byref(d)):
+                if out is None:
+                    out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device, dtype=torch.float32)
+                ws = workspace(lib.query("dcs_head_wgrad_proj_workspace_size", ctypes.byref(d)), dy.device)
+                lib.call("dcs_head_wgrad_proj", ctypes.byref(d), _p(dy), _p(s.t), _p(pro[0]), _p(pro[1]),
+                         _p(pro_max), _p(out), _p(ws), ws.numel(), _stream())
+                return out
+            d.mma = m0
         if not self.narrow and s.t2 is None and _h3() and s.t.is_contiguous():
             _set_mma(d, dy, None, range_rec(s.t, pro))
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
@@ -798,6 +821,23 @@ def in_act_backward(da: torch.Tensor, y: torch.Tensor, st: INStats, act: int) ->
     ws = workspace(nb, y.device)
     lib.call("dcs_in_act_backward", _p(da), _p(y), _p(st.scale), _p(st.shift), _p(dy), N, H * W, C,
              act, _p(ws), ws.numel(), _out_rng(dy), _stream())
+    return dy
+
+
+def head_dgrad_in(dy_out: torch.Tensor, wk: torch.Tensor, y: torch.Tensor, st: INStats, act: int) -> Optional[torch.Tensor]:
+    """in_act_backward(head.dgrad(dy_out), y, st, act) for the Generator head (7x7 reflect-pad-3
+    64 -> 1) in the fp16 operand modes, with the 64-channel data gradient recomputed on MFMA inside
+    the IN backward's two passes (dcs_head_dgrad_in).  ``wk``: the head's dgrad pack (K-major
+    [49 * 64][1]).  None where it does not apply (other modes, act, or images below 8 x 8)."""
+    N, H, W, C = y.shape
+    if not (_HEAD_PROJ and _h3() and C == 64 and act == ACT_RELU and H >= 8 and W >= 8 and y.is_contiguous()
+            and dy_out.numel() == N * H * W and wk.numel() == 49 * 64):
+        return None
+    _check_dev(dy_out, wk, y)
+    dy = torch.empty_like(y)
+    ws = workspace(lib.query("dcs_head_dgrad_in_workspace_size", N, H, W), y.device)
+    lib.call("dcs_head_dgrad_in", _p(dy_out.contiguous()), _p(wk), N, H, W, _p(y), _p(st.scale), _p(st.shift), act,
+             _MMA, _p(dy), _p(ws), ws.numel(), _out_rng(dy), _stream())
     return dy
 
 

@@ -346,6 +346,34 @@ int dcs_in_act_backward_parts(const float* da, const float* y, const float* scal
 int dcs_conv_rows_narrow(const dcs_conv_desc* d, const float* src, const float* src2,
                          const float* wpack, const float* bias, const float* pro_scale,
                          const float* pro_shift, float* out, void* stream);
+/* The Generator head (modules/model.py:112: ReflectionPad2d(3) + Conv 7x7 64 -> 1 (+ bias) + Tanh) forward
+ * in the fp16 operand modes, by tap projection on the MFMA pipe: z = a W (a = relu(src * pro_scale +
+ * pro_shift) per (image, channel), W [64][49] from wpack = the narrow pack, K-major (tap * 64 + c) * ldb),
+ * then a fixed-order 49-tap gather per output pixel.  d: the head's forward descriptor with pro_act =
+ * DCS_ACT_RELU, epi_act DCS_ACT_NONE / _TANH, mma DCS_MMA_F16X3 / _F16 (dcs_head_fwd_proj_ok).  xmax:
+ * [N][64] max of src per (image, channel) (dcs_in_stats_finish), for the operand scale.  out: [N][H][W]. */
+int dcs_head_fwd_proj_ok(const dcs_conv_desc* d);
+int dcs_head_fwd_proj(const dcs_conv_desc* d, const float* src, const float* wpack, const float* bias,
+                      const float* pro_scale, const float* pro_shift, const float* xmax, float* out, void* stream);
+/* The head's weight gradient in the same modes, by the transposed projection: dW[c][t] = sum_p a[p + off_t][c]
+ * dy[p] as an MFMA GEMM (M = 64 channels, N = 49 taps, K = source columns) per workgroup band, the
+ * workgroups' partials summed in a fixed order.  d, src, pro_scale, pro_shift, xmax as dcs_head_fwd_proj;
+ * dy: [N][H][W] gradient at the conv output (before the bias); dw: [1][64][7][7] (OIHW).
+ * ws: dcs_head_wgrad_proj_workspace_size(d) bytes. */
+size_t dcs_head_wgrad_proj_workspace_size(const dcs_conv_desc* d);
+int dcs_head_wgrad_proj(const dcs_conv_desc* d, const float* dy, const float* src, const float* pro_scale,
+                        const float* pro_shift, const float* xmax, float* dw, void* ws, size_t ws_bytes,
+                        void* stream);
+/* The head's data gradient fused with the InstanceNorm + ReLU backward of its input (modules/model.py:110-112
+ * backward) in the fp16 operand modes: da = the 7x7 reflect-pad-3 adjoint of dy_out onto 64 channels, on MFMA
+ * (never written), then dy = IN-ReLU-backward(da) given y (the IN input, NHWC [N][H][W][64]) and its
+ * per-(image, channel) scale / shift.  dy_out: [N][H][W] gradient at the head conv's output; wk: the weights
+ * K-major, wk[(ty * 7 + tx) * 64 + c] = W[0][c][ty][tx].  act: DCS_ACT_RELU; mma: DCS_MMA_F16X3 / _F16;
+ * H, W >= 8.  rng: optional range record of dy.  ws: dcs_head_dgrad_in_workspace_size(N, H, W) bytes. */
+size_t dcs_head_dgrad_in_workspace_size(int N, int H, int W);
+int dcs_head_dgrad_in(const float* dy_out, const float* wk, int N, int H, int W, const float* y, const float* scale,
+                      const float* shift, int act, int mma, float* dy, void* ws, size_t ws_bytes, float* rng,
+                      void* stream);
 size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* d);
 int dcs_conv_wgrad_narrow(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
                           const float* pro_scale, const float* pro_shift, float* dw, void* ws,

@@ -71,20 +71,21 @@ def main():
         x = torch.randn(N, H, H, g.cin, device=dev)
         w = torch.randn(g.cout, g.cin, g.k, g.k, device=dev) * 0.02
         pro = pro and not a.nopro
-        st = ops.in_stats(x) if pro else None
+        st = ops.in_stats(x, want_max=True) if pro else None
+        pm = st.xmax if (pro and g.narrow) else None  # the head's projection kernels
         p = (st.scale, st.shift, ACT_RELU) if pro else None
         Ho, Wo = g.out_hw(H, H)
         flop = 2.0 * N * Ho * Wo * g.cout * g.cin * g.k * g.k
         if g.cin < 4:  # production layout of the stem / PatchGAN layer 0: NHWC x 4 (zero channels)
             x = torch.nn.functional.pad(x, (0, 4 - g.cin))
         wp = g.pack_fwd(w, cin_pad=x.shape[-1])
-        t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p), a.reps)
+        t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p, pro_max=pm), a.reps)
         print(f"{name:8s} {'fwd':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
         dy = torch.randn(N, Ho, Wo, g.cout, device=dev)
         wd = g.pack_dgrad(w)
         t = timeit(lambda: g.dgrad(dy, wd, H, H), a.reps)
         print(f"{name:8s} {'dgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
-        t = timeit(lambda: g.wgrad(dy, Src.nhwc(x), pro=p), a.reps)
+        t = timeit(lambda: g.wgrad(dy, Src.nhwc(x), pro=p, pro_max=pm), a.reps)
         print(f"{name:8s} {'wgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}", flush=True)
 
 

@@ -1,0 +1,115 @@
+"""The Generator head's forward by tap projection (csrc/conv_head.hip dcs_head_fwd_proj, the fp16
+operand modes): out = tanh(b + conv7x7(ReflectionPad2d(3)(relu(IN(y))))) (modules/model.py:110-113)
+against float64 on the same fp32 activation and weights, and against the exact-f32 VALU kernel it
+replaces (conv_narrow.hip).  f16x3: max |err| / max |ref| <= 2e-6 before the tanh (the f32 kernel's
+own error is ~1e-6: both sum 3136 products in fp32); f16: <= 3e-3."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import prng
+from test_gpu_ops import rnd
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _relmax(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max())
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 40, 200), (2, 512, 512), (1, 7, 9)])
+@pytest.mark.parametrize("mode,tol", [("f16x3", 2e-6), ("f16", 3e-3)])
+def test_head_proj_vs_fp64(N, H, W, mode, tol):
+    from modules.hip import ops
+    from modules.hip.lib import ACT_NONE, ACT_RELU, ACT_TANH, DCS_PAD_REFLECT
+    prev = ops.get_mma()
+    ops.set_mma(mode)
+    try:
+        g = ops.ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT)
+        y = (rnd((N, 64, H, W), 31, "y") * 3.0 + 0.5).float().to(DEV).permute(0, 2, 3, 1).contiguous()
+        w = torch.from_numpy(prng.normal(32, "w", (1, 64, 7, 7), 0, 0.05)).float().to(DEV)
+        b = torch.tensor([0.1], device=DEV)
+        st = ops.in_stats(y, want_max=True)
+        a = torch.relu(y.double() * st.scale.double()[:, None, None, :] + st.shift.double()[:, None, None, :])
+        ref = F.conv2d(F.pad(a.permute(0, 3, 1, 2), (3, 3, 3, 3), mode="reflect"), w.double()) + 0.1
+        pk = g.pack_fwd(w)
+        pro = (st.scale, st.shift, ACT_RELU)
+        lin = g.forward(ops.Src.nhwc(y), pk, bias=b, pro=pro, epi_act=ACT_NONE, pro_max=st.xmax).view(N, 1, H, W)
+        th = g.forward(ops.Src.nhwc(y), pk, bias=b, pro=pro, epi_act=ACT_TANH, pro_max=st.xmax).view(N, 1, H, W)
+        valu = g.forward(ops.Src.nhwc(y), pk, bias=b, pro=pro, epi_act=ACT_NONE).view(N, 1, H, W)
+        e_proj, e_valu = _relmax(lin, ref), _relmax(valu, ref)
+        print(mode, (N, H, W), "proj", e_proj, "f32 VALU", e_valu)
+        assert e_proj <= tol, (e_proj, e_valu)
+        assert _relmax(th, torch.tanh(ref)) <= tol
+        assert not torch.equal(lin, valu)  # the projection kernel ran (it rounds differently)
+        torch.testing.assert_close(g.forward(ops.Src.nhwc(y), pk, bias=b, pro=pro, pro_max=st.xmax).view(N, 1, H, W),
+                                   lin, rtol=0, atol=0)  # deterministic
+    finally:
+        ops.set_mma(prev)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 40, 200), (2, 512, 512), (1, 7, 9)])
+@pytest.mark.parametrize("mode,tol", [("f16x3", 5e-6), ("f16", 5e-3)])
+def test_head_wgrad_proj_vs_fp64(N, H, W, mode, tol):
+    """dcs_head_wgrad_proj: dW of the same head against float64 autograd, and against the exact-f32
+    VALU kernel (conv_narrow.hip narrow_wgrad_win_kernel) it replaces."""
+    from modules.hip import ops
+    from modules.hip.lib import ACT_RELU, DCS_PAD_REFLECT
+    prev = ops.get_mma()
+    ops.set_mma(mode)
+    try:
+        g = ops.ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT)
+        y = (rnd((N, 64, H, W), 41, "y") * 3.0 + 0.5).float().to(DEV).permute(0, 2, 3, 1).contiguous()
+        dy = (rnd((N, 1, H, W), 42, "dy") * 1e-3).float().to(DEV)
+        st = ops.in_stats(y, want_max=True)
+        a = torch.relu(y.double() * st.scale.double()[:, None, None, :] + st.shift.double()[:, None, None, :])
+        ref = torch.nn.grad.conv2d_weight(F.pad(a.permute(0, 3, 1, 2), (3, 3, 3, 3), mode="reflect"),
+                                          (1, 64, 7, 7), dy.double())
+        pro = (st.scale, st.shift, ACT_RELU)
+        dyn = dy.permute(0, 2, 3, 1).contiguous()
+        dw = g.wgrad(dyn, ops.Src.nhwc(y), pro=pro, pro_max=st.xmax)
+        valu = g.wgrad(dyn, ops.Src.nhwc(y), pro=pro)
+        e_proj, e_valu = _relmax(dw, ref), _relmax(valu, ref)
+        print(mode, (N, H, W), "wgrad proj", e_proj, "f32 VALU", e_valu)
+        assert e_proj <= tol, (e_proj, e_valu)
+        assert not torch.equal(dw, valu)
+        torch.testing.assert_close(g.wgrad(dyn, ops.Src.nhwc(y), pro=pro, pro_max=st.xmax), dw, rtol=0, atol=0)
+    finally:
+        ops.set_mma(prev)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 40, 200), (2, 512, 512), (1, 8, 9)])
+@pytest.mark.parametrize("mode,tol", [("f16x3", 2e-5), ("f16", 5e-3)])
+def test_head_dgrad_in_vs_fp64(N, H, W, mode, tol):
+    """dcs_head_dgrad_in: IN-ReLU-backward of the head's data gradient (the padding adjoint folded)
+    against float64 autograd of relu(IN(y)) -> reflect pad 3 -> conv 7x7 64 -> 1, and against the
+    separate passes it replaces (dcs_conv_dgrad_c1 + dcs_in_act_backward)."""
+    from modules.hip import ops
+    from modules.hip.lib import ACT_RELU, DCS_PAD_REFLECT
+    prev = ops.get_mma()
+    ops.set_mma(mode)
+    try:
+        g = ops.ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT)
+        y = (rnd((N, 64, H, W), 51, "y") * 3.0 + 0.5).float().to(DEV).permute(0, 2, 3, 1).contiguous()
+        w = torch.from_numpy(prng.normal(52, "w", (1, 64, 7, 7), 0, 0.05)).float().to(DEV)
+        dout = (rnd((N, 1, H, W), 53, "dy") * 1e-3).float().to(DEV)
+        st = ops.in_stats(y, want_max=True)
+        yd = y.double().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        m = yd.mean((2, 3), keepdim=True)
+        v = yd.var((2, 3), unbiased=False, keepdim=True)
+        a = torch.relu((yd - m) / torch.sqrt(v + 1e-5))
+        out = F.conv2d(F.pad(a, (3, 3, 3, 3), mode="reflect"), w.double())
+        out.backward(dout.double())
+        ref = yd.grad.permute(0, 2, 3, 1)
+        wk = g.pack_dgrad(w)
+        dyn = dout.permute(0, 2, 3, 1).contiguous()
+        fused = ops.head_dgrad_in(dyn, wk, y, st, ACT_RELU)
+        assert fused is not None
+        sep = ops.in_act_backward(g.dgrad(dyn, wk, H, W), y, st, ACT_RELU)
+        e_f, e_s = _relmax(fused, ref), _relmax(sep, ref)
+        print(mode, (N, H, W), "dgrad+IN fused", e_f, "separate", e_s)
+        assert e_f <= tol, (e_f, e_s)
+        torch.testing.assert_close(ops.head_dgrad_in(dyn, wk, y, st, ACT_RELU), fused, rtol=0, atol=0)
+    finally:
+        ops.set_mma(prev)
