@@ -1147,6 +1147,10 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
         }
     };
     const __amdgpu_buffer_rsrc_t brsrc = src_rsrc(wp);
+    // f16x3 / f16 with pre-split weights (d.b_h3, dcs_pack_split_h3): B is staged without a split,
+    // rows [r][hi | lo][ldb] halves; the fp32 pack (wp) is then not read
+    const bool bpre = H3 && d.b_h3 != nullptr;
+    const __amdgpu_buffer_rsrc_t b3rsrc = src_rsrc(reinterpret_cast<const float*>(d.b_h3));
     auto load_b = [&](int kt, auto& dst) {
         if constexpr (MMA == MMA_BF16P) {  // slice-major packed B: the tile's 48 k are consecutive
             constexpr int BQ = BCH / 3;      // float4 per sub-tile: 2 (256 threads) or 1 (512)
@@ -1180,6 +1184,20 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
                     col = (long long)bt * d.Cs + bc;
                     advance16(bj, bc);
                 }
+                if (bpre) {  // 8 k: hi (16 B) into dst[2 sub], lo into dst[2 sub + 1]; 4 k: hi in .xy, lo in .zw
+                    const int oh = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * 2 * d.ldb + col) * 2) : OOB_OFF;
+                    const int ol = oh == OOB_OFF ? OOB_OFF : oh + 2 * d.ldb;
+                    if constexpr (BQ == 2) {
+                        dst[BQ * sub] = buf_load4(b3rsrc, oh);
+                        if constexpr (!F1) dst[BQ * sub + 1] = buf_load4(b3rsrc, ol);
+                    } else {
+                        const float2 h = buf_load2(b3rsrc, oh);
+                        float2 l = make_float2(0.f, 0.f);
+                        if constexpr (!F1) l = buf_load2(b3rsrc, ol);
+                        dst[BQ * sub] = make_float4(h.x, h.y, l.x, l.y);
+                    }
+                    continue;
+                }
                 const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
 #pragma unroll
                 for (int q = 0; q < BQ; ++q) dst[BQ * sub + q] = buf_load4(brsrc, off + 16 * q);
@@ -1202,6 +1220,14 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             if (ok) tap_decode(d, g, bj, ady, adx, bt);
             col = (long long)bt * d.Cs + bc;
             advance(bj, bc);
+        }
+        if (H3 && BCH == 1 && bpre) {  // 4 k: hi (8 B) in .xy, lo in .zw
+            const int oh = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * 2 * d.ldb + col) * 2) : OOB_OFF;
+            const float2 h = buf_load2(b3rsrc, oh);
+            float2 l = make_float2(0.f, 0.f);
+            if constexpr (!F1) l = buf_load2(b3rsrc, oh == OOB_OFF ? OOB_OFF : oh + 2 * d.ldb);
+            dst[0] = make_float4(h.x, h.y, l.x, l.y);
+            return;
         }
         if constexpr (X6F && DCS_BF16_BUFGATHER) {  // branch-free: k-tiles past the end read zeros
             const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
@@ -1271,12 +1297,22 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
                 *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, arow, akq >> 3)) = hi;
                 if constexpr (!F1) *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, arow, akq >> 3)) = lo;
                 if constexpr (BCH == 2 * NSUB) {
-                    split8h(sb[2 * sub], sb[2 * sub + 1], bsc, hi, lo);
+                    if (bpre) {
+                        hi = __builtin_bit_cast(f16x8, sb[2 * sub]);
+                        lo = __builtin_bit_cast(f16x8, sb[2 * sub + 1]);
+                    } else {
+                        split8h(sb[2 * sub], sb[2 * sub + 1], bsc, hi, lo);
+                    }
                     *reinterpret_cast<f16x8*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3)) = hi;
                     if constexpr (!F1) *reinterpret_cast<f16x8*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3)) = lo;
                 } else {  // 4 k of B per thread: the 8-byte half of a 16-byte chunk
                     f16x4 h4, l4;
-                    split4h(sb[sub], bsc, h4, l4);
+                    if (bpre) {
+                        h4 = __builtin_bit_cast(f16x4, make_float2(sb[sub].x, sb[sub].y));
+                        l4 = __builtin_bit_cast(f16x4, make_float2(sb[sub].z, sb[sub].w));
+                    } else {
+                        split4h(sb[sub], bsc, h4, l4);
+                    }
                     const int q = 4 * ((bkq >> 2) & 1);
                     *reinterpret_cast<f16x4*>(Ah + x6o(sub, buf, BM + brow, bkq >> 3) + q) = h4;
                     if constexpr (!F1) *reinterpret_cast<f16x4*>(Ah + x6o(NSUB + sub, buf, BM + brow, bkq >> 3) + q) = l4;
@@ -2154,6 +2190,34 @@ extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int
         hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
                            Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out);
     return check_launch("pack_weights");
+}
+
+namespace dcs {
+// pre-split B of the f16x3 / f16 rows pass: out[r][0][k] = hi, out[r][1][k] = lo of wpack[r][k] * 2^eb, eb the
+// exponent the rows kernel derives from the same range record (f16x3_exp), so the split is the one it would
+// do at staging (split8h)
+__global__ __launch_bounds__(256) void pack_split_h3_kernel(const float* __restrict__ wp, long long total, int ldb,
+                                                            const float* __restrict__ rng, int rng_n,
+                                                            _Float16* __restrict__ out) {
+    const float sc = __builtin_ldexpf(1.f, f16x3_exp(rng, rng_n));
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const long long r = i / ldb, k = i - r * ldb;
+        const float v = wp[i] * sc;
+        const _Float16 h = (_Float16)v;
+        out[2 * r * ldb + k] = h;
+        out[(2 * r + 1) * ldb + k] = (_Float16)(v - (float)h);
+    }
+}
+}  // namespace dcs
+
+extern "C" int dcs_pack_split_h3(const float* wpack, int rows, int ldb, const float* rng, int rng_n, void* out,
+                                 void* stream) {
+    if (!wpack || !rng || !out || rows <= 0 || ldb <= 0 || rng_n <= 0) return fail(DCS_E_INVALID, "pack_split_h3: bad arguments");
+    const long long total = (long long)rows * ldb;
+    const long long blocks = cdiv(total, 256) < 1024 ? cdiv(total, 256) : 1024;
+    hipLaunchKernelGGL(pack_split_h3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), wpack, total, ldb,
+                       rng, rng_n, reinterpret_cast<_Float16*>(out));
+    return check_launch("pack_split_h3");
 }
 
 namespace dcs {

@@ -426,37 +426,53 @@ __global__ __launch_bounds__(HW_NT, 2) void head_wgrad_proj_kernel(HeadArgs a, c
     }
 }
 
-// dw[c][t] (OIHW, Co = 1) = sum over the blocks, in block order, of part[block][t * 64 + c]
-__global__ void head_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, float* __restrict__ dw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // t * 64 + c
-    if (i >= HW_TAPS * HP_C) return;
+// dw[c][t] (OIHW, Co = 1) = sum over the blocks of part[block][t * 64 + c]: 64 outputs per workgroup,
+// four block groups (b = g mod 4) summed in block order each, then the four in a fixed order
+__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                                float* __restrict__ dw) {
+    __shared__ float red[4][64];
+    const int o = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + o;  // t * 64 + c
     float s = 0.f;
+    if (i < HW_TAPS * HP_C) {
 #pragma unroll 8
-    for (int b = 0; b < nblk; ++b) s += part[(long long)b * (HW_TAPS * HP_C) + i];
-    const int t = i / HP_C, c = i - t * HP_C;
-    dw[c * HW_TAPS + t] = s;
+        for (int b = grp; b < nblk; b += 4) s += part[(long long)b * (HW_TAPS * HP_C) + i];
+    }
+    red[grp][o] = s;
+    __syncthreads();
+    if (grp == 0 && i < HW_TAPS * HP_C) {
+        const float t4 = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+        const int t = i / HP_C, c = i - t * HP_C;
+        dw[c * HW_TAPS + t] = t4;
+    }
 }
 
 // Data gradient of the head fused with the InstanceNorm + ReLU backward of its input
 // (modules/model.py:110-112): da[p][c] = sum_t G[p][t] W[c][t], G[p][t] = sum over the padded
 // positions q that reflect onto p of g[q - off_t] (the padding adjoint folded into the one-channel
 // gradient, as dgrad_c1_kernel does), then dy = IN-ReLU-backward(da).  da is a GEMM (M = pixels,
-// N = 64 channels, K = 49 taps padded to 64) on the MFMA pipe and is never written: pass 0 computes
-// it per tile and reduces the IN backward's per-channel sums sum(da m) and sum(da m xhat) (m: ReLU
-// mask), pass 1 recomputes it (bit-identical: same tiles, scales and instruction sequence) and writes
-// dy.  HBM traffic: y once in pass 0, y + dy in pass 1, against da written, re-read twice and y read
-// twice by the separate dgrad / partial / apply passes.
-// Tile: HB_TR rows x 64 columns per workgroup, one row per wave (two 32-pixel MFMA blocks); the
-// one-channel g over the tile + 3-pixel halo is staged in LDS (fp32), and each lane builds its A
-// fragments (8 taps of one pixel) from it, interior tiles by one read per entry, border tiles by
-// the sum over the pixel's reflection preimages.
+// N = 64 channels, K = the 7 x 7 taps laid out as 8 kernel rows x 8 columns, the eighth of each
+// zero) on the MFMA pipe and is never written: pass 0 computes it per tile and reduces the IN
+// backward's per-channel sums sum(da m) and sum(da m xhat) (m: ReLU mask), pass 1 recomputes it
+// (bit-identical: same tiles, scales and instruction sequence) and writes dy.  HBM traffic: y once in
+// pass 0, y + dy in pass 1, against da written, re-read twice and y read twice by the separate
+// dgrad / partial / apply passes.
+// Tile: HB_TR rows x 64 columns, one row per wave (two 32-pixel MFMA blocks); the one-channel g over
+// the tile + 3-pixel halo is staged in LDS (fp32, plus a zero margin row and column for the padding
+// taps).  K step ks holds kernel rows 2 ks (lanes kh = 0) and 2 ks + 1 (kh = 1), columns 0..7, so a
+// lane's 8 entries are 8 consecutive window values (one row, descending columns).  Pixels away from
+// the border read them directly; the 3-pixel border sums its reflection preimages.  Workgroups are
+// persistent per image (HB_PP of them), so the partial sums come in HB_PP chunks per image.
 constexpr int HB_TR = 4, HB_TC = 64;
-constexpr int HB_WR = HB_TR + 2 * HP_R, HB_WC = HB_TC + 2 * HP_R;  // 10 x 70 g window
+constexpr int HB_WR = HB_TR + 2 * HP_R + 1, HB_WC = HB_TC + 2 * HP_R + 1;  // 11 x 71: window + margin
 constexpr int HB_NT = 64 * HB_TR;
+constexpr int HB_PP = 64;  // workgroups (partial-sum chunks) per image
 
 struct HeadBwdArgs {
     int N, H, W;
-    int tiles_x, tiles_y;  // per image; nchunk = tiles_x * tiles_y
+    int tiles_x, tiles_y;  // per image
+    int pp;                // workgroups per image
+    int grng_n;            // partial maxima in g's range record
 };
 
 __device__ __forceinline__ int hb_pre(int i, int n, int* a) {  // padded-row preimages of i (pad_preimages)
@@ -469,6 +485,7 @@ __device__ __forceinline__ int hb_pre(int i, int n, int* a) {  // padded-row pre
 
 template <int NP, int PASS>
 __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, const float* __restrict__ g,
+                                                               const float* __restrict__ grng,
                                                                const float* __restrict__ wk,
                                                                const float* __restrict__ y,
                                                                const float* __restrict__ sc,
@@ -476,142 +493,153 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                                                                const Sum2* __restrict__ coef,
                                                                Sum2* __restrict__ parts,
                                                                float* __restrict__ dy, float* __restrict__ rng) {
-    __shared__ float Gw[HB_WR][HB_WC];
+    __shared__ float Gw[HB_WR][HB_WC];  // Gw[1 + r][1 + c] = g[y0 - 3 + r][x0 - 3 + c]; row / column 0: zero
     __shared__ float red[HB_NT / 64][2][HP_C];
-    __shared__ float gred[HB_NT / 64];
 
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = blockIdx.x / a.pp, wg = blockIdx.x - n * a.pp;
     const int per = a.tiles_x * a.tiles_y;
-    const int n = L / per, chunk = L - n * per;
-    const int ty0 = chunk / a.tiles_x, tx0 = chunk - ty0 * a.tiles_x;
-    const int y0 = ty0 * HB_TR, x0 = tx0 * HB_TC;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int l32 = lane & 31, kh = lane >> 5;
     const int H = a.H, W = a.W;
-
-    // g window (zero outside the image) and its max |g|
-    float gm = 0.f;
     const float* gn = g + (long long)n * H * W;
-    for (int i = tid; i < HB_WR * HB_WC; i += HB_NT) {
-        const int r = i / HB_WC, c = i - r * HB_WC;
-        const int gy = y0 - HP_R + r, gx = x0 - HP_R + c;
-        const float v = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? gn[(long long)gy * W + gx] : 0.f;
-        Gw[r][c] = v;
-        gm = fmaxf(gm, fabsf(v));
-    }
-    gm = wave_max(gm);
-    if (lane == 0) gred[wid] = gm;
-    // weight scale (every wave: max |W| over the 3136 weights)
+
+    // weight scale (every wave: max |W| over the 3136 weights); g scale from g's range record, two
+    // binades lower since a folded entry sums up to four g values
     float wm = 0.f;
     for (int i = lane; i < HW_TAPS * HP_C; i += 64) wm = fmaxf(wm, fabsf(wk[i]));
     wm = wave_max(wm);
-    __syncthreads();
-    gm = fmaxf(fmaxf(gred[0], gred[1]), fmaxf(gred[2], gred[3]));
-    int eg, eb;
+    const int eg = f16x3_exp(grng, a.grng_n) - 2;
+    int eb;
     {
-        int e1 = 0, e2 = 0;
-        (void)frexpf(4.f * gm, &e1);  // a folded entry sums up to four g values
+        int e2 = 0;
         (void)frexpf(wm, &e2);
-        eg = __builtin_amdgcn_readfirstlane(min(max(15 - e1, -100), 100));
         eb = __builtin_amdgcn_readfirstlane(min(max(15 - e2, -100), 100));
     }
     const float gsc = __builtin_ldexpf(1.f, eg), bsc = __builtin_ldexpf(1.f, eb);
+    const int eab = -(eg + eb);
 
-    // B fragments: lane (channel nb * 32 + l32, h) holds W[c][t], t = 16 ks + 8 h .. + 7
+    // B fragments: lane (channel nb * 32 + l32, h) at step ks holds W[c][ty = 2 ks + h][tx = 0..7]
     f16x8 bh[2][4], bl[2][4];
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
+            const int ty = 2 * ks + kh;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int t = 16 * ks + 8 * kh + i;
-                const float v = t < HW_TAPS ? wk[t * HP_C + nb * 32 + l32] * bsc : 0.f;
+                const float v = (ty < HP_KS && i < HP_KS) ? wk[(ty * HP_KS + i) * HP_C + nb * 32 + l32] * bsc : 0.f;
                 const _Float16 h = (_Float16)v;
                 bh[nb][ks][i] = h;
                 bl[nb][ks][i] = (_Float16)(v - (float)h);
             }
         }
-
-    const int yy = y0 + wid;  // this wave's pixel row
-    const bool row_ok = yy < H;
-    // interior tile: every pixel has one preimage (rows / columns 4 .. n-5) and all g reads are primary
-    const bool inner = y0 > HP_R && y0 + HB_TR < H - 1 - HP_R && x0 > HP_R && x0 + HB_TC < W - 1 - HP_R;
-    const long long ybase = ((long long)n * H + (row_ok ? yy : 0)) * W;
-    const int eab = -(eg + eb);
+    float sclo[2], shlo[2];
+    Sum2 kk[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        sclo[nb] = sc[(long long)n * HP_C + nb * 32 + l32];
+        shlo[nb] = sh[(long long)n * HP_C + nb * 32 + l32];
+        kk[nb] = PASS == 1 ? coef[(long long)n * HP_C + nb * 32 + l32] : Sum2{0.f, 0.f};
+    }
 
     float psa[2] = {0.f, 0.f}, psb[2] = {0.f, 0.f};
     float rmax = 0.f;
 #pragma unroll 1
-    for (int mb = 0; mb < 2; ++mb) {
-        const int xl = mb * 32 + l32;  // the lane's A-row pixel (column within the tile)
-        const int xx = x0 + xl;
-        int ay[3], ax[3], ny = 1, nx = 1;
-        ay[0] = yy + HP_R;
-        ax[0] = xx + HP_R;
-        if (!inner) {
-            ny = hb_pre(yy, H, ay);
-            nx = hb_pre(xx, W, ax);
+    for (int chunk = wg; chunk < per; chunk += a.pp) {
+        const int tyi = chunk / a.tiles_x, txi = chunk - tyi * a.tiles_x;
+        const int y0 = tyi * HB_TR, x0 = txi * HB_TC;
+        __syncthreads();  // the previous tile's reads of Gw are done
+        for (int i = tid; i < HB_WR * HB_WC; i += HB_NT) {
+            const int r = i / HB_WC, c = i - r * HB_WC;
+            const int gy = y0 - HP_R - 1 + r, gx = x0 - HP_R - 1 + c;
+            Gw[r][c] = (r > 0 && c > 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) ? gn[(long long)gy * W + gx] : 0.f;
         }
-        floatx16 acc[2] = {};
+        __syncthreads();
+        const int yy = y0 + wid;  // this wave's pixel row
+        const bool row_ok = yy < H;
+        const int yc = row_ok ? yy : H - 1;
+#pragma unroll 1
+        for (int mb = 0; mb < 2; ++mb) {
+            const int xl = mb * 32 + l32;  // the lane's A-row pixel (column within the tile)
+            const int xx = x0 + xl;
+            // a lane's entries at step ks: Gw[1 + wid + 6 - (2 ks + kh)][1 + xl + 6 - i], i = 0..7
+            const bool lane_inner = yy > HP_R && yy < H - 1 - HP_R && xx > HP_R && xx < W - 1 - HP_R;
+            int ay[3], ax[3], ny = 1, nx = 1;
+            if (!lane_inner) {
+                ny = hb_pre(yy, H, ay);
+                nx = hb_pre(xx, W, ax);
+            }
+            floatx16 acc[2] = {};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            f16x8 ah, al;
+            for (int ks = 0; ks < 4; ++ks) {
+                const int ty = 2 * ks + kh;
+                float v[8];
+                if (lane_inner) {
+                    const float* rp = &Gw[1 + wid + 2 * HP_R - ty][1 + xl + 2 * HP_R];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int t = 16 * ks + 8 * kh + i;
-                float v = 0.f;
-                if (t < HW_TAPS) {
-                    const int tty = t / HP_KS, ttx = t - tty * HP_KS;
-                    if (inner) {
-                        v = Gw[wid + 2 * HP_R - tty][xl + 2 * HP_R - ttx];
-                    } else {
+                    for (int i = 0; i < 8; ++i) v[i] = rp[-i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        float s = 0.f;
                         for (int iy = 0; iy < ny; ++iy) {
-                            const int r = ay[iy] - tty;  // g row
+                            const int r = ay[iy] - ty;  // g row
                             if ((unsigned)r >= (unsigned)H) continue;
                             for (int ix = 0; ix < nx; ++ix) {
-                                const int c = ax[ix] - ttx;
-                                if ((unsigned)c < (unsigned)W) v += Gw[r - y0 + HP_R][c - x0 + HP_R];
+                                const int c = ax[ix] - i;
+                                if ((unsigned)c < (unsigned)W) s += Gw[1 + r - y0 + HP_R][1 + c - x0 + HP_R];
                             }
                         }
+                        v[i] = s;
                     }
                 }
-                v *= gsc;
-                const _Float16 h = (_Float16)v;
-                ah[i] = h;
-                al[i] = (_Float16)(v - (float)h);
+                f16x8 ah, al;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float f = v[i] * gsc;
+                    const _Float16 h = (_Float16)f;
+                    ah[i] = h;
+                    al[i] = (_Float16)(f - (float)h);
+                }
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    if constexpr (NP == 3) {
+                        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[nb][ks], acc[nb], 0, 0, 0);
+                        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[nb][ks], acc[nb], 0, 0, 0);
+                    }
+                    acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nb][ks], acc[nb], 0, 0, 0);
+                }
             }
+            // epilogue: lane (channel nb * 32 + l32) holds pixels (q & 3) + 8 (q >> 2) + 4 kh of the block;
+            // all 32 loads of y issued before the first use (clamped addresses, masked after)
+            float yv[2][16];
+            const long long ybase = ((long long)n * H + yc) * W;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int px = x0 + mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
+                    yv[nb][q] = y[(ybase + (px < W ? px : W - 1)) * HP_C + nb * 32 + l32];
+                }
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
-                if constexpr (NP == 3) {
-                    acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[nb][ks], acc[nb], 0, 0, 0);
-                    acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[nb][ks], acc[nb], 0, 0, 0);
-                }
-                acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nb][ks], acc[nb], 0, 0, 0);
-            }
-        }
-        // epilogue: lane (channel nb * 32 + l32) holds pixels (q & 3) + 8 (q >> 2) + 4 kh of the block
+                const int c = nb * 32 + l32;
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const int c = nb * 32 + l32;
-            const float s = sc[(long long)n * HP_C + c], b = sh[(long long)n * HP_C + c];
-            Sum2 k = {0.f, 0.f};
-            if constexpr (PASS == 1) k = coef[(long long)n * HP_C + c];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int px = x0 + mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
-                if (row_ok && px < W) {
-                    const long long o = (ybase + px) * HP_C + c;
+                for (int q = 0; q < 16; ++q) {
+                    const int px = x0 + mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
+                    const bool ok = row_ok && px < W;
                     const float da = __builtin_ldexpf(acc[nb][q], eab);
-                    const float xh = fmaf(y[o], s, b);
-                    const float gd = xh > 0.f ? da : 0.f;
+                    const float xh = fmaf(yv[nb][q], sclo[nb], shlo[nb]);
+                    const float gd = (ok && xh > 0.f) ? da : 0.f;
                     if constexpr (PASS == 0) {
                         psa[nb] += gd;
                         psb[nb] = fmaf(gd, xh, psb[nb]);
                     } else {
-                        const float v = s * (gd - k.a - xh * k.b);
-                        dy[o] = v;
-                        rmax = fmaxf(rmax, fabsf(v));
+                        const float o = sclo[nb] * (gd - kk[nb].a - xh * kk[nb].b);
+                        if (ok) {
+                            dy[(ybase + px) * HP_C + c] = o;
+                            rmax = fmaxf(rmax, fabsf(o));
+                        }
                     }
                 }
             }
@@ -620,6 +648,7 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
     if constexpr (PASS == 1) {
         range_note(rng, rmax);
     } else {
+        __syncthreads();
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             psa[nb] += __shfl_xor(psa[nb], 32, 64);
@@ -637,7 +666,7 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                 sa += red[w][0][tid];
                 sb += red[w][1][tid];
             }
-            parts[((long long)n * per + chunk) * HP_C + tid] = Sum2{sa, sb};
+            parts[((long long)n * a.pp + wg) * HP_C + tid] = Sum2{sa, sb};
         }
     }
 }
@@ -732,21 +761,21 @@ extern "C" int dcs_head_wgrad_proj(const dcs_conv_desc* dp, const float* dy, con
                            xmax, dy, part);
     int e = check_launch("head_wgrad_proj");
     if (e) return e;
-    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((unsigned)cdiv(HW_TAPS * HP_C, 256)), dim3(256), 0, s, part,
+    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((unsigned)cdiv(HW_TAPS * HP_C, 64)), dim3(256), 0, s, part,
                        (int)blocks, dw);
     return check_launch("head_wgrad_proj_reduce");
 }
 
 extern "C" size_t dcs_head_dgrad_in_workspace_size(int N, int H, int W) {
     if (N <= 0 || H <= 0 || W <= 0) return 0;
-    const long long nchunk = cdiv(H, HB_TR) * cdiv(W, HB_TC);
-    return align_up((size_t)N * nchunk * HP_C * sizeof(Sum2), 256) + (size_t)N * HP_C * sizeof(Sum2);
+    return align_up((size_t)N * HB_PP * HP_C * sizeof(Sum2), 256) + (size_t)N * HP_C * sizeof(Sum2);
 }
 
-extern "C" int dcs_head_dgrad_in(const float* dy_out, const float* wk, int N, int H, int W, const float* y,
-                                 const float* scale, const float* shift, int act, int mma, float* dy, void* ws,
-                                 size_t ws_bytes, float* rng, void* stream) {
-    if (!dy_out || !wk || !y || !scale || !shift || !dy || !ws) return fail(DCS_E_INVALID, "head_dgrad_in: null pointer");
+extern "C" int dcs_head_dgrad_in(const float* dy_out, const float* dy_rng, int dy_rng_n, const float* wk, int N, int H,
+                                 int W, const float* y, const float* scale, const float* shift, int act, int mma,
+                                 float* dy, void* ws, size_t ws_bytes, float* rng, void* stream) {
+    if (!dy_out || !dy_rng || dy_rng_n <= 0 || !wk || !y || !scale || !shift || !dy || !ws)
+        return fail(DCS_E_INVALID, "head_dgrad_in: null pointer");
     if (N <= 0 || H < 2 * HP_R + 2 || W < 2 * HP_R + 2 || act != DCS_ACT_RELU || (mma != DCS_MMA_F16X3 && mma != DCS_MMA_F16))
         return fail(DCS_E_INVALID, "head_dgrad_in: H, W >= 8, ReLU, f16x3 / f16 operands expected");
     if (ws_bytes < dcs_head_dgrad_in_workspace_size(N, H, W)) return fail(DCS_E_WORKSPACE, "head_dgrad_in: workspace too small");
@@ -754,28 +783,29 @@ extern "C" int dcs_head_dgrad_in(const float* dy_out, const float* wk, int N, in
     a.N = N; a.H = H; a.W = W;
     a.tiles_x = (int)cdiv(W, HB_TC);
     a.tiles_y = (int)cdiv(H, HB_TR);
-    const int nchunk = a.tiles_x * a.tiles_y;
-    const unsigned blocks = (unsigned)((long long)N * nchunk);
+    a.pp = a.tiles_x * a.tiles_y < HB_PP ? a.tiles_x * a.tiles_y : HB_PP;
+    a.grng_n = dy_rng_n;
+    const unsigned blocks = (unsigned)((long long)N * a.pp);
     Sum2* parts = reinterpret_cast<Sum2*>(ws);
-    Sum2* coef = reinterpret_cast<Sum2*>(reinterpret_cast<char*>(ws) + align_up((size_t)N * nchunk * HP_C * sizeof(Sum2), 256));
+    Sum2* coef = reinterpret_cast<Sum2*>(reinterpret_cast<char*>(ws) + align_up((size_t)N * HB_PP * HP_C * sizeof(Sum2), 256));
     hipStream_t s = as_stream(stream);
     int e;
     if (mma == DCS_MMA_F16)
-        hipLaunchKernelGGL((head_bwd_in_kernel<1, 0>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, wk, y, scale, shift,
+        hipLaunchKernelGGL((head_bwd_in_kernel<1, 0>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, dy_rng, wk, y, scale, shift,
                            nullptr, parts, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((head_bwd_in_kernel<3, 0>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, wk, y, scale, shift,
+        hipLaunchKernelGGL((head_bwd_in_kernel<3, 0>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, dy_rng, wk, y, scale, shift,
                            nullptr, parts, nullptr, nullptr);
     if ((e = check_launch("head_dgrad_in_partial"))) return e;
     hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv((long long)N * HP_C, 256)), dim3(256), 0, s, parts,
-                       N, nchunk, H * W, coef);
+                       N, a.pp, H * W, coef);
     if ((e = check_launch("head_dgrad_in_finalize"))) return e;
     if ((e = range_zero(rng, s))) return e;
     if (mma == DCS_MMA_F16)
-        hipLaunchKernelGGL((head_bwd_in_kernel<1, 1>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, wk, y, scale, shift,
+        hipLaunchKernelGGL((head_bwd_in_kernel<1, 1>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, dy_rng, wk, y, scale, shift,
                            coef, nullptr, dy, rng);
     else
-        hipLaunchKernelGGL((head_bwd_in_kernel<3, 1>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, wk, y, scale, shift,
+        hipLaunchKernelGGL((head_bwd_in_kernel<3, 1>), dim3(blocks), dim3(HB_NT), 0, s, a, dy_out, dy_rng, wk, y, scale, shift,
                            coef, nullptr, dy, rng);
     return check_launch("head_dgrad_in_apply");
 }

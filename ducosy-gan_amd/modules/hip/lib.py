@@ -33,6 +33,7 @@ class ConvDesc(ctypes.Structure):
         ("ldb", c_int32), ("pro_act", c_int32), ("epi_act", c_int32), ("mma", c_int32),
         ("korder", c_int32),
         ("rng_a_n", c_int32), ("rng_b_n", c_int32), ("rng_a", c_void_p), ("rng_b", c_void_p),
+        ("b_h3", c_void_p),
     ]
 
 
@@ -62,12 +63,19 @@ SIGNATURES = {
     "dcs_pack_weights_h3": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "dcs_conv3_win_ok": (c_int, [DP, c_int]),
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
+    "dcs_pack_split_h3": (c_int, [P, c_int, c_int, P, c_int, P, P]),
+    "dcs_stem_fwd_ok": (c_int, [DP]),
+    "dcs_stem_fwd_parts_size": (c_size_t, [DP]),
+    "dcs_stem_fwd": (c_int, [DP, P, P, P, P, c_size_t, POINTER(c_int), P]),
+    "dcs_stem_wgrad_ok": (c_int, [DP]),
+    "dcs_stem_wgrad_workspace_size": (c_size_t, [DP]),
+    "dcs_stem_wgrad": (c_int, [DP, P, P, P, P, c_size_t, P]),
     "dcs_head_fwd_proj_ok": (c_int, [DP]),
     "dcs_head_fwd_proj": (c_int, [DP, P, P, P, P, P, P, P, P]),
     "dcs_head_wgrad_proj_workspace_size": (c_size_t, [DP]),
     "dcs_head_wgrad_proj": (c_int, [DP, P, P, P, P, P, P, P, c_size_t, P]),
     "dcs_head_dgrad_in_workspace_size": (c_size_t, [c_int, c_int, c_int]),
-    "dcs_head_dgrad_in": (c_int, [P, P, c_int, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P, P]),
+    "dcs_head_dgrad_in": (c_int, [P, P, c_int, P, c_int, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P, P]),
     "dcs_conv_dgrad_reflect_win": (c_int, [DP, P, P, P, P, P, P, P, P, P]),
     "dcs_conv_dgrad_reflect_win_inbwd_parts_size": (c_size_t, [DP]),
     "dcs_conv_dgrad_reflect_win_inbwd": (c_int, [DP, P, P, P, P, P, P, P, P, P, P, c_int, P, c_size_t, P, P]),

@@ -31,6 +31,8 @@ _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
 # the Generator head's forward by tap projection on the MFMA pipe in the fp16 modes
 # (csrc/conv_head.hip); "0" = the exact-f32 VALU kernel (A/B)
 _HEAD_PROJ = os.environ.get("DUCOSY_HEAD_PROJ", "1") == "1"
+_BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"
+_STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -193,11 +195,14 @@ def _drop_rng(t: torch.Tensor) -> None:
         del t._dcs_rng
 
 
-def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[torch.Tensor]) -> None:
+def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[torch.Tensor],
+             wpack: Optional[torch.Tensor] = None) -> None:
     """Operand mode of one MFMA pass.  f16x3 needs the range records of both operands: ``a`` (the
     gathered tensor, contiguous, with its prologue) and ``b_rng`` (the packed weights' record, or the
-    wgrad source's); a pass without them (concat or strided sources) runs bf16x6."""
+    wgrad source's); a pass without them (concat or strided sources) runs bf16x6.  ``wpack``: the
+    rows pass's packed weights, whose pre-split planes (if any) it then stages directly."""
     d.mma = _MMA
+    d.b_h3 = None
     if not _h3():
         return
     if a is None or b_rng is None or not a.is_contiguous() or (a.numel() // a.shape[0]) % 4 or a.data_ptr() % 16:
@@ -206,6 +211,9 @@ def _set_mma(d: lib.ConvDesc, a: Optional[torch.Tensor], a_pro, b_rng: Optional[
     ra = range_rec(a, a_pro)
     d.rng_a, d.rng_a_n = ra.data_ptr(), ra.numel()
     d.rng_b, d.rng_b_n = b_rng.data_ptr(), b_rng.numel()
+    bh = getattr(wpack, "_dcs_bh3", None) if wpack is not None else None
+    if bh is not None and bh[0] == wpack._version:
+        d.b_h3 = bh[1].data_ptr()
 
 
 # ---------------------------------------------------------------------------------------
@@ -447,6 +455,10 @@ class ConvGeom:
             lib.call("dcs_pack_weights_r", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
                      cols, nmajor, _p(out), _p(rng), _stream())
             out._dcs_rng = (out._version, None, ACT_NONE, rng)
+            if _BPRE and not self.win:  # pre-split fp16 planes for the rows pass (dcs_conv_desc.b_h3)
+                planes = torch.empty(cols * 2 * Kpad, device=w.device, dtype=torch.float16)
+                lib.call("dcs_pack_split_h3", _p(out), cols, Kpad, _p(rng), lib.RANGE_PARTS, _p(planes), _stream())
+                out._dcs_bh3 = (out._version, planes)
         else:
             lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
                      cols, nmajor, _p(out), _stream())
@@ -489,7 +501,9 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro[2] if pro is not None else ACT_NONE, epi_act)
         nb = 0 if (self.narrow or not _FUSE_STATS) else lib.query("dcs_conv_rows_in_stats_parts_size", ctypes.byref(d))
         if nb and s.t2 is None:
-            _set_mma(d, s.t, pro, _wrng(wpack))
+            _set_mma(d, s.t, pro, _wrng(wpack), wpack)
+        if nb and _STEM and bias is None and lib.query("dcs_stem_fwd_ok", ctypes.byref(d)):
+            return self._stem(s, d, wpack, True, want_max)
         h3 = getattr(wpack, "_dcs_h3", None)
         if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
             return self._win_in_stats(s, d, h3, nb, want_max)
@@ -507,6 +521,26 @@ class ConvGeom:
                  _p(pro[0]) if pro else None, _p(pro[1]) if pro else None, _p(out), _p(parts), parts.numel(),
                  ctypes.byref(nchunk), _stream())
         PROBE.end(e0, 2.0 * s.N * Ho * Wo * self.cout * self.cin * self.k * self.k)
+        C = self.cout
+        scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        shift = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        xmax = torch.empty(s.N, C, device=dev, dtype=torch.float32) if want_max else None
+        xam = torch.empty(s.N, C, device=dev, dtype=torch.int32) if want_max else None
+        lib.call("dcs_in_stats_finish", _p(parts), s.N, C, nchunk.value, IN_EPS, _p(scale), _p(shift), _p(xmax),
+                 _p(xam), _stream())
+        return out, INStats(scale, shift, xmax, xam)
+
+    def _stem(self, s: Src, d, wpack, stats: bool, want_max: bool = False):
+        """The Generator stem (7x7 reflect-pad-3, NHWC x 4 source -> 64) on its MFMA kernel
+        (csrc/conv_stem.hip), with the IN statistics of its output when ``stats``."""
+        dev = s.t.device
+        out = torch.empty(s.N, s.H, s.W, self.cout, device=dev, dtype=torch.float32)
+        parts = workspace(lib.query("dcs_stem_fwd_parts_size", ctypes.byref(d)), dev) if stats else None
+        nchunk = ctypes.c_int(0)
+        lib.call("dcs_stem_fwd", ctypes.byref(d), _p(s.t), _p(wpack), _p(out), _p(parts),
+                 parts.numel() if stats else 0, ctypes.byref(nchunk), _stream())
+        if not stats:
+            return out
         C = self.cout
         scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
         shift = torch.empty(s.N, C, device=dev, dtype=torch.float32)
@@ -556,7 +590,9 @@ class ConvGeom:
             d.mma = _fallback()
         fn = "dcs_conv_rows_narrow" if self.narrow else "dcs_conv_rows"
         if not self.narrow and s.t2 is None:
-            _set_mma(d, s.t, pro, _wrng(wpack))
+            _set_mma(d, s.t, pro, _wrng(wpack), wpack)
+            if _STEM and bias is None and lib.query("dcs_stem_fwd_ok", ctypes.byref(d)):
+                return self._stem(s, d, wpack, False)
         h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
         if h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
@@ -612,7 +648,7 @@ class ConvGeom:
         d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
         d.mma = _fallback() if _h3() else _MMA
         if not narrow:
-            _set_mma(d, dy, None, _wrng(wpack_d))
+            _set_mma(d, dy, None, _wrng(wpack_d), wpack_d)
         d.korder = lib.KORDER_SLICE if (self.kslice and ci > 4) else lib.KORDER_TAP
         d.Co = ci
         dev = dy.device
@@ -754,6 +790,10 @@ class ConvGeom:
         if out is None:
             out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device,
                               dtype=torch.float32)
+        if _STEM and pro is None and dy.is_contiguous() and lib.query("dcs_stem_wgrad_ok", ctypes.byref(d)):
+            ws = workspace(lib.query("dcs_stem_wgrad_workspace_size", ctypes.byref(d)), dy.device)
+            lib.call("dcs_stem_wgrad", ctypes.byref(d), _p(dy), _p(s.t), _p(out), _p(ws), ws.numel(), _stream())
+            return out
         if self.narrow:
             nb = lib.query("dcs_conv_wgrad_narrow_workspace_size", ctypes.byref(d))
             ws = workspace(nb, dy.device)
@@ -836,8 +876,10 @@ def head_dgrad_in(dy_out: torch.Tensor, wk: torch.Tensor, y: torch.Tensor, st: I
     _check_dev(dy_out, wk, y)
     dy = torch.empty_like(y)
     ws = workspace(lib.query("dcs_head_dgrad_in_workspace_size", N, H, W), y.device)
-    lib.call("dcs_head_dgrad_in", _p(dy_out.contiguous()), _p(wk), N, H, W, _p(y), _p(st.scale), _p(st.shift), act,
-             _MMA, _p(dy), _p(ws), ws.numel(), _out_rng(dy), _stream())
+    g = dy_out.contiguous()
+    g_rng = range_rec(g.view(N, H, W, 1))
+    lib.call("dcs_head_dgrad_in", _p(g), _p(g_rng), g_rng.numel(), _p(wk), N, H, W, _p(y), _p(st.scale), _p(st.shift),
+             act, _MMA, _p(dy), _p(ws), ws.numel(), _out_rng(dy), _stream())
     return dy
 
 

@@ -81,6 +81,9 @@ typedef struct dcs_conv_desc {
                                     /* max an upper bound of every value (dcs_range_parts) */
     const float* rng_b;             /* F16X3: the same for the other operand (rows: the   */
                                     /* packed weights, dcs_pack_weights_r; wgrad: source) */
+    const void* b_h3;               /* F16X3 / F16 rows pass, optional: the packed weights */
+                                    /* pre-split by dcs_pack_split_h3 (B staged without a */
+                                    /* split); NULL: split at staging                     */
 } dcs_conv_desc;
 
 /* K order of the rows pass.  TAP: k = tap * Cs + c.  SLICE: k = (c / 16) * taps * 16 + tap * 16 +
@@ -369,11 +372,34 @@ int dcs_head_wgrad_proj(const dcs_conv_desc* d, const float* dy, const float* sr
  * (never written), then dy = IN-ReLU-backward(da) given y (the IN input, NHWC [N][H][W][64]) and its
  * per-(image, channel) scale / shift.  dy_out: [N][H][W] gradient at the head conv's output; wk: the weights
  * K-major, wk[(ty * 7 + tx) * 64 + c] = W[0][c][ty][tx].  act: DCS_ACT_RELU; mma: DCS_MMA_F16X3 / _F16;
- * H, W >= 8.  rng: optional range record of dy.  ws: dcs_head_dgrad_in_workspace_size(N, H, W) bytes. */
+ * H, W >= 8.  dy_rng: the range record of dy_out (dy_rng_n partial maxima, dcs_range_parts); rng: optional
+ * range record of dy.  ws: dcs_head_dgrad_in_workspace_size(N, H, W) bytes. */
 size_t dcs_head_dgrad_in_workspace_size(int N, int H, int W);
-int dcs_head_dgrad_in(const float* dy_out, const float* wk, int N, int H, int W, const float* y, const float* scale,
-                      const float* shift, int act, int mma, float* dy, void* ws, size_t ws_bytes, float* rng,
-                      void* stream);
+int dcs_head_dgrad_in(const float* dy_out, const float* dy_rng, int dy_rng_n, const float* wk, int N, int H, int W,
+                      const float* y, const float* scale, const float* shift, int act, int mma, float* dy, void* ws,
+                      size_t ws_bytes, float* rng, void* stream);
+/* The Generator stem (modules/model.py:96-98: ReflectionPad2d(3) + Conv 7x7 cin -> 64 over the NHWC x 4
+ * packed image, dcs_pack_nhwc4) forward in the f16x3 / f16 operand modes, on MFMA with the weights resident
+ * in LDS.  d: the rows-pass descriptor of that conv (Cs = 4, pro_act / epi_act none, mma F16X3 / F16 with
+ * both range records, ldb the packed weights' Kpad; dcs_stem_fwd_ok).  wpack: the rows pack (tap * 4 + c
+ * K order).  parts (optional): per-(image, tile, channel) InstanceNorm partials for dcs_in_stats_finish
+ * (dcs_stem_fwd_parts_size bytes; *nchunk receives the tiles per image). */
+int dcs_stem_fwd_ok(const dcs_conv_desc* d);
+size_t dcs_stem_fwd_parts_size(const dcs_conv_desc* d);
+int dcs_stem_fwd(const dcs_conv_desc* d, const float* src, const float* wpack, float* out, void* parts,
+                 size_t parts_bytes, int* nchunk, void* stream);
+/* The stem's weight gradient in the same modes (rows pass over 64 output channels x 7 kernel-row blocks,
+ * K = output pixels, on MFMA): d as for dcs_stem_fwd with cw = the weights' input channels (<= 4), rng_a
+ * the range record of dy and rng_b that of the source; dw: [64][cw][7][7] (OIHW).
+ * ws: dcs_stem_wgrad_workspace_size(d) bytes. */
+int dcs_stem_wgrad_ok(const dcs_conv_desc* d);
+size_t dcs_stem_wgrad_workspace_size(const dcs_conv_desc* d);
+int dcs_stem_wgrad(const dcs_conv_desc* d, const float* dy, const float* src, float* dw, void* ws, size_t ws_bytes,
+                   void* stream);
+/* Pre-split fp16 planes of an N-major packed weight tensor for the f16x3 / f16 rows pass (dcs_conv_desc.b_h3):
+ * out[r][0][k] = hi, out[r][1][k] = lo of wpack[r][k] * 2^e (fp16), e the operand exponent of the pack's range
+ * record rng (dcs_pack_weights_r).  out: rows * 2 * ldb halves. */
+int dcs_pack_split_h3(const float* wpack, int rows, int ldb, const float* rng, int rng_n, void* out, void* stream);
 size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* d);
 int dcs_conv_wgrad_narrow(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
                           const float* pro_scale, const float* pro_shift, float* dw, void* ws,

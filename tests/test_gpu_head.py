@@ -95,19 +95,25 @@ def test_head_dgrad_in_vs_fp64(N, H, W, mode, tol):
         w = torch.from_numpy(prng.normal(52, "w", (1, 64, 7, 7), 0, 0.05)).float().to(DEV)
         dout = (rnd((N, 1, H, W), 53, "dy") * 1e-3).float().to(DEV)
         st = ops.in_stats(y, want_max=True)
-        yd = y.double().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        # reference on the CPU (float64 autograd)
+        yd = y.double().cpu().permute(0, 3, 1, 2).clone().requires_grad_(True)
         m = yd.mean((2, 3), keepdim=True)
         v = yd.var((2, 3), unbiased=False, keepdim=True)
-        a = torch.relu((yd - m) / torch.sqrt(v + 1e-5))
-        out = F.conv2d(F.pad(a, (3, 3, 3, 3), mode="reflect"), w.double())
-        out.backward(dout.double())
-        ref = yd.grad.permute(0, 2, 3, 1)
+        xh = (yd - m) / torch.sqrt(v + 1e-5)
+        a = torch.relu(xh)
+        out = F.conv2d(F.pad(a, (3, 3, 3, 3), mode="reflect"), w.double().cpu())
+        out.backward(dout.double().cpu())
+        ref = yd.grad.permute(0, 2, 3, 1).to(DEV)
+        # elements whose normalised value is within fp32 rounding of the ReLU kink may take either side
+        # of it (a few in 3e7 at 512 x 512); they are left out of the max-error check
+        safe = (xh.detach().abs() > 1e-4).permute(0, 2, 3, 1).to(DEV)
         wk = g.pack_dgrad(w)
         dyn = dout.permute(0, 2, 3, 1).contiguous()
         fused = ops.head_dgrad_in(dyn, wk, y, st, ACT_RELU)
         assert fused is not None
         sep = ops.in_act_backward(g.dgrad(dyn, wk, H, W), y, st, ACT_RELU)
-        e_f, e_s = _relmax(fused, ref), _relmax(sep, ref)
+        e_f = _relmax(torch.where(safe, fused, ref), ref)
+        e_s = _relmax(torch.where(safe, sep, ref), ref)
         print(mode, (N, H, W), "dgrad+IN fused", e_f, "separate", e_s)
         assert e_f <= tol, (e_f, e_s)
         torch.testing.assert_close(ops.head_dgrad_in(dyn, wk, y, st, ACT_RELU), fused, rtol=0, atol=0)
