@@ -87,6 +87,12 @@ def main():
         print(f"{name:8s} {'dgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
         t = timeit(lambda: g.wgrad(dy, Src.nhwc(x), pro=p, pro_max=pm), a.reps)
         print(f"{name:8s} {'wgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}", flush=True)
+        if name == "head" and pro:  # the data gradient with the IN + ReLU backward of its input
+            t = timeit(lambda: ops.in_act_backward(g.dgrad(dy, wd, H, H), x, st, ACT_RELU), a.reps)
+            print(f"{name:8s} {'dg+in':6s} {t:9.3f} {'sep':>9s}")
+            if ops.head_dgrad_in(dy, wd, x, st, ACT_RELU) is not None:
+                t = timeit(lambda: ops.head_dgrad_in(dy, wd, x, st, ACT_RELU), a.reps)
+                print(f"{name:8s} {'dg+in':6s} {t:9.3f} {'fused':>9s}", flush=True)
 
 
 if __name__ == "__main__":
