@@ -544,17 +544,36 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
 
     float psa[2] = {0.f, 0.f}, psb[2] = {0.f, 0.f};
     float rmax = 0.f;
+    // g window of a tile, HB_GU values per thread, loaded one tile ahead (unconditional loads from
+    // clamped addresses, the zero fill applied at the LDS store)
+    constexpr int HB_GU = (HB_WR * HB_WC + HB_NT - 1) / HB_NT;
+    float gv[HB_GU];
+    auto load_g = [&](int chunk) {
+        const int tyi = chunk / a.tiles_x, txi = chunk - tyi * a.tiles_x;
+#pragma unroll
+        for (int q = 0; q < HB_GU; ++q) {
+            const int i = tid + q * HB_NT;
+            const int r = i / HB_WC, c = i - r * HB_WC;
+            const int gy = tyi * HB_TR - HP_R - 1 + r, gx = txi * HB_TC - HP_R - 1 + c;
+            gv[q] = gn[(long long)min(max(gy, 0), H - 1) * W + min(max(gx, 0), W - 1)];
+        }
+    };
+    if (wg < per) load_g(wg);
 #pragma unroll 1
     for (int chunk = wg; chunk < per; chunk += a.pp) {
         const int tyi = chunk / a.tiles_x, txi = chunk - tyi * a.tiles_x;
         const int y0 = tyi * HB_TR, x0 = txi * HB_TC;
         __syncthreads();  // the previous tile's reads of Gw are done
-        for (int i = tid; i < HB_WR * HB_WC; i += HB_NT) {
+#pragma unroll
+        for (int q = 0; q < HB_GU; ++q) {
+            const int i = tid + q * HB_NT;
             const int r = i / HB_WC, c = i - r * HB_WC;
             const int gy = y0 - HP_R - 1 + r, gx = x0 - HP_R - 1 + c;
-            Gw[r][c] = (r > 0 && c > 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) ? gn[(long long)gy * W + gx] : 0.f;
+            if (i < HB_WR * HB_WC)
+                Gw[r][c] = (r > 0 && c > 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) ? gv[q] : 0.f;
         }
         __syncthreads();
+        if (chunk + a.pp < per) load_g(chunk + a.pp);  // in flight across this tile
         const int yy = y0 + wid;  // this wave's pixel row
         const bool row_ok = yy < H;
         const int yc = row_ok ? yy : H - 1;
@@ -569,6 +588,16 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                 ny = hb_pre(yy, H, ay);
                 nx = hb_pre(xx, W, ax);
             }
+            // y of the block's outputs: all 32 loads issued before the MFMAs (clamped addresses, masked after)
+            float yv[2][16];
+            const long long ybase = ((long long)n * H + yc) * W;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int px = x0 + mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
+                    yv[nb][q] = y[(ybase + (px < W ? px : W - 1)) * HP_C + nb * 32 + l32];
+                }
             floatx16 acc[2] = {};
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
@@ -610,17 +639,7 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                     acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nb][ks], acc[nb], 0, 0, 0);
                 }
             }
-            // epilogue: lane (channel nb * 32 + l32) holds pixels (q & 3) + 8 (q >> 2) + 4 kh of the block;
-            // all 32 loads of y issued before the first use (clamped addresses, masked after)
-            float yv[2][16];
-            const long long ybase = ((long long)n * H + yc) * W;
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int px = x0 + mb * 32 + (q & 3) + 8 * (q >> 2) + 4 * kh;
-                    yv[nb][q] = y[(ybase + (px < W ? px : W - 1)) * HP_C + nb * 32 + l32];
-                }
+            // epilogue: lane (channel nb * 32 + l32) holds pixels (q & 3) + 8 (q >> 2) + 4 kh of the block
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
                 const int c = nb * 32 + l32;
