@@ -291,12 +291,26 @@ __device__ __forceinline__ RowInfo row_info(const dcs_conv_desc& d, const ClassG
         // the one-pixel ring of the (H+2) x (W+2) padded grid only (dcs_conv_dgrad_reflect_win: the
         // interior comes from the window kernel), rows in the ring buffer's order: top row, bottom
         // row, then (left, right) of rows 1..H; out_off indexes the ring buffer
+        // The rows are enumerated segment by segment over the whole batch (every image's top row,
+        // then every bottom row, left column, right column), so a 128-row tile lies in one segment
+        // and reads only that segment's kernel row / column of taps (ring_tap_mask)
         const int H = d.Ho - 2, ringlen = 2 * d.Wo + 2 * H;
         if (m >= ringlen * d.N) { r.n = 0; r.by = -100000; r.bx = -100000; r.out_off = -1; return r; }
-        const int n = m / ringlen, idx = m - n * ringlen;
-        int oy, ox;
-        if (idx < 2 * d.Wo) { oy = idx < d.Wo ? 0 : d.Ho - 1; ox = idx < d.Wo ? idx : idx - d.Wo; }
-        else { const int u = idx - 2 * d.Wo; oy = 1 + (u >> 1); ox = (u & 1) ? d.Wo - 1 : 0; }
+        int n, idx, oy, ox;
+        const int sw = d.N * d.Wo, sh = d.N * H;
+        if (m < 2 * sw) {  // top / bottom rows
+            const int u = m < sw ? m : m - sw;
+            n = u / d.Wo;
+            ox = u - n * d.Wo;
+            oy = m < sw ? 0 : d.Ho - 1;
+            idx = (m < sw ? 0 : d.Wo) + ox;
+        } else {           // left / right columns of rows 1 .. H
+            const int v = m - 2 * sw, right = v >= sh ? 1 : 0, u = right ? v - sh : v;
+            n = u / H;
+            oy = 1 + (u - n * H);
+            ox = right ? d.Wo - 1 : 0;
+            idx = 2 * d.Wo + 2 * (oy - 1) + right;
+        }
         r.n = n;
         r.by = oy * d.stride - d.pt;
         r.bx = ox * d.stride - d.pl;
@@ -490,6 +504,8 @@ __global__ __launch_bounds__(256) void pack_weights_r_kernel(const float* __rest
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) rng[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (blockIdx.x == 0)  // a grid smaller than the record: the remaining partial maxima are zero
+        for (int i = gridDim.x + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) rng[i] = 0.f;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -825,7 +841,27 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     const int brow = tid / BTPR, bkq = (tid % BTPR) * ((MMA == MMA_BF16P || NSUB > 1) ? 16 / BTPR : BKPT);
     const float* bsrc = wp + (long long)(n0 + brow) * d.ldb;
 
-    const int K = g.ntaps * d.Cs;
+    // taps this tile needs (ring rows of a padded-grid data gradient, TAG 1 fold 2: a segment of the ring
+    // reads one kernel row or column; every other launch: all taps)
+    int tapmask = (1 << g.ntaps) - 1, ntap_act = g.ntaps;
+    if constexpr (TAG == 1 && H3) {
+        if (fold == 2) {
+            const int Hr = d.Ho - 2, sw = d.N * d.Wo, sh = d.N * Hr;
+            auto seg_mask = [&](long long m) {  // (ty, tx) bit ty * 3 + tx of the taps segment m's rows read
+                return m < sw ? 0x1C0 : (m < 2 * sw ? 0x007 : (m < 2 * sw + sh ? 0x124 : 0x049));
+            };
+            const long long mlast = (m0 + BM < M ? m0 + BM : M) - 1;
+            int msk = 0;
+            for (int sgi = 0; sgi < 4; ++sgi) {  // the segments between the tile's first and last row
+                const long long sb = sgi == 0 ? 0 : (sgi == 1 ? sw : (sgi == 2 ? 2 * sw : 2 * sw + sh));
+                const long long se = sgi == 0 ? sw : (sgi == 1 ? 2 * sw : (sgi == 2 ? 2 * sw + sh : 2 * sw + 2 * sh));
+                if (sb <= mlast && se > m0) msk |= seg_mask(sb);
+            }
+            tapmask = __builtin_amdgcn_readfirstlane(msk);
+            ntap_act = __builtin_popcount(tapmask);
+        }
+    }
+    const int K = ntap_act * d.Cs;
     const int nkt_all = (K + BKT - 1) / BKT;
     const int kper = (nkt_all + ksplit - 1) / ksplit;
     const int kt_beg = ks * kper;                                         // this split's k-tiles
@@ -919,18 +955,33 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
     };
     auto walk_init = [&](int p0) {  // p0: index of the first 16-k step (uniform)
         Walk w;
-        const int j = p0 % g.ntaps;
-        w.cs = __builtin_amdgcn_readfirstlane((p0 / g.ntaps) * 16);
+        int j = p0 % ntap_act;
+        if constexpr (TAG == 1 && H3) {  // the j-th tap of the mask
+            int t = 0;
+            for (int q = 0; q < g.ntaps; ++q)
+                if ((tapmask >> q) & 1) {
+                    if (j == 0) { t = q; break; }
+                    --j;
+                }
+            j = t;
+        }
+        w.cs = __builtin_amdgcn_readfirstlane((p0 / ntap_act) * 16);
         w.ty = __builtin_amdgcn_readfirstlane(j / wntx);
         w.tx = __builtin_amdgcn_readfirstlane(j - (j / wntx) * wntx);
         return w;
     };
-    auto walk_step = [&](Walk& w) {
+    auto walk_step1 = [&](Walk& w) {
         const bool wx = w.tx + 1 == wntx;
         const bool wy = wx && w.ty + 1 == wnty;
         w.tx = wx ? 0 : w.tx + 1;
         w.ty = wy ? 0 : (wx ? w.ty + 1 : w.ty);
         w.cs += wy ? 16 : 0;
+    };
+    auto walk_step = [&](Walk& w) {
+        walk_step1(w);
+        if constexpr (TAG == 1 && H3) {  // skip the taps outside the mask (uniform; a no-op for a full mask)
+            while (!((tapmask >> (w.ty * wntx + w.tx)) & 1)) walk_step1(w);
+        }
     };
     // (ady, adx): source offset of the tap; bt: its column block in the packed weights (tap_decode).
     // All three are affine in (ty, tx) with per-class constants (parity 1: ady = (ry + pt - ty0) / 2
@@ -1169,7 +1220,11 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
             for (int sub = 0; sub < NSUB; ++sub) {
                 long long col;
                 bool ok = true;
-                if (!d.parity && !KSB) {
+                if constexpr (TAG == 1 && H3 && DCS_UWALK) {  // the (masked) slice-major walk: 9 taps x 16 per slice
+                    ok = wb.cs < d.Cs;
+                    col = (long long)(wb.cs >> 4) * (9 * 16) + (wb.ty * 3 + wb.tx) * 16 + blo;
+                    walk_step(wb);
+                } else if (!d.parity && !KSB) {
                     col = (long long)kt * BKT + 16 * sub + bkq;
                 } else if constexpr (KSB && DCS_UWALK) {
                     ok = wb.cs < d.Cs;
@@ -2168,6 +2223,14 @@ using namespace dcs;
 
 extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                   int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream);
+namespace {
+// blocks of a per-pack range / pack launch: one element per thread, at most one block per range-record
+// slot (a small pack no longer dispatches 512 mostly idle blocks; ~8 elements per thread measured slower)
+unsigned pack_blocks(long long total) {
+    const long long b = cdiv(total, 256);
+    return (unsigned)(b < 1 ? 1 : (b > DCS_RANGE_PARTS ? DCS_RANGE_PARTS : b));
+}
+}  // namespace
 extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
                                 int Kpad, int ncols, int nmajor, float* out, void* stream) {
     return dcs_pack_weights_r(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out, nullptr, stream);
@@ -2184,7 +2247,7 @@ extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int
     if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
     long long total = (long long)Kpad * ncols;
     if (rng)
-        hipLaunchKernelGGL(pack_weights_r_kernel, dim3(DCS_RANGE_PARTS), dim3(256), 0, as_stream(stream), w, Cout, Cin,
+        hipLaunchKernelGGL(pack_weights_r_kernel, dim3(pack_blocks(total)), dim3(256), 0, as_stream(stream), w, Cout, Cin,
                            KH, KW, kind, ci_count, Kpad, ncols, nmajor, out, rng);
     else
         hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, as_stream(stream), w,
@@ -2229,10 +2292,11 @@ int conv_rows_impl(const dcs_conv_desc* dp, const float* src, const float* src2,
 int ring_ksplit(const dcs_conv_desc& d) {
     const long long M = (long long)d.N * (2 * d.Wo + 2 * (d.Ho - 2));
     const long long tiles = cdiv(M, 128) * cdiv(d.Co, d.Co > 64 ? 128 : 64);
-    const long long nkt = cdiv((long long)d.KH * d.KW * d.Cs, 32);
+    // a ring segment reads one kernel row or column (the masked walk of conv_rows_kernel, fold 2)
+    const long long nkt = cdiv((long long)(d.KH > d.KW ? d.KH : d.KW) * d.Cs, 32);
     long long k = cdiv(512, tiles);
     if (k > 8) k = 8;
-    while (k > 1 && nkt / k < 4) --k;
+    while (k > 1 && nkt / k < 8) --k;
     return k < 1 ? 1 : (int)k;
 }
 }  // namespace dcs

@@ -464,7 +464,10 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
 // the border read them directly; the 3-pixel border sums its reflection preimages.  Workgroups are
 // persistent per image (HB_PP of them), so the partial sums come in HB_PP chunks per image.
 constexpr int HB_TR = 4, HB_TC = 64;
-constexpr int HB_WR = HB_TR + 2 * HP_R + 1, HB_WC = HB_TC + 2 * HP_R + 1;  // 11 x 71: window + margin
+// g window rows y0 - 7 .. y0 + 12 and columns x0 - 7 .. x0 + 72 (zero outside the image): every read of
+// the primary preimage (taps padded to 8 x 8) and of the reflected ones stays inside it
+constexpr int HB_OFF = 7;
+constexpr int HB_WR = HB_TR + 16, HB_WC = HB_TC + 16;  // 20 x 80
 constexpr int HB_NT = 64 * HB_TR;
 constexpr int HB_PP = 64;  // workgroups (partial-sum chunks) per image
 
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                                                                const Sum2* __restrict__ coef,
                                                                Sum2* __restrict__ parts,
                                                                float* __restrict__ dy, float* __restrict__ rng) {
-    __shared__ float Gw[HB_WR][HB_WC];  // Gw[1 + r][1 + c] = g[y0 - 3 + r][x0 - 3 + c]; row / column 0: zero
+    __shared__ float Gw[HB_WR][HB_WC];  // Gw[r][c] = g[y0 - 7 + r][x0 - 7 + c], zero outside the image
     __shared__ float red[HB_NT / 64][2][HP_C];
 
     const int n = blockIdx.x / a.pp, wg = blockIdx.x - n * a.pp;
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
         for (int q = 0; q < HB_GU; ++q) {
             const int i = tid + q * HB_NT;
             const int r = i / HB_WC, c = i - r * HB_WC;
-            const int gy = tyi * HB_TR - HP_R - 1 + r, gx = txi * HB_TC - HP_R - 1 + c;
+            const int gy = tyi * HB_TR - HB_OFF + r, gx = txi * HB_TC - HB_OFF + c;
             gv[q] = gn[(long long)min(max(gy, 0), H - 1) * W + min(max(gx, 0), W - 1)];
         }
     };
@@ -568,9 +571,8 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
         for (int q = 0; q < HB_GU; ++q) {
             const int i = tid + q * HB_NT;
             const int r = i / HB_WC, c = i - r * HB_WC;
-            const int gy = y0 - HP_R - 1 + r, gx = x0 - HP_R - 1 + c;
-            if (i < HB_WR * HB_WC)
-                Gw[r][c] = (r > 0 && c > 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) ? gv[q] : 0.f;
+            const int gy = y0 - HB_OFF + r, gx = x0 - HB_OFF + c;
+            if (i < HB_WR * HB_WC) Gw[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? gv[q] : 0.f;
         }
         __syncthreads();
         if (chunk + a.pp < per) load_g(chunk + a.pp);  // in flight across this tile
@@ -581,13 +583,16 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
         for (int mb = 0; mb < 2; ++mb) {
             const int xl = mb * 32 + l32;  // the lane's A-row pixel (column within the tile)
             const int xx = x0 + xl;
-            // a lane's entries at step ks: Gw[1 + wid + 6 - (2 ks + kh)][1 + xl + 6 - i], i = 0..7
+            // a lane's entries at step ks: g rows r = a - ty over the padded-row preimages a of its pixel
+            // row (a = yy + 3, and a reflected one within 3 pixels of the border), columns likewise:
+            // Gw[7 + r - y0][7 + c - x0] (c = b - i); the second preimage, where absent, enters with
+            // weight 0 (adding +0 leaves the sum unchanged, so the order of the terms is fixed)
             const bool lane_inner = yy > HP_R && yy < H - 1 - HP_R && xx > HP_R && xx < W - 1 - HP_R;
-            int ay[3], ax[3], ny = 1, nx = 1;
-            if (!lane_inner) {
-                ny = hb_pre(yy, H, ay);
-                nx = hb_pre(xx, W, ax);
-            }
+            int ay[3], ax[3];
+            const int ny = hb_pre(yy, H, ay), nx = hb_pre(xx, W, ax);
+            const int ry0 = HB_OFF + ay[0] - y0, ry1 = HB_OFF + (ny > 1 ? ay[1] : ay[0]) - y0;
+            const int rx0 = HB_OFF + ax[0] - x0, rx1 = HB_OFF + (nx > 1 ? ax[1] : ax[0]) - x0;
+            const float my = ny > 1 ? 1.f : 0.f, mx = nx > 1 ? 1.f : 0.f;
             // y of the block's outputs: all 32 loads issued before the MFMAs (clamped addresses, masked after)
             float yv[2][16];
             const long long ybase = ((long long)n * H + yc) * W;
@@ -604,23 +609,17 @@ __global__ __launch_bounds__(HB_NT, 2) void head_bwd_in_kernel(HeadBwdArgs a, co
                 const int ty = 2 * ks + kh;
                 float v[8];
                 if (lane_inner) {
-                    const float* rp = &Gw[1 + wid + 2 * HP_R - ty][1 + xl + 2 * HP_R];
+                    const float* rp = &Gw[ry0 - ty][rx0];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = rp[-i];
                 } else {
+                    const float* p00 = &Gw[ry0 - ty][rx0];
+                    const float* p01 = &Gw[ry0 - ty][rx1];
+                    const float* p10 = &Gw[ry1 - ty][rx0];
+                    const float* p11 = &Gw[ry1 - ty][rx1];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        float s = 0.f;
-                        for (int iy = 0; iy < ny; ++iy) {
-                            const int r = ay[iy] - ty;  // g row
-                            if ((unsigned)r >= (unsigned)H) continue;
-                            for (int ix = 0; ix < nx; ++ix) {
-                                const int c = ax[ix] - i;
-                                if ((unsigned)c < (unsigned)W) s += Gw[1 + r - y0 + HP_R][1 + c - x0 + HP_R];
-                            }
-                        }
-                        v[i] = s;
-                    }
+                    for (int i = 0; i < 8; ++i)
+                        v[i] = fmaf(my * mx, p11[-i], fmaf(my, p10[-i], fmaf(mx, p01[-i], p00[-i])));
                 }
                 f16x8 ah, al;
 #pragma unroll

@@ -423,6 +423,8 @@ __global__ __launch_bounds__(256) void wrange_kernel(const float* __restrict__ w
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (blockIdx.x == 0)  // a grid smaller than the record: the remaining partial maxima are zero
+        for (int i = gridDim.x + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) parts[i] = 0.f;
 }
 
 __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ w, int Cout, int Cin, int flip,
@@ -824,10 +826,13 @@ extern "C" int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, 
         (flip ? Cout : Cin) % 16 != 0 || ncols < (flip ? Cin : Cout))
         return fail(DCS_E_INVALID, "pack_weights_h3: bad arguments (3x3, reduction channels % 16 == 0)");
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(wrange_kernel, dim3(DCS_RANGE_PARTS), dim3(256), 0, s, w, (long long)Cout * Cin * 9, scratch);
+    const long long nw = (long long)Cout * Cin * 9;
+    const long long rb = cdiv(nw, 2048) < DCS_RANGE_PARTS ? cdiv(nw, 2048) : DCS_RANGE_PARTS;  // ~8 weights per thread
+    hipLaunchKernelGGL(wrange_kernel, dim3((unsigned)(rb < 1 ? 1 : rb)), dim3(256), 0, s, w, nw, scratch);
     int e = check_launch("pack_weights_h3 range");
     if (e) return e;
-    hipLaunchKernelGGL(pack_h3_kernel, dim3(256), dim3(256), 0, s, w, Cout, Cin, flip, ncols, scratch,
+    const long long pb = cdiv((long long)ncols * 9 * (flip ? Cout : Cin), 2048);
+    hipLaunchKernelGGL(pack_h3_kernel, dim3((unsigned)(pb < 1 ? 1 : (pb > 256 ? 256 : pb))), dim3(256), 0, s, w, Cout, Cin, flip, ncols, scratch,
                        (int)DCS_RANGE_PARTS, reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo),
                        wexp);
     return check_launch("pack_weights_h3");

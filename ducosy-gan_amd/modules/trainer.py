@@ -235,7 +235,8 @@ class CycleGANSystem:
             dxB, _ = net.discriminator_backward(S_dB, d_dB, True, False)
             ops.scale_add_(d_ab[:N], dxB.reshape(d_ab[:N].shape))
             dxA, _ = net.discriminator_backward(S_dA, d_dA, True, False)
-            del S_dB, S_dA
+            # (S_dA / S_dB stay: the D steps below reuse these forwards of the fake samples, the
+            # Discriminators' weights being unchanged until their own steps)
             dx_rb, _ = net.generator_backward(S_rb, d_rb, True, 1, 0, pAB)
             torch.add(dxA.reshape(d_ba[:N].shape), dx_rb.reshape(d_ba[:N].shape), out=d_ba[:N])
             del S_rb, dxA, dx_rb
@@ -248,21 +249,29 @@ class CycleGANSystem:
         self.optimizer_G.step()
         out = {k: vals[i] for i, k in enumerate(_G_TERMS)}
 
-        # --- Discriminator steps (trainer.py:517-525), real and fake batched ---
-        for name, D, params, real, fake in (("loss_D_A", D_A, pDA, real_A, fake_A),
-                                            ("loss_D_B", D_B, pDB, real_B, fake_B)):
+        # --- Discriminator steps (trainer.py:517-525) ---
+        # D(fake.detach()) is the forward the G step already ran on the same samples with the same
+        # Discriminator weights (only G moved since): its outputs and saved activations are reused,
+        # and only D(real) is computed here.  The weight gradient is the real half's backward plus
+        # the fake half's (the second one added into .grad).
+        for name, D, params, real, o_f, S_f in (("loss_D_A", D_A, pDA, real_A, dA, S_dA),
+                                                ("loss_D_B", D_B, pDB, real_B, dB, S_dB)):
             opt = self.optimizer_D_A if D is D_A else self.optimizer_D_B
             opt.zero_grad()
             with torch.no_grad():
-                o, S = net.discriminator_forward(params, torch.cat([real, fake]), True)
-                d_o = torch.empty_like(o)
-                jobs = [dict(pred=o[:N], grad=d_o[:N], flags=GL_MSEC, c_mse=0.5, t_const=1.0),
-                        dict(pred=o[N:], grad=d_o[N:], flags=GL_MSEC, c_mse=0.5, t_const=0.0)]
+                o_r, S_r = net.discriminator_forward(params, real, True)
+                d_r, d_f = torch.empty_like(o_r), torch.empty_like(o_f)
+                jobs = [dict(pred=o_r, grad=d_r, flags=GL_MSEC, c_mse=0.5, t_const=1.0),
+                        dict(pred=o_f, grad=d_f, flags=GL_MSEC, c_mse=0.5, t_const=0.0)]
                 v = ops.gen_loss_fused(jobs, ([0.0], [[0, 0, 0, 0, .5, 0, 0, 0, 0, .5]], [[0.0] * 4]))
-                net.discriminator_backward(S, d_o, False, True, dict(enumerate(params)))
+                pd = dict(enumerate(params))
+                net.discriminator_backward(S_r, d_r, False, True, pd)
+                net.discriminator_backward(S_f, d_f, False, True, pd)
+                del S_r
             parallel.allreduce_mean_(opt.flat_g)
             opt.step()
             out[name] = v[0]
+        del S_dA, S_dB
         return out
 
     def _train_step_autograd(self, real_A, real_B, masks=None):
