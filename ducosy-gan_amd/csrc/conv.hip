@@ -2236,15 +2236,24 @@ extern "C" int dcs_pack_weights(const float* w, int Cout, int Cin, int KH, int K
     return dcs_pack_weights_r(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, out, nullptr, stream);
 }
 
-extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
-                                  int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream) {
+namespace {
+const char* pack_args_error(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count, int Kpad,
+                            int ncols, const float* out) {
     if (!w || !out || Cout <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || Kpad <= 0 || ncols <= 0 || ci_count <= 0 ||
         (kind != 5 && ci_count > Cin) || (kind == 5 && ci_count < Cin) || kind < 0 ||
         (kind & 7) > 5 || (kind & ~(7 | DCS_PACK_KSLICE)) ||
         ((kind & DCS_PACK_KSLICE) && (((kind & 7) != 0 && (kind & 7) != 1) ||
                                       ((kind & 7) == 0 ? Cin : Cout) % 16 != 0)))
-        return fail(DCS_E_INVALID, "pack_weights: bad arguments");
-    if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return fail(DCS_E_INVALID, "pack_weights: sub-pixel kinds need 3x3");
+        return "pack_weights: bad arguments";
+    if ((kind == 3 || kind == 4) && (KH != 3 || KW != 3)) return "pack_weights: sub-pixel kinds need 3x3";
+    return nullptr;
+}
+}  // namespace
+
+extern "C" int dcs_pack_weights_r(const float* w, int Cout, int Cin, int KH, int KW, int kind, int ci_count,
+                                  int Kpad, int ncols, int nmajor, float* out, float* rng, void* stream) {
+    if (const char* err = pack_args_error(w, Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, out))
+        return fail(DCS_E_INVALID, err);
     long long total = (long long)Kpad * ncols;
     if (rng)
         hipLaunchKernelGGL(pack_weights_r_kernel, dim3(pack_blocks(total)), dim3(256), 0, as_stream(stream), w, Cout, Cin,
@@ -2281,6 +2290,147 @@ extern "C" int dcs_pack_split_h3(const float* wpack, int rows, int ldb, const fl
     hipLaunchKernelGGL(pack_split_h3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), wpack, total, ldb,
                        rng, rng_n, reinterpret_cast<_Float16*>(out));
     return check_launch("pack_split_h3");
+}
+
+namespace dcs {
+namespace {
+// batched weight packs (dcs_pack_batch): block -> job by a binary search over the jobs' first blocks
+__device__ __forceinline__ int pack_job_of(const dcs_pack_job* __restrict__ jobs, int njobs, int b, bool second) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const int start = second ? jobs[mid].p0 : jobs[mid].b0;
+        if (start <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// launch 1: each pack and its range record (kind >= 0), or the range of the raw weights of a window pack
+__global__ __launch_bounds__(256) void pack_batch1_kernel(const dcs_pack_job* __restrict__ jobs, int njobs) {
+    const int j = pack_job_of(jobs, njobs, blockIdx.x, false);
+    const dcs_pack_job& jb = jobs[j];
+    const int lb = blockIdx.x - jb.b0, nb = jb.b1;
+    float m = 0.f;
+    float* rng;
+    if (jb.h3) {
+        const long long n = (long long)jb.Cout * jb.Cin * 9;
+        for (long long i = (long long)lb * 256 + threadIdx.x; i < n; i += (long long)nb * 256) m = fmaxf(m, fabsf(jb.w[i]));
+        rng = jb.h3_scratch;
+    } else {
+        const long long total = (long long)jb.Kpad * jb.ncols;
+        for (long long idx = (long long)lb * 256 + threadIdx.x; idx < total; idx += (long long)nb * 256) {
+            const float v = pack_value(jb.w, jb.Cout, jb.Cin, jb.KH, jb.KW, jb.kind, jb.ci_count, jb.Kpad, jb.ncols,
+                                       jb.nmajor, idx);
+            jb.out[idx] = v;
+            m = fmaxf(m, fabsf(v));
+        }
+        rng = jb.rng;
+    }
+    if (!rng) return;  // block-uniform
+    __shared__ float red[4];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) rng[lb] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (lb == 0)
+        for (int i = nb + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) rng[i] = 0.f;
+}
+
+// launch 2: the pre-split planes of a pack (dcs_pack_split_h3), or the hi / lo planes of a window pack
+// (dcs_pack_weights_h3), each with the exponent of the range record launch 1 wrote
+__global__ __launch_bounds__(256) void pack_batch2_kernel(const dcs_pack_job* __restrict__ jobs, int njobs) {
+    const int j = pack_job_of(jobs, njobs, blockIdx.x, true);
+    const dcs_pack_job& jb = jobs[j];
+    const int lb = blockIdx.x - jb.p0, nb = jb.p1;
+    if (jb.h3) {
+        const int e = f16x3_exp(jb.h3_scratch, DCS_RANGE_PARTS);
+        const float sc = __builtin_ldexpf(1.f, e);
+        if (lb == 0 && threadIdx.x == 0) jb.h3_wexp[0] = e;
+        const int C = jb.h3_flip ? jb.Cout : jb.Cin;
+        const int K = 9 * C;
+        const long long total = (long long)jb.h3_ncols * K;
+        _Float16* oh = reinterpret_cast<_Float16*>(jb.h3_hi);
+        _Float16* ol = reinterpret_cast<_Float16*>(jb.h3_lo);
+        for (long long idx = (long long)lb * 256 + threadIdx.x; idx < total; idx += (long long)nb * 256) {
+            const int col = (int)(idx / K), k = (int)(idx - (long long)col * K);
+            const int slice = k / 144, rem = k - slice * 144;
+            const int tap = rem >> 4, c = slice * 16 + (rem & 15);
+            const int ty = tap / 3, tx = tap - 3 * (tap / 3);
+            float v = 0.f;
+            if (!jb.h3_flip) {
+                if (col < jb.Cout) v = jb.w[(((long long)col * jb.Cin + c) * 3 + ty) * 3 + tx];
+            } else {
+                if (col < jb.Cin) v = jb.w[(((long long)c * jb.Cin + col) * 3 + (2 - ty)) * 3 + (2 - tx)];
+            }
+            const float f = v * sc;
+            const _Float16 h = (_Float16)f;
+            oh[idx] = h;
+            ol[idx] = (_Float16)(f - (float)h);
+        }
+    } else {
+        const float sc = __builtin_ldexpf(1.f, f16x3_exp(jb.rng, DCS_RANGE_PARTS));
+        const long long total = (long long)jb.ncols * jb.Kpad;
+        _Float16* out = reinterpret_cast<_Float16*>(jb.planes);
+        for (long long i = (long long)lb * 256 + threadIdx.x; i < total; i += (long long)nb * 256) {
+            const long long r = i / jb.Kpad, k = i - r * jb.Kpad;
+            const float v = jb.out[i] * sc;
+            const _Float16 h = (_Float16)v;
+            out[2 * r * jb.Kpad + k] = h;
+            out[(2 * r + 1) * jb.Kpad + k] = (_Float16)(v - (float)h);
+        }
+    }
+}
+}  // namespace
+}  // namespace dcs
+
+// block counts: about one element per thread, at most one block per range-record slot in launch 1 (a
+// record's partial maxima then depend on the grid, their maximum - the only thing a consumer reads -
+// does not, so every pack, exponent and plane equals the per-pack calls')
+extern "C" int dcs_pack_plan(dcs_pack_job* jobs, int njobs, int* g1, int* g2) {
+    if (!jobs || njobs <= 0 || !g1 || !g2) return fail(DCS_E_INVALID, "pack_plan: bad arguments");
+    long long b = 0, p = 0;
+    for (int i = 0; i < njobs; ++i) {
+        dcs_pack_job& jb = jobs[i];
+        if (!jb.w) return fail(DCS_E_INVALID, "pack_plan: job without weights");
+        long long n1, n2 = 0, cap2 = 1;
+        if (jb.h3) {
+            if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || jb.Cout <= 0 || jb.Cin <= 0 ||
+                (jb.h3_flip ? jb.Cout : jb.Cin) % 16 != 0 || jb.h3_ncols < (jb.h3_flip ? jb.Cin : jb.Cout))
+                return fail(DCS_E_INVALID, "pack_plan: window job (3x3, reduction channels % 16 == 0)");
+            n1 = cdiv((long long)jb.Cout * jb.Cin * 9, 2048);  // dcs_pack_weights_h3's range launch
+            n2 = cdiv((long long)jb.h3_ncols * 9 * (jb.h3_flip ? jb.Cout : jb.Cin), 2048);
+            cap2 = 256;
+        } else {
+            if (const char* err = pack_args_error(jb.w, jb.Cout, jb.Cin, jb.KH, jb.KW, jb.kind, jb.ci_count, jb.Kpad,
+                                                  jb.ncols, jb.out))
+                return fail(DCS_E_INVALID, err);
+            n1 = cdiv((long long)jb.Kpad * jb.ncols, 256);
+            if (jb.planes) {
+                if (!jb.rng || !jb.nmajor) return fail(DCS_E_INVALID, "pack_plan: planes need an N-major pack with a range record");
+                n2 = cdiv((long long)jb.ncols * jb.Kpad, 256);
+                cap2 = 1024;
+            }
+        }
+        n1 = n1 < 1 ? 1 : (n1 > DCS_RANGE_PARTS ? DCS_RANGE_PARTS : n1);
+        n2 = n2 > cap2 ? cap2 : n2;
+        jb.b0 = (int)b; jb.b1 = (int)n1;
+        jb.p0 = (int)p; jb.p1 = (int)n2;
+        b += n1;
+        p += n2;
+    }
+    *g1 = (int)b;
+    *g2 = (int)p;
+    return 0;
+}
+
+extern "C" int dcs_pack_batch(const dcs_pack_job* jobs_dev, int njobs, int g1, int g2, void* stream) {
+    if (!jobs_dev || njobs <= 0 || g1 <= 0 || g2 < 0) return fail(DCS_E_INVALID, "pack_batch: bad arguments");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(pack_batch1_kernel, dim3((unsigned)g1), dim3(256), 0, s, jobs_dev, njobs);
+    int e = check_launch("pack_batch1");
+    if (e || g2 == 0) return e;
+    hipLaunchKernelGGL(pack_batch2_kernel, dim3((unsigned)g2), dim3(256), 0, s, jobs_dev, njobs);
+    return check_launch("pack_batch2");
 }
 
 namespace dcs {

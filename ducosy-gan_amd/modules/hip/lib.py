@@ -37,6 +37,19 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):
+    """Mirror of dcs_pack_job (include/ducosy_hip.h): one weight pack of dcs_pack_batch."""
+    _fields_ = [
+        ("w", c_void_p),
+        ("Cout", c_int32), ("Cin", c_int32), ("KH", c_int32), ("KW", c_int32), ("kind", c_int32),
+        ("ci_count", c_int32), ("Kpad", c_int32), ("ncols", c_int32), ("nmajor", c_int32), ("h3", c_int32),
+        ("h3_flip", c_int32), ("h3_ncols", c_int32),
+        ("out", c_void_p), ("rng", c_void_p), ("planes", c_void_p), ("h3_hi", c_void_p), ("h3_lo", c_void_p),
+        ("h3_wexp", c_void_p), ("h3_scratch", c_void_p),
+        ("b0", c_int32), ("b1", c_int32), ("p0", c_int32), ("p1", c_int32),
+    ]
+
+
 class GLJob(ctypes.Structure):
     """Mirror of dcs_gl_job (include/ducosy_hip.h): one plane set of the fused G-step loss kernel."""
     _fields_ = [
@@ -64,6 +77,8 @@ SIGNATURES = {
     "dcs_conv3_win_ok": (c_int, [DP, c_int]),
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_pack_split_h3": (c_int, [P, c_int, c_int, P, c_int, P, P]),
+    "dcs_pack_plan": (c_int, [P, c_int, POINTER(c_int), POINTER(c_int)]),
+    "dcs_pack_batch": (c_int, [P, c_int, c_int, c_int, P]),
     "dcs_stem_fwd_ok": (c_int, [DP]),
     "dcs_stem_fwd_parts_size": (c_size_t, [DP]),
     "dcs_stem_fwd": (c_int, [DP, P, P, P, P, c_size_t, POINTER(c_int), P]),

@@ -31,8 +31,9 @@ _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
 # the Generator head's forward by tap projection on the MFMA pipe in the fp16 modes
 # (csrc/conv_head.hip); "0" = the exact-f32 VALU kernel (A/B)
 _HEAD_PROJ = os.environ.get("DUCOSY_HEAD_PROJ", "1") == "1"
-_BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"
-_STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
+_BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
+_STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)
+_PREPACK = os.environ.get("DUCOSY_PREPACK", "1") == "1"  # the step's weight packs in two batched launches
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -301,17 +302,24 @@ BN_MAX = 128
 # Packed-weight cache: a pack is reused while its weight tensor is unchanged -- same autograd version
 # and storage (in-place torch ops, load_state_dict, broadcasts bump the version; a .data reassignment
 # changes the storage) and same weights epoch (the fused Adam
-# kernel writes parameters behind the version counter and bumps the epoch, modules/optim.py).  Within a
-# step the second batched G_A2B call and the G-step / D-step Discriminator calls reuse the packs.
+# kernel writes parameters behind the version counter and bumps the epoch of the parameters it
+# stepped, modules/optim.py; a broadcast through a flat buffer bumps the global one).  Within a step
+# the second batched G_A2B call and the G-step / D-step Discriminator calls reuse the packs, and the
+# Discriminator packs outlive the Generator's optimizer step.
 _EPOCH = [0]
 
 
-def bump_weights_epoch() -> None:
-    _EPOCH[0] += 1
+def bump_weights_epoch(params=None) -> None:
+    """Invalidate the packs of ``params`` (every pack when None)."""
+    if params is None:
+        _EPOCH[0] += 1
+        return
+    for p in params:
+        p._dcs_epoch = getattr(p, "_dcs_epoch", 0) + 1
 
 
 def _cached_pack(w: torch.Tensor, key, make):
-    stamp = (w.data_ptr(), w._version, _EPOCH[0], _MMA, _WIN, _KSLICE)
+    stamp = (w.data_ptr(), w._version, _EPOCH[0], getattr(w, "_dcs_epoch", 0), _MMA, _WIN, _KSLICE)
     c = getattr(w, "_dcs_packs", None)
     if c is None or c[0] != stamp:
         c = (stamp, {})
@@ -321,6 +329,75 @@ def _cached_pack(w: torch.Tensor, key, make):
         pk = make()
         c[1][key] = pk
     return pk
+
+
+class _PackBatch:
+    """The weight packs of one prepack call, launched as two batched kernels (dcs_pack_batch)."""
+    _pinned = []  # staging buffers of the last few batches (their async copies may still be in flight)
+
+    def __init__(self):
+        self.jobs = []
+        self.keep = []
+
+    def add(self, w, **kw):
+        j = lib.PackJob()
+        j.w = w.data_ptr()
+        for k, v in kw.items():
+            if torch.is_tensor(v):
+                self.keep.append(v)  # alive until the launches are queued (the h3 scratch has no other owner)
+            setattr(j, k, v.data_ptr() if torch.is_tensor(v) else (0 if v is None else v))
+        self.jobs.append(j)
+        self.keep.append(w)
+
+    def flush(self, device):
+        if not self.jobs:
+            return
+        n = len(self.jobs)
+        arr = (lib.PackJob * n)(*self.jobs)
+        g1, g2 = ctypes.c_int(0), ctypes.c_int(0)
+        lib.call("dcs_pack_plan", ctypes.addressof(arr), n, ctypes.byref(g1), ctypes.byref(g2))
+        nbytes = ctypes.sizeof(arr)
+        host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        ctypes.memmove(host.data_ptr(), ctypes.addressof(arr), nbytes)
+        dev = host.to(device, non_blocking=True)
+        _PackBatch._pinned = (_PackBatch._pinned + [host])[-8:]
+        lib.call("dcs_pack_batch", _p(dev), n, g1.value, g2.value, _stream())
+
+
+_BATCH: Optional[_PackBatch] = None
+
+
+def _record_pack(w: torch.Tensor, method: str, geom, arg) -> None:
+    plan = getattr(w, "_dcs_plan", None)
+    if plan is None:
+        plan = {}
+        w._dcs_plan = plan
+    plan.setdefault((method, geom._key(), arg), geom)
+
+
+def prepack(params) -> None:
+    """Every pack a training step will ask for (the pack_fwd / pack_dgrad calls recorded on each
+    weight by earlier steps), for the weights' current values, in two batched launches instead of
+    one or two small launches per pack at first use.  The packs land in the same cache, so the
+    step's own calls find them; their values equal the per-pack calls'."""
+    global _BATCH
+    if _BATCH is not None or not _PREPACK:
+        return
+    b = _PackBatch()
+    dev = None
+    _BATCH = b
+    try:
+        for w in params:
+            plan = getattr(w, "_dcs_plan", None)
+            if not plan:
+                continue
+            dev = w.device
+            for (method, _, arg), geom in list(plan.items()):
+                getattr(geom, method)(w, arg)
+    finally:
+        _BATCH = None
+    if dev is not None:
+        b.flush(dev)
 
 
 def _wrng(wpack: torch.Tensor) -> Optional[torch.Tensor]:
@@ -383,9 +460,14 @@ class ConvGeom:
         hi = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
         lo = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
         wexp = torch.empty(1, device=w.device, dtype=torch.int32)
-        scratch = workspace(lib.query("dcs_pack_weights_h3_scratch_size"), w.device)
-        lib.call("dcs_pack_weights_h3", _p(w), self.cout, self.cin, flip, ncols, _p(hi), _p(lo), _p(scratch),
-                 _p(wexp), _stream())
+        if _BATCH is not None:  # prepack: one batched launch pair for every pack of the step
+            scratch = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
+            _BATCH.add(w, h3=1, Cout=self.cout, Cin=self.cin, h3_flip=flip, h3_ncols=ncols, h3_hi=hi, h3_lo=lo,
+                       h3_wexp=wexp, h3_scratch=scratch)
+        else:
+            scratch = workspace(lib.query("dcs_pack_weights_h3_scratch_size"), w.device)
+            lib.call("dcs_pack_weights_h3", _p(w), self.cout, self.cin, flip, ncols, _p(hi), _p(lo), _p(scratch),
+                     _p(wexp), _stream())
         wpack._dcs_h3 = (hi, lo, wexp)
         return wpack
 
@@ -393,11 +475,15 @@ class ConvGeom:
         return (self.cin, self.cout, self.k, self.stride, self.pads, self.pad_mode, self.up)
 
     def pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
-        """B operand of the forward GEMM (cached per weight version, _cached_pack)."""
+        """B operand of the forward GEMM (cached per weight version, _cached_pack; recorded on the
+        weight for prepack)."""
+        _record_pack(w, "pack_fwd", self, cin_pad)
         return _cached_pack(w, ("fwd", self._key(), cin_pad), lambda: self._pack_fwd(w, cin_pad))
 
     def pack_dgrad(self, w: torch.Tensor, ci_count: Optional[int] = None) -> torch.Tensor:
-        """B operand of the data-gradient GEMM (cached per weight version, _cached_pack)."""
+        """B operand of the data-gradient GEMM (cached per weight version, _cached_pack; recorded on
+        the weight for prepack)."""
+        _record_pack(w, "pack_dgrad", self, ci_count)
         return _cached_pack(w, ("dgrad", self._key(), ci_count), lambda: self._pack_dgrad(w, ci_count))
 
     def _pack_fwd(self, w: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
@@ -450,15 +536,25 @@ class ConvGeom:
         else:
             Kpad, cols, nmajor = _round_up(K, 32), _round_up(ncols, _bn_for(ncols)), 1
             out = torch.empty(cols, Kpad, device=w.device, dtype=torch.float32)
+        job = dict(Cout=self.cout, Cin=self.cin, KH=self.k, KW=self.k, kind=kind, ci_count=ci_count, Kpad=Kpad,
+                   ncols=cols, nmajor=nmajor, out=out)
         if nmajor and _h3():  # f16x3 rows pass: the pack also writes the range record
             rng = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
-            lib.call("dcs_pack_weights_r", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
-                     cols, nmajor, _p(out), _p(rng), _stream())
             out._dcs_rng = (out._version, None, ACT_NONE, rng)
+            planes = None
             if _BPRE and not self.win:  # pre-split fp16 planes for the rows pass (dcs_conv_desc.b_h3)
                 planes = torch.empty(cols * 2 * Kpad, device=w.device, dtype=torch.float16)
-                lib.call("dcs_pack_split_h3", _p(out), cols, Kpad, _p(rng), lib.RANGE_PARTS, _p(planes), _stream())
                 out._dcs_bh3 = (out._version, planes)
+            if _BATCH is not None:
+                _BATCH.add(w, rng=rng, planes=planes, **job)
+            else:
+                lib.call("dcs_pack_weights_r", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
+                         cols, nmajor, _p(out), _p(rng), _stream())
+                if planes is not None:
+                    lib.call("dcs_pack_split_h3", _p(out), cols, Kpad, _p(rng), lib.RANGE_PARTS, _p(planes),
+                             _stream())
+        elif _BATCH is not None:
+            _BATCH.add(w, **job)
         else:
             lib.call("dcs_pack_weights", _p(w), self.cout, self.cin, self.k, self.k, kind, ci_count, Kpad,
                      cols, nmajor, _p(out), _stream())

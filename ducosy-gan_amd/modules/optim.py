@@ -64,7 +64,7 @@ class FusedAdam(torch.optim.Optimizer):
         self._t += 1
         b1, b2 = g["betas"]
         ops.adam_step(self.flat_p, self.flat_g, self.flat_m, self.flat_v, g["lr"], b1, b2, g["eps"], self._t)
-        ops.bump_weights_epoch()  # the kernel wrote the parameters behind autograd's version counter
+        ops.bump_weights_epoch(g["params"])  # the kernel wrote them behind autograd's version counter
         return loss
 
     def state_dict(self):

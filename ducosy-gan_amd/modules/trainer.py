@@ -212,6 +212,7 @@ class CycleGANSystem:
 
         # --- Generator step (trainer.py:463-514) ---
         ops.range_arena_reset(self.device)  # this step's range records: one zeroing launch
+        ops.prepack([p for m in self.models for p in m.parameters()])  # every weight pack of the step, batched
         self.optimizer_G.zero_grad()
         with torch.no_grad():
             ab, S_ab = net.generator_forward(pAB, torch.cat([real_A, real_B]), mk(2), nb, cb, True)

@@ -400,6 +400,27 @@ int dcs_stem_wgrad(const dcs_conv_desc* d, const float* dy, const float* src, fl
  * out[r][0][k] = hi, out[r][1][k] = lo of wpack[r][k] * 2^e (fp16), e the operand exponent of the pack's range
  * record rng (dcs_pack_weights_r).  out: rows * 2 * ldb halves. */
 int dcs_pack_split_h3(const float* wpack, int rows, int ldb, const float* rng, int rng_n, void* out, void* stream);
+/* Every weight pack of a training step in two launches (instead of one or two small launches per pack).
+ * A job is either a dcs_pack_weights_r pack (kind >= 0: w, Cout .. nmajor, out, rng as there; planes:
+ * optional dcs_pack_split_h3 output of that pack, rows = ncols) or, with h3 = 1, a dcs_pack_weights_h3
+ * pack (w, Cout, Cin, h3_flip, h3_ncols, h3_hi, h3_lo, h3_wexp, h3_scratch as there).  Results are
+ * bit-identical to the per-pack calls.  jobs_dev: device copy of jobs[0 .. njobs) (the caller stages it;
+ * jobs only supplies the host-side block counts); the b0 / b1 / p0 / p1 fields are filled here. */
+typedef struct dcs_pack_job {
+    const float* w;
+    int32_t Cout, Cin, KH, KW, kind, ci_count, Kpad, ncols, nmajor, h3, h3_flip, h3_ncols;
+    float* out;
+    float* rng;
+    void* planes;
+    void* h3_hi;
+    void* h3_lo;
+    int32_t* h3_wexp;
+    float* h3_scratch;
+    int32_t b0, b1, p0, p1;  /* first block and block count of the job in the two launches (set by dcs_pack_plan) */
+} dcs_pack_job;
+/* Fills each job's block ranges and returns the grid sizes of the two launches (*g1, *g2). */
+int dcs_pack_plan(dcs_pack_job* jobs, int njobs, int* g1, int* g2);
+int dcs_pack_batch(const dcs_pack_job* jobs_dev, int njobs, int g1, int g2, void* stream);
 size_t dcs_conv_wgrad_narrow_workspace_size(const dcs_conv_desc* d);
 int dcs_conv_wgrad_narrow(const dcs_conv_desc* d, const float* dy, const float* x, const float* x2,
                           const float* pro_scale, const float* pro_shift, float* dw, void* ws,
