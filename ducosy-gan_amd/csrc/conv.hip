@@ -2312,7 +2312,15 @@ __global__ __launch_bounds__(256) void pack_batch1_kernel(const dcs_pack_job* __
     const int lb = blockIdx.x - jb.b0, nb = jb.b1;
     float m = 0.f;
     float* rng;
-    if (jb.h3) {
+    if (jb.h3 == 2) {  // sub-pixel phase weights: the range of the combined values
+        const long long n = 16LL * jb.Cout * jb.Cin;
+        const int K = 4 * jb.Cin;
+        for (long long i = (long long)lb * 256 + threadIdx.x; i < n; i += (long long)nb * 256) {
+            const int v = (int)(i / K);
+            m = fmaxf(m, fabsf(subpix_value(jb.w, jb.Cout, jb.Cin, v, (int)(i - (long long)v * K))));
+        }
+        rng = jb.h3_scratch;
+    } else if (jb.h3) {
         const long long n = (long long)jb.Cout * jb.Cin * 9;
         for (long long i = (long long)lb * 256 + threadIdx.x; i < n; i += (long long)nb * 256) m = fmaxf(m, fabsf(jb.w[i]));
         rng = jb.h3_scratch;
@@ -2342,7 +2350,22 @@ __global__ __launch_bounds__(256) void pack_batch2_kernel(const dcs_pack_job* __
     const int j = pack_job_of(jobs, njobs, blockIdx.x, true);
     const dcs_pack_job& jb = jobs[j];
     const int lb = blockIdx.x - jb.p0, nb = jb.p1;
-    if (jb.h3) {
+    if (jb.h3 == 2) {
+        const int e = f16x3_exp(jb.h3_scratch, DCS_RANGE_PARTS);
+        const float sc = __builtin_ldexpf(1.f, e);
+        if (lb == 0 && threadIdx.x == 0) jb.h3_wexp[0] = e;
+        const long long total = 16LL * jb.Cout * jb.Cin;
+        const int K = 4 * jb.Cin;
+        _Float16* oh = reinterpret_cast<_Float16*>(jb.h3_hi);
+        _Float16* ol = reinterpret_cast<_Float16*>(jb.h3_lo);
+        for (long long i = (long long)lb * 256 + threadIdx.x; i < total; i += (long long)nb * 256) {
+            const int v = (int)(i / K);
+            const float f = subpix_value(jb.w, jb.Cout, jb.Cin, v, (int)(i - (long long)v * K)) * sc;
+            const _Float16 h = (_Float16)f;
+            oh[i] = h;
+            ol[i] = (_Float16)(f - (float)h);
+        }
+    } else if (jb.h3) {
         const int e = f16x3_exp(jb.h3_scratch, DCS_RANGE_PARTS);
         const float sc = __builtin_ldexpf(1.f, e);
         if (lb == 0 && threadIdx.x == 0) jb.h3_wexp[0] = e;
@@ -2393,7 +2416,13 @@ extern "C" int dcs_pack_plan(dcs_pack_job* jobs, int njobs, int* g1, int* g2) {
         dcs_pack_job& jb = jobs[i];
         if (!jb.w) return fail(DCS_E_INVALID, "pack_plan: job without weights");
         long long n1, n2 = 0, cap2 = 1;
-        if (jb.h3) {
+        if (jb.h3 == 2) {
+            if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || jb.Cout <= 0 || jb.Cin <= 0 ||
+                jb.Cout % 64 || jb.Cin % 16 || 16LL * jb.Cout * jb.Cin >= (1LL << 30))
+                return fail(DCS_E_INVALID, "pack_plan: sub-pixel job (Cout % 64 == 0, Cin % 16 == 0)");
+            n1 = n2 = cdiv(16LL * jb.Cout * jb.Cin, 2048);  // dcs_pack_subpix_h3's launches
+            cap2 = 256;
+        } else if (jb.h3) {
             if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || jb.Cout <= 0 || jb.Cin <= 0 ||
                 (jb.h3_flip ? jb.Cout : jb.Cin) % 16 != 0 || jb.h3_ncols < (jb.h3_flip ? jb.Cin : jb.Cout))
                 return fail(DCS_E_INVALID, "pack_plan: window job (3x3, reduction channels % 16 == 0)");

@@ -1,4 +1,4 @@
-// Device helpers shared by the convolution kernels (conv.hip, conv_win.hip): MFMA operand vector
+// Device helpers shared by the convolution kernels (conv.hip, conv_win.hip, conv_subpix.hip): MFMA operand vector
 // types, the f16x3 operand split and scale exponent, the XCD-aware workgroup order.
 #pragma once
 #include "common.hpp"
@@ -46,6 +46,25 @@ __device__ __forceinline__ int xcd_remap(int L, int T) {
     const int xcd = L & 7, q = T >> 3, r = T & 7;
     const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
     return base + (L >> 3);
+}
+
+// B of the sub-pixel window kernel (conv_subpix.hip) for nearest-x2 upsample + 3x3 zero-pad conv weights
+// w[Cout][Cin][3][3]: virtual row v = (column tile (px, 64-channel block), row phase py, channel) and
+// k = (16-channel slice, source row offset u, column offset t, channel); the value is the sum of the
+// 3x3 taps that land on source offset (u, t) for output phase (py, px): taps 0 | 1,2 for phase 0,
+// 0,1 | 2 for phase 1 (the upsample folded into the weights, four taps per phase instead of nine)
+__device__ __forceinline__ float subpix_value(const float* __restrict__ w, int Cout, int Cin, int v, int k) {
+    const int cblk = Cout >> 6;
+    const int ntile = v >> 7, py = (v >> 6) & 1;
+    const int px = ntile / cblk, co = (ntile - px * cblk) * 64 + (v & 63);
+    const int rem = k & 63, u = rem >> 5, t = (rem >> 4) & 1, c = (k >> 6) * 16 + (rem & 15);
+    const int ya = py ? (u ? 2 : 0) : (u ? 1 : 0), yb = py ? (u ? 2 : 1) : (u ? 2 : 0);
+    const int xa = px ? (t ? 2 : 0) : (t ? 1 : 0), xb = px ? (t ? 2 : 1) : (t ? 2 : 0);
+    const float* wp = w + ((long long)co * Cin + c) * 9;
+    float s = 0.f;
+    for (int ty = ya; ty <= yb; ++ty)
+        for (int tx = xa; tx <= xb; ++tx) s += wp[ty * 3 + tx];
+    return s;
 }
 
 }  // namespace dcs

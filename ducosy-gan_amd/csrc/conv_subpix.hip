@@ -1,0 +1,413 @@
+// Nearest-x2 upsample + 3x3 zero-pad convolution (the Generator's up-convolutions,
+// modules/model.py:112-120 Upsample + Conv2d) on f16x3 operands, the source window of a tile staged once
+// per 16-channel slice.
+//
+// Output pixel (2i + py, 2j + px) reads source rows {i - 1, i} (py = 0) or {i, i + 1} (py = 1) and
+// likewise for columns: each of the four phases is a 2x2 convolution of the LOW-resolution source with
+// weights that sum the 3x3 taps landing on the same source pixel (subpix_value, conv_common.hpp).
+// conv.hip's rows pass runs the phases as four classes and gathers A per k-tile (every source value
+// fetched and split four times per phase); here a workgroup owns 256 source pixels (R = 256 / TW rows
+// of a TW-wide strip) x 128 virtual output columns, and per 16-channel slice stages the
+// (R + 2) x (TW + 2) source window once (zero outside the image) for 2 phases x 4 taps.
+//
+// Virtual columns: a column tile is (px, 64-channel block); its halves are the row phases py = 0, 1.
+// Waves w and w + 4 (one SIMD) own the same 64 pixels in the two row phases; each wave runs 4 taps
+// (u, t) x 2 x 2 blocks x 3 products per slice, so no wave idles on a tap another phase needs.
+// B arrives pre-split (dcs_pack_subpix_h3: hi / lo fp16 planes [4 Co][4 C], k = slice * 64 + u * 32 +
+// t * 16 + c).  One fp32 chain per slice (64 k), added to the running sum (two-level, as conv.hip).
+// LDS: window [2][2 planes][520 px][16] + B [2][2 planes][4 taps][128 rows x 16 + 48] halves (131 KB).
+#include "common.hpp"
+#include "conv_common.hpp"
+
+namespace dcs {
+namespace {
+
+constexpr int SP_NT = 512, SP_BN = 128;
+constexpr int SP_PIX = 520;                 // window pixels: (256 / TW + 2) * (TW + 2) <= 520 for 16 <= TW <= 128
+constexpr int SP_SLOT = 128 * 16 + 48;      // halves per B tap slot (the four slots of a row on distinct banks)
+constexpr int SP_UNITS = (2 * SP_PIX + SP_NT - 1) / SP_NT;
+
+struct SubArgs {
+    int N, Hs, Ws, C, Co;  // source NHWC [N][Hs][Ws][C]; output NHWC [N][2 Hs][2 Ws][Co]
+    int R, TW, tiles_x, tiles;  // tile = R rows x TW columns of the source; tiles per row band / image
+    int gy, cblk;          // column tiles (4 Co / 128), 64-channel blocks (Co / 64)
+    int rng_n;
+};
+
+// window: pixel pairs swap on odd groups of 8 pixels, 16-byte halves on odd groups of 16 (conflict-free
+// reads of every other pixel: the MFMA row blocks interleave, as conv_win.hip)
+__device__ __forceinline__ int sp_woff(int buf, int pl, int wpix, int h) {
+    return ((buf * 2 + pl) * SP_PIX + (wpix ^ ((wpix >> 3) & 1))) * 16 + 8 * (h ^ ((wpix >> 4) & 1));
+}
+__device__ __forceinline__ int sp_boff(int buf, int pl, int tap, int row, int h) {
+    return ((buf * 2 + pl) * 4 + tap) * SP_SLOT + row * 16 + 8 * (h ^ ((row >> 3) & 1));
+}
+
+template <int NP>  // 3: f16x3 (lo*hi + hi*lo + hi*hi); 1: f16 (hi planes only)
+__global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const float* __restrict__ src,
+                                                              const _Float16* __restrict__ wh,
+                                                              const _Float16* __restrict__ wl,
+                                                              const float* __restrict__ rng,
+                                                              const int* __restrict__ wexp, float* __restrict__ out,
+                                                              Part* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * SP_PIX * 16 + 2 * 2 * 4 * SP_SLOT];
+    _Float16* const Wn = smem;
+    _Float16* const Bs = smem + 2 * 2 * SP_PIX * 16;
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = L % a.gy, mt = L / a.gy;
+    const int n = mt / a.tiles, tile = mt - n * a.tiles;
+    const int tyi = tile / a.tiles_x, txi = tile - tyi * a.tiles_x;
+    const int y0 = tyi * a.R, x0 = txi * a.TW;
+    const int px = ntile / a.cblk, cb = ntile - px * a.cblk;
+    const int n0 = ntile * SP_BN;  // first virtual B row of the tile
+    const int TW = a.TW, WP = a.TW + 2, C = a.C;
+    const int K = 4 * C, nslice = C / 16;
+    const int npix = (a.R + 2) * WP;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid & 3, py = wid >> 2;
+    const int l32 = lane & 31, kh = lane >> 5;
+
+    const int ea = f16x3_exp(rng, a.rng_n);
+    const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
+    const float asc = __builtin_ldexpf(1.f, ea);
+
+    // window staging units (pixel, 8-channel half): byte offset of the unit's channel 0 (-1: zero)
+    int uoff[SP_UNITS];
+#pragma unroll
+    for (int q = 0; q < SP_UNITS; ++q) {
+        const int u = tid + q * SP_NT;
+        const int wpix = u >> 1, h = u & 1;
+        uoff[q] = -1;
+        if (wpix < npix) {
+            const int wr = wpix / WP, wc = wpix - wr * WP;
+            const int sy = y0 - 1 + wr, sx = x0 - 1 + wc;
+            if (sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws) uoff[q] = (((n * a.Hs + sy) * a.Ws + sx) * C + 8 * h) * 4;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    float4 wr_[SP_UNITS][2];
+    auto win_load = [&](int s) {
+#pragma unroll
+        for (int q = 0; q < SP_UNITS; ++q) {
+            const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+            __builtin_memcpy(&wr_[q][0], &v0, 16);
+            __builtin_memcpy(&wr_[q][1], &v1, 16);
+        }
+    };
+    auto win_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < SP_UNITS; ++q) {
+            const int u = tid + q * SP_NT;
+            const int wpix = u >> 1, h = u & 1;
+            if (wpix < npix) {
+                f16x8 hi, lo;
+                split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
+                *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 0, wpix, h)) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 1, wpix, h)) = lo;
+            }
+        }
+    };
+    // B slice: 2 planes x 128 rows x 64 k = 2048 16-byte chunks, 4 per thread; chunk -> (plane, row,
+    // tap, half) with (tap, half) fastest (the 128 contiguous bytes of a row)
+    int bg[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = tid + i * SP_NT;
+        const int pl = q >> 10, rem = q & 1023;
+        const int row = rem >> 3, c8 = rem & 7;
+        bg[i] = pl * 0x40000000 + (n0 + row) * K + c8 * 8;  // bit 30: the lo plane
+        bl[i] = sp_boff(0, pl, c8 >> 1, row, c8 & 1);
+    }
+    uint4 br0, br1, br2, br3;
+    auto b_ld = [&](int i, int kb) {
+        const int g = bg[i] & 0x3fffffff;
+        const _Float16* w = (bg[i] >> 30) ? wl : wh;
+        return *reinterpret_cast<const uint4*>(w + g + kb);
+    };
+    auto b_load = [&](int s) {
+        const int kb = s * 64;
+        br0 = b_ld(0, kb);
+        br1 = b_ld(1, kb);
+        br2 = b_ld(2, kb);
+        br3 = b_ld(3, kb);
+    };
+    auto b_store = [&](int buf) {
+        const int boff = buf * 8 * SP_SLOT;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[0]) = br0;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[1]) = br1;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[2]) = br2;
+        *reinterpret_cast<uint4*>(Bs + boff + bl[3]) = br3;
+    };
+
+    // row block i holds source pixels 2m + i of the wave's 64 (TW even: a pair shares a row), so block 0
+    // at column offset t + 1 reads the fragment block 1 reads at t.  Window pixel of the lane's block-0
+    // pixel at tap (u, t) = (0, 0) of phase (py, px): window row qy + py + u, column qx + px + t
+    int wbe;
+    {
+        const int q = wm * 64 + 2 * l32;
+        const int qy = q / TW;
+        wbe = (qy + py) * WP + (q - qy * TW) + px;
+    }
+
+    floatx16 acc[2][2], t[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
+
+    win_load(0);
+    win_store(0);
+    b_load(0);
+    b_store(0);
+    __syncthreads();
+
+    f16x8 fh[3], fl[3];
+    for (int s = 0; s < nslice; ++s) {
+        const int buf = s & 1, sn = s + 1 < nslice ? s + 1 : s;
+        win_load(sn);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
+        b_load(sn);
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+            const int u = tap >> 1, tx = tap & 1;
+            f16x8 ah[2], al[2], bh[2], bl_[2];
+            if (tx == 0) {  // fragments of window pixels wbe + u * WP + 0 .. 2 (block i, offset t: f = t + i)
+#pragma unroll
+                for (int f = 0; f < 3; ++f) {
+                    const int wpix = wbe + u * WP + f;
+                    fh[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 0, wpix, kh));
+                    if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 1, wpix, kh));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ah[i] = fh[tx + i];
+                if constexpr (NP == 3) al[i] = fl[tx + i];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = py * 64 + j * 32 + l32;
+                bh[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 0, tap, row, kh));
+                if constexpr (NP == 3) bl_[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 1, tap, row, kh));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (NP == 3) {
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl_[j], t[i][j], 0, 0, 0);
+                    }
+                    t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                }
+        }
+        // the other buffers were last read before the previous barrier
+        win_store(buf ^ 1);
+        b_store(buf ^ 1);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] += t[i][j];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+            }
+    }
+
+    // epilogue: undo the operand scales, NHWC store of the phase's pixels, IN statistics
+    const int eab = -(ea + eb);
+    const int Wo = 2 * a.Ws;
+    auto opix = [&](int i, int r) {  // output pixel index within the image (increasing along r, then i)
+        const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+        const int qy = q / TW;
+        return (2 * (y0 + qy) + py) * Wo + 2 * (x0 + q - qy * TW) + px;
+    };
+    const long long obase = (long long)n * (2 * a.Hs) * Wo * a.Co;
+    const int co0 = cb * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+                out[obase + (long long)opix(i, r) * a.Co + co0 + j * 32 + l32] = acc[i][j][r];
+            }
+    if (!parts) return;  // kernel argument: block-uniform
+    // per virtual column: count / mean / M2 / max / first argmax over the wave's 64 pixels, then the
+    // four pixel waves merged in a fixed order; chunk = (tile, px, py) of the image
+    Part* sp = reinterpret_cast<Part*>(smem);  // [4][128]; the loop's last barrier freed the LDS
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        float s = 0.f, mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)  // increasing pixel order (first maximum)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float v = acc[i][j][r];
+                s += v;
+                if (v > mx) { mx = v; am = opix(i, r); }
+            }
+        const float mean = s * (1.f / 32.f);
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float dv = acc[i][j][r] - mean;
+                m2 = fmaf(dv, dv, m2);
+            }
+        const float mb = __shfl_xor(mean, 32, 64), m2b = __shfl_xor(m2, 32, 64), mxb = __shfl_xor(mx, 32, 64);
+        const int amb = __shfl_xor(am, 32, 64);
+        if (kh == 0) {
+            const float dl = mb - mean;
+            Part p;
+            p.cnt = 64.f;
+            p.mean = mean + 0.5f * dl;
+            p.m2 = m2 + m2b + dl * dl * 16.f;
+            p.mx = mx;
+            p.amax = am;
+            if (mxb > mx || (mxb == mx && amb < am)) { p.mx = mxb; p.amax = amb; }
+            p.pad[0] = p.pad[1] = p.pad[2] = 0;
+            sp[wm * SP_BN + py * 64 + j * 32 + l32] = p;
+        }
+    }
+    __syncthreads();
+    if (tid < SP_BN) {
+        Part p = sp[tid];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            const Part b = sp[w * SP_BN + tid];
+            const float tot = p.cnt + b.cnt, dl = b.mean - p.mean;
+            p.mean += dl * (b.cnt / tot);
+            p.m2 += b.m2 + dl * dl * (p.cnt * b.cnt / tot);
+            p.cnt = tot;
+            if (b.mx > p.mx || (b.mx == p.mx && b.amax < p.amax)) { p.mx = b.mx; p.amax = b.amax; }
+        }
+        const int nchunk = 4 * a.tiles;
+        const int chunk = tile * 4 + px * 2 + (tid >> 6);
+        parts[((long long)n * nchunk + chunk) * a.Co + co0 + (tid & 63)] = p;
+    }
+}
+
+// sub-pixel B pack: the range of the combined weights, then every block derives the exponent and
+// writes the hi / lo planes
+__global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restrict__ w, int Cout, int Cin,
+                                                           float* __restrict__ parts) {
+    const long long total = 16LL * Cout * Cin;
+    const int K = 4 * Cin;
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int v = (int)(i / K);
+        m = fmaxf(m, fabsf(subpix_value(w, Cout, Cin, v, (int)(i - (long long)v * K))));
+    }
+    __shared__ float red[4];
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (blockIdx.x == 0)
+        for (int i = gridDim.x + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) parts[i] = 0.f;
+}
+
+__global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restrict__ w, int Cout, int Cin,
+                                                          const float* __restrict__ parts,
+                                                          _Float16* __restrict__ oh, _Float16* __restrict__ ol,
+                                                          int* __restrict__ wexp) {
+    const int e = f16x3_exp(parts, DCS_RANGE_PARTS);
+    const float sc = __builtin_ldexpf(1.f, e);
+    if (blockIdx.x == 0 && threadIdx.x == 0) wexp[0] = e;
+    const long long total = 16LL * Cout * Cin;
+    const int K = 4 * Cin;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const int v = (int)(i / K);
+        const float f = subpix_value(w, Cout, Cin, v, (int)(i - (long long)v * K)) * sc;
+        const _Float16 h = (_Float16)f;
+        oh[i] = h;
+        ol[i] = (_Float16)(f - (float)h);
+    }
+}
+
+bool subpix_geom(const dcs_conv_desc& d, SubArgs* a) {
+    const bool ok = d.parity == 2 && d.up == 1 && d.stride == 1 && d.KH == 3 && d.KW == 3 &&
+                    d.pad_mode == DCS_PAD_ZERO && d.pt == 1 && d.pl == 1 && d.Ho == 2 * d.Hs && d.Wo == 2 * d.Ws &&
+                    d.N > 0 && d.Hs > 0 && d.Ws > 0 && d.Cs % 16 == 0 && d.Cs > 0 && d.Co % 64 == 0 && d.Co > 0 &&
+                    d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+                    d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                    d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
+                    d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+                    16LL * d.Co * d.Cs < (1LL << 30);
+    if (!ok) return false;
+    const int TW = d.Ws < 128 ? d.Ws : 128;
+    if (TW < 16 || 256 % TW || d.Ws % TW || d.Hs % (256 / TW)) return false;  // (TW even)
+    if (a) {
+        a->N = d.N; a->Hs = d.Hs; a->Ws = d.Ws; a->C = d.Cs; a->Co = d.Co;
+        a->TW = TW; a->R = 256 / TW; a->tiles_x = d.Ws / TW; a->tiles = (d.Hs / a->R) * a->tiles_x;
+        a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n;
+    }
+    return true;
+}
+
+}  // namespace
+}  // namespace dcs
+
+using namespace dcs;
+
+extern "C" int dcs_subpix_win_ok(const dcs_conv_desc* dp) { return dp && subpix_geom(*dp, nullptr) ? 1 : 0; }
+
+extern "C" size_t dcs_subpix_win_parts_size(const dcs_conv_desc* dp) {
+    SubArgs a;
+    if (!dp || !subpix_geom(*dp, &a)) return 0;
+    return (size_t)a.N * 4 * a.tiles * a.Co * sizeof(Part);
+}
+
+extern "C" int dcs_subpix_win(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
+                              const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
+    if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "subpix_win: null pointer");
+    SubArgs a;
+    if (!subpix_geom(*dp, &a))
+        return fail(DCS_E_INVALID, "subpix_win: needs a sub-pixel rows descriptor (parity 2: nearest-x2 + 3x3 zero-pad "
+                                   "conv) over contiguous NHWC, Cs % 16 == 0, Co % 64 == 0, min(Ws, 128) dividing 256 "
+                                   "and Ws, Hs % (256 / min(Ws, 128)) == 0, f16x3 / f16 with the source range record");
+    if (parts) {
+        if (!nchunk || parts_bytes < dcs_subpix_win_parts_size(dp))
+            return fail(DCS_E_WORKSPACE, "subpix_win: parts buffer too small");
+        *nchunk = 4 * a.tiles;
+    }
+    const unsigned blocks = (unsigned)((long long)a.N * a.tiles * a.gy);
+    hipStream_t s = as_stream(stream);
+    const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
+    const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
+    if (dp->mma == DCS_MMA_F16)
+        hipLaunchKernelGGL(subpix_win_kernel<1>, dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out,
+                           reinterpret_cast<Part*>(parts));
+    else
+        hipLaunchKernelGGL(subpix_win_kernel<3>, dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out,
+                           reinterpret_cast<Part*>(parts));
+    return check_launch("subpix_win");
+}
+
+extern "C" int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, void* out_hi, void* out_lo, float* scratch,
+                                  int* wexp, void* stream) {
+    if (!w || !out_hi || !out_lo || !scratch || !wexp || Cout <= 0 || Cin <= 0 || Cout % 64 || Cin % 16 ||
+        16LL * Cout * Cin >= (1LL << 30))
+        return fail(DCS_E_INVALID, "pack_subpix_h3: bad arguments (Cout % 64 == 0, Cin % 16 == 0)");
+    hipStream_t s = as_stream(stream);
+    const long long total = 16LL * Cout * Cin;
+    const long long rb = cdiv(total, 2048) < DCS_RANGE_PARTS ? cdiv(total, 2048) : DCS_RANGE_PARTS;
+    hipLaunchKernelGGL(subpix_range_kernel, dim3((unsigned)rb), dim3(256), 0, s, w, Cout, Cin, scratch);
+    int e = check_launch("pack_subpix_h3 range");
+    if (e) return e;
+    const long long pb = cdiv(total, 2048) < 256 ? cdiv(total, 2048) : 256;
+    hipLaunchKernelGGL(subpix_pack_kernel, dim3((unsigned)pb), dim3(256), 0, s, w, Cout, Cin, scratch,
+                       reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo), wexp);
+    return check_launch("pack_subpix_h3");
+}

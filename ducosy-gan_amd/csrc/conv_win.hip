@@ -39,11 +39,17 @@ struct WinArgs {
 
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 
-// half-element offset of (buffer, plane, window pixel, 8-channel half) in the window region:
-// the 16-byte halves of a pixel swap on odd groups of 8 pixels (conflict-free ds_read_b128 for the
-// shifted tap reads and the staging writes alike)
+// half-element offset of (buffer, plane, window pixel, 8-channel half) in the window region: the
+// pixels of a pair swap on odd groups of 8 pixels and the 16-byte halves of a pixel on odd groups of
+// 16, so the fragment reads (every other pixel from any start: the MFMA row blocks interleave) and the
+// staging writes are both conflict-free
 __device__ __forceinline__ int win_off(int buf, int pl, int wpix, int h) {
-    return ((buf * 2 + pl) * WIN_PIX + wpix) * 16 + 8 * (h ^ ((wpix >> 3) & 1));
+    return ((buf * 2 + pl) * WIN_PIX + (wpix ^ ((wpix >> 3) & 1))) * 16 + 8 * (h ^ ((wpix >> 4) & 1));
+}
+// tile pixel of accumulator element r of row block i (the blocks interleave: block i holds pixels
+// 2m + i of the wave's 64, so block 0 at tap tx + 1 reads the fragment block 1 read at tap tx)
+__device__ __forceinline__ int win_pix(int wm, int i, int r, int kh) {
+    return wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
 }
 // B: (buffer, plane, tx, output-channel row, half)
 __device__ __forceinline__ int wb_off(int buf, int pl, int tx, int row, int h) {
@@ -62,12 +68,12 @@ __device__ __forceinline__ void win_stats(const floatx16 (&acc)[2][2], int p0, i
         float s = 0.f, mx = -INFINITY;
         int am = 0;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int r = 0; r < 16; ++r)  // increasing pixel order (first maximum)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int i = 0; i < 2; ++i) {
                 const float v = acc[i][j][r];
                 s += v;
-                if (v > mx) { mx = v; am = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi; }
+                if (v > mx) { mx = v; am = p0 + win_pix(wm, i, r, hi); }
             }
         const float mean = s * (1.f / 32.f);
         float m2 = 0.f;
@@ -131,7 +137,7 @@ __device__ __forceinline__ void win_ibw_load(float (&yv)[2][2][16], const IbwArg
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int pix = p0 + win_pix(wm, i, r, kh);
                 yv[i][j][r] = ib.y[obase + (long long)pix * Co + n0 + wn * 64 + j * 32 + l32];
             }
 }
@@ -150,7 +156,7 @@ __device__ __forceinline__ void win_ibw(const floatx16 (&acc)[2][2], const float
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int pix = p0 + win_pix(wm, i, r, kh);
                 const int py = pix / W, px = pix - py * W;
                 if (py == 1 || py == H - 2 || px == 1 || px == W - 2) continue;  // the ring fold's pixels
                 const float xh = fmaf(yv[i][j][r], s, b);
@@ -288,12 +294,12 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         *reinterpret_cast<uint4*>(Bs + boff + bl[2]) = br2;
     };
 
-    // window pixel of this lane's output row in each 32-row block (tap (0, 0) = the window's top-left)
-    int wb[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int q = wm * 64 + i * 32 + l32;
-        wb[i] = (q / W) * WP + (q - (q / W) * W);
+    // window pixel of this lane's block-0 output pixel 2m (tap (0, 0) = the window's top-left); its
+    // block-1 pixel 2m + 1 is the next one (W is even: the pair shares a row)
+    int wbe;
+    {
+        const int q = wm * 64 + 2 * l32;
+        wbe = (q / W) * WP + (q - (q / W) * W);
     }
 
     floatx16 acc[2][2], t[2][2];
@@ -322,14 +328,21 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty) {
             const int tt = 3 * s + ty, bbuf = tt & 1;
+            // A fragments of window pixels wbe + ty * WP + 0 .. 3: block i at tap tx takes fragment tx + i
+            f16x8 fh[4], fl[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const int wpix = wbe + ty * WP + f;
+                fh[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
+                if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
+            }
 #pragma unroll
             for (int tx = 0; tx < 3; ++tx) {
                 f16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int wpix = wb[i] + ty * WP + tx;
-                    ah[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
-                    if constexpr (NP == 3) al[i] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
+                    ah[i] = fh[tx + i];
+                    if constexpr (NP == 3) al[i] = fl[tx + i];
                 }
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -377,7 +390,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
     const long long obase = (long long)n * a.H * W * a.Co;
     auto ooff = [&](int i, int j, int r) {
-        const int pix = p0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int pix = p0 + win_pix(wm, i, r, kh);
         return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 32 + l32;
     };
 
@@ -770,7 +783,7 @@ namespace {
 
 int win_check(const dcs_conv_desc& d, bool fwd) {
     const bool geom = d.KH == 3 && d.KW == 3 && d.stride == 1 && d.up == 1 && !d.parity && d.Cs % 16 == 0 &&
-                      d.Co % WIN_BN == 0 && d.Ws <= 128 && 256 % d.Ws == 0 && d.Hs % (256 / d.Ws) == 0 &&
+                      d.Co % WIN_BN == 0 && d.Ws >= 2 && d.Ws <= 128 && 256 % d.Ws == 0 && d.Hs % (256 / d.Ws) == 0 &&
                       d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
                       d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs &&
                       d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_a_n > 0 &&

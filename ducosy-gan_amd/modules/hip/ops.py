@@ -34,6 +34,7 @@ _HEAD_PROJ = os.environ.get("DUCOSY_HEAD_PROJ", "1") == "1"
 _BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
 _STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)
 _PREPACK = os.environ.get("DUCOSY_PREPACK", "1") == "1"  # the step's weight packs in two batched launches
+_SUBWIN = os.environ.get("DUCOSY_SUBWIN", "1") == "1"  # up-conv forwards on the sub-pixel window kernel
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -471,6 +472,24 @@ class ConvGeom:
         wpack._dcs_h3 = (hi, lo, wexp)
         return wpack
 
+    @property
+    def subwin(self) -> bool:
+        """Sub-pixel window kernel for this up-conv's forward (csrc/conv_subpix.hip): its pack carries
+        the pre-split phase weights (_dcs_sp) next to the rows pass's kind-3 pack."""
+        return _SUBWIN and _h3() and self.subpixel and self.cout % 64 == 0 and self.cin % 16 == 0
+
+    def _attach_sp(self, wpack: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        hi = torch.empty(4 * self.cout, 4 * self.cin, device=w.device, dtype=torch.float16)
+        lo = torch.empty_like(hi)
+        wexp = torch.empty(1, device=w.device, dtype=torch.int32)
+        scratch = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
+        if _BATCH is not None:
+            _BATCH.add(w, h3=2, Cout=self.cout, Cin=self.cin, h3_hi=hi, h3_lo=lo, h3_wexp=wexp, h3_scratch=scratch)
+        else:
+            lib.call("dcs_pack_subpix_h3", _p(w), self.cout, self.cin, _p(hi), _p(lo), _p(scratch), _p(wexp), _stream())
+        wpack._dcs_sp = (hi, lo, wexp)
+        return wpack
+
     def _key(self):
         return (self.cin, self.cout, self.k, self.stride, self.pads, self.pad_mode, self.up)
 
@@ -493,7 +512,8 @@ class ConvGeom:
         if cin_pad is not None and cin_pad != self.cin:
             return self._pack(w, 5, cin_pad, self.k * self.k * cin_pad, self.cout)
         if self.subpixel:
-            return self._pack(w, 3, self.cin, 16 * self.cin, self.cout)
+            out = self._pack(w, 3, self.cin, 16 * self.cin, self.cout)
+            return self._attach_sp(out, w) if self.subwin else out
         K = self.k * self.k * self.cin
         out = self._pack(w, 0, self.cin, K, self.cout)
         return self._attach_h3(out, w, 0) if self.win else out
@@ -603,6 +623,9 @@ class ConvGeom:
         h3 = getattr(wpack, "_dcs_h3", None)
         if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
             return self._win_in_stats(s, d, h3, nb, want_max)
+        sp = getattr(wpack, "_dcs_sp", None)
+        if nb and sp is not None and bias is None and lib.query("dcs_subpix_win_ok", ctypes.byref(d)):
+            return self._subpix(s, d, sp, True, want_max)
         if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
@@ -635,6 +658,29 @@ class ConvGeom:
         parts = workspace(lib.query("dcs_stem_fwd_parts_size", ctypes.byref(d)), dev) if stats else None
         nchunk = ctypes.c_int(0)
         lib.call("dcs_stem_fwd", ctypes.byref(d), _p(s.t), _p(wpack), _p(out), _p(parts),
+                 parts.numel() if stats else 0, ctypes.byref(nchunk), _stream())
+        if not stats:
+            return out
+        C = self.cout
+        scale = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        shift = torch.empty(s.N, C, device=dev, dtype=torch.float32)
+        xmax = torch.empty(s.N, C, device=dev, dtype=torch.float32) if want_max else None
+        xam = torch.empty(s.N, C, device=dev, dtype=torch.int32) if want_max else None
+        lib.call("dcs_in_stats_finish", _p(parts), s.N, C, nchunk.value, IN_EPS, _p(scale), _p(shift), _p(xmax),
+                 _p(xam), _stream())
+        return out, INStats(scale, shift, xmax, xam)
+
+    def _subpix(self, s: Src, d, sp, stats: bool, want_max: bool = False):
+        """An up-conv forward (+ the IN statistics of its output when ``stats``) on the sub-pixel window
+        kernel (csrc/conv_subpix.hip); f16x3 operands in both fp16 modes, as the stem and head (the f16
+        step's edge-loss selection sits at its tolerance with fp16 up-convs)."""
+        dev = s.t.device
+        d.mma = lib.MMA_F16X3
+        Ho, Wo = self.out_hw(s.H, s.W)
+        out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
+        parts = workspace(lib.query("dcs_subpix_win_parts_size", ctypes.byref(d)), dev) if stats else None
+        nchunk = ctypes.c_int(0)
+        lib.call("dcs_subpix_win", ctypes.byref(d), _p(s.t), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _p(parts),
                  parts.numel() if stats else 0, ctypes.byref(nchunk), _stream())
         if not stats:
             return out
@@ -690,6 +736,9 @@ class ConvGeom:
             _set_mma(d, s.t, pro, _wrng(wpack), wpack)
             if _STEM and bias is None and lib.query("dcs_stem_fwd_ok", ctypes.byref(d)):
                 return self._stem(s, d, wpack, False)
+            sp = getattr(wpack, "_dcs_sp", None)
+            if sp is not None and bias is None and lib.query("dcs_subpix_win_ok", ctypes.byref(d)):
+                return self._subpix(s, d, sp, False)
         h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
         if h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):

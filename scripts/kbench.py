@@ -81,6 +81,12 @@ def main():
         wp = g.pack_fwd(w, cin_pad=x.shape[-1])
         t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p, pro_max=pm), a.reps)
         print(f"{name:8s} {'fwd':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
+        sp = getattr(wp, "_dcs_sp", None)
+        if sp is not None:  # the up-convs: the rows pass the sub-pixel window kernel replaces
+            del wp._dcs_sp
+            t = timeit(lambda: g.forward(Src.nhwc(x), wp, pro=p, pro_max=pm), a.reps)
+            wp._dcs_sp = sp
+            print(f"{name:8s} {'fwdrow':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
         dy = torch.randn(N, Ho, Wo, g.cout, device=dev)
         wd = g.pack_dgrad(w)
         t = timeit(lambda: g.dgrad(dy, wd, H, H), a.reps)

@@ -1,0 +1,87 @@
+"""The sub-pixel window kernel of the Generator's up-convolutions (csrc/conv_subpix.hip;
+modules/model.py:112-120: Upsample(x2, nearest) + Conv2d 3x3 pad 1) against float64 references of
+the same fp32 operands:
+  * forward + the InstanceNorm statistics of its output (scale / shift / max / argmax from the
+    epilogue partials) for up1 (256 -> 128) and up2 (128 -> 64) shapes, source widths 16 .. 256
+    (every tile width the kernel takes: 16, 32, 64, 128 and two column strips);
+  * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in both fp16
+    modes (the host runs the kernel on f16x3 operands in f16 mode too);
+  * the rows pass on the same pack (the phase planes removed) agrees to the same bound, and the
+    batched pack (ops.prepack) equals the per-pack launches bit for bit.
+Tolerances written per check below."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import prng
+from test_gpu_ops import rnd
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _relmax(a, b):
+    return float((a.double().cpu() - b).abs().max() / b.abs().max())
+
+
+@pytest.fixture
+def ops():
+    from modules.hip import ops as o
+    prev = o.get_mma()
+    yield o
+    o.set_mma(prev)
+
+
+def _geom(ops, cin, cout):
+    from modules.hip.lib import DCS_PAD_ZERO
+    return ops.ConvGeom(cin, cout, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2)
+
+
+@pytest.mark.parametrize("mode,tol", [("f16x3", 1e-5), ("f16", 1e-5)])
+@pytest.mark.parametrize("cin,cout,N,H,W", [(256, 128, 2, 16, 16), (256, 128, 1, 8, 32), (128, 64, 2, 8, 64),
+                                            (128, 64, 1, 4, 128), (128, 64, 1, 2, 256)])
+def test_subpix_forward_and_stats_vs_fp64(ops, mode, tol, cin, cout, N, H, W):
+    ops.set_mma(mode)
+    g = _geom(ops, cin, cout)
+    assert g.subwin
+    x = rnd((N, cin, H, W), 81, "x").double()
+    w = torch.from_numpy(prng.normal(82, "w", (cout, cin, 3, 3), 0, 0.05)).float().double()
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, padding=1)
+    mean = ref.mean(dim=(2, 3))
+    var = ref.var(dim=(2, 3), unbiased=False)
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wp = g.pack_fwd(w.float().to(DEV))
+    assert getattr(wp, "_dcs_sp", None) is not None
+    y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
+    assert _relmax(y.permute(0, 3, 1, 2), ref) <= tol
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    assert _relmax(st.scale, rstd) <= tol
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= tol * float((mean * rstd).abs().max() + 1)
+    mx = ref.flatten(2).max(dim=2)
+    assert _relmax(st.xmax, mx.values) <= tol
+    am = st.xargmax.cpu().long()  # the first maximum; a near-tie within rounding may pick either
+    got_at = ref.flatten(2).gather(2, am[..., None])[..., 0]
+    assert float((got_at - mx.values).abs().max()) <= tol * float(mx.values.abs().max())
+    # forward without statistics: the same values
+    y2 = g.forward(ops.Src.nhwc(xd), wp)
+    assert torch.equal(y2, y)
+    # the rows pass over the same pack (phase planes removed) to the same bound
+    sp = wp._dcs_sp
+    del wp._dcs_sp
+    try:
+        y0 = g.forward(ops.Src.nhwc(xd), wp)
+    finally:
+        wp._dcs_sp = sp
+    assert _relmax(y0.permute(0, 3, 1, 2), ref) <= (tol if mode == "f16x3" else 2e-3)  # rows pass: fp16 operands
+
+
+def test_subpix_pack_batched_bit_identical(ops):
+    ops.set_mma("f16x3")
+    g = _geom(ops, 256, 128)
+    w = (rnd((128, 256, 3, 3), 83, "w") * 0.05).float().to(DEV)
+    sp = [a.clone() for a in g.pack_fwd(w)._dcs_sp]
+    w.mul_(1.0)
+    ops.prepack([w])
+    got = g.pack_fwd(w)._dcs_sp
+    for a, b in zip(got, sp):
+        assert torch.equal(a, b)
