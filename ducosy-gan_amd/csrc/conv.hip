@@ -2314,10 +2314,10 @@ __global__ __launch_bounds__(256) void pack_batch1_kernel(const dcs_pack_job* __
     float* rng;
     if (jb.h3 == 2) {  // sub-pixel phase weights: the range of the combined values
         const long long n = 16LL * jb.Cout * jb.Cin;
-        const int K = 4 * jb.Cin;
+        const int K = jb.h3_flip ? 16 * jb.Cout : 4 * jb.Cin;
         for (long long i = (long long)lb * 256 + threadIdx.x; i < n; i += (long long)nb * 256) {
             const int v = (int)(i / K);
-            m = fmaxf(m, fabsf(subpix_value(jb.w, jb.Cout, jb.Cin, v, (int)(i - (long long)v * K))));
+            m = fmaxf(m, fabsf(subpix_value(jb.w, jb.Cout, jb.Cin, jb.h3_flip, v, (int)(i - (long long)v * K))));
         }
         rng = jb.h3_scratch;
     } else if (jb.h3) {
@@ -2355,12 +2355,12 @@ __global__ __launch_bounds__(256) void pack_batch2_kernel(const dcs_pack_job* __
         const float sc = __builtin_ldexpf(1.f, e);
         if (lb == 0 && threadIdx.x == 0) jb.h3_wexp[0] = e;
         const long long total = 16LL * jb.Cout * jb.Cin;
-        const int K = 4 * jb.Cin;
+        const int K = jb.h3_flip ? 16 * jb.Cout : 4 * jb.Cin;
         _Float16* oh = reinterpret_cast<_Float16*>(jb.h3_hi);
         _Float16* ol = reinterpret_cast<_Float16*>(jb.h3_lo);
         for (long long i = (long long)lb * 256 + threadIdx.x; i < total; i += (long long)nb * 256) {
             const int v = (int)(i / K);
-            const float f = subpix_value(jb.w, jb.Cout, jb.Cin, v, (int)(i - (long long)v * K)) * sc;
+            const float f = subpix_value(jb.w, jb.Cout, jb.Cin, jb.h3_flip, v, (int)(i - (long long)v * K)) * sc;
             const _Float16 h = (_Float16)f;
             oh[i] = h;
             ol[i] = (_Float16)(f - (float)h);
@@ -2418,8 +2418,10 @@ extern "C" int dcs_pack_plan(dcs_pack_job* jobs, int njobs, int* g1, int* g2) {
         long long n1, n2 = 0, cap2 = 1;
         if (jb.h3 == 2) {
             if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || jb.Cout <= 0 || jb.Cin <= 0 ||
-                jb.Cout % 64 || jb.Cin % 16 || 16LL * jb.Cout * jb.Cin >= (1LL << 30))
-                return fail(DCS_E_INVALID, "pack_plan: sub-pixel job (Cout % 64 == 0, Cin % 16 == 0)");
+                jb.Cout % 64 || jb.Cin % 16 || 16LL * jb.Cout * jb.Cin >= (1LL << 30) ||
+                (jb.h3_flip && jb.Cin % 128))
+                return fail(DCS_E_INVALID, "pack_plan: sub-pixel job (Cout % 64 == 0, Cin % 16 == 0; data gradient: "
+                                           "Cin % 128 == 0)");
             n1 = n2 = cdiv(16LL * jb.Cout * jb.Cin, 2048);  // dcs_pack_subpix_h3's launches
             cap2 = 256;
         } else if (jb.h3) {
@@ -3099,6 +3101,14 @@ namespace dcs {
 bool wgrad_win_check(const dcs_conv_desc& d);
 size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
 int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
+// conv_subpix.hip: the f16x3 window weight gradient of the up-convolutions (a VARIANT build with
+// EXTRA=-DDCS_SUBPIX_WGRAD=0 runs the x6 phase classes instead, for A/B)
+#ifndef DCS_SUBPIX_WGRAD
+#define DCS_SUBPIX_WGRAD 1
+#endif
+bool subpix_wgrad_check(const dcs_conv_desc& d);
+size_t subpix_wgrad_workspace_size(const dcs_conv_desc& d);
+int subpix_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
 }  // namespace dcs
 
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
@@ -3107,6 +3117,10 @@ extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
     size_t n = (size_t)p.nsplit * (dp->parity == 2 ? 4 : 1) * dp->Co * p.Ktot * sizeof(float);
     if (DCS_WGRAD_WIN && wgrad_win_check(*dp)) {
         const size_t nw = wgrad_win_workspace_size(*dp);
+        n = nw > n ? nw : n;
+    }
+    if (DCS_SUBPIX_WGRAD && subpix_wgrad_check(*dp)) {
+        const size_t nw = subpix_wgrad_workspace_size(*dp);
         n = nw > n ? nw : n;
     }
     return n;
@@ -3137,6 +3151,14 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
                            3, 3, d.Cs, dw);
         return check_launch("conv_wgrad_reduce");
+    }
+    if (DCS_SUBPIX_WGRAD && subpix_wgrad_check(d) && !x2) {  // f16x3 up-convolution: the rolling-window phase kernel
+        const int ns = subpix_wgrad_launch(d, dy, x, w, s);
+        if (ns < 0) return -ns;
+        const long long tot9 = (long long)d.Co * d.Cs * 9;
+        hipLaunchKernelGGL(wgrad_subpixel_fold_kernel, dim3((unsigned)cdiv(tot9, 256)), dim3(256), 0, s, w, ns, d.Co,
+                           d.Cs, dw);
+        return check_launch("wgrad_subpixel_fold");
     }
     const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity &&
                      d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;

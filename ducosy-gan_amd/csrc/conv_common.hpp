@@ -48,23 +48,34 @@ __device__ __forceinline__ int xcd_remap(int L, int T) {
     return base + (L >> 3);
 }
 
-// B of the sub-pixel window kernel (conv_subpix.hip) for nearest-x2 upsample + 3x3 zero-pad conv weights
-// w[Cout][Cin][3][3]: virtual row v = (column tile (px, 64-channel block), row phase py, channel) and
-// k = (16-channel slice, source row offset u, column offset t, channel); the value is the sum of the
-// 3x3 taps that land on source offset (u, t) for output phase (py, px): taps 0 | 1,2 for phase 0,
-// 0,1 | 2 for phase 1 (the upsample folded into the weights, four taps per phase instead of nine)
-__device__ __forceinline__ float subpix_value(const float* __restrict__ w, int Cout, int Cin, int v, int k) {
-    const int cblk = Cout >> 6;
-    const int ntile = v >> 7, py = (v >> 6) & 1;
-    const int px = ntile / cblk, co = (ntile - px * cblk) * 64 + (v & 63);
-    const int rem = k & 63, u = rem >> 5, t = (rem >> 4) & 1, c = (k >> 6) * 16 + (rem & 15);
+// Sub-pixel phase weights (conv_subpix.hip): for nearest-x2 upsample + 3x3 zero-pad conv weights
+// w[Cout][Cin][3][3], output phase (py, px) at source offset (u, t) sums the 3x3 taps that land on that
+// source pixel: rows 0 | 1,2 for phase 0, 0,1 | 2 for phase 1 (likewise columns) -- the upsample folded
+// into the weights, four taps per phase instead of nine.
+__device__ __forceinline__ float subpix_tapsum(const float* __restrict__ w, int Cin, int co, int ci, int py, int px,
+                                               int u, int t) {
     const int ya = py ? (u ? 2 : 0) : (u ? 1 : 0), yb = py ? (u ? 2 : 1) : (u ? 2 : 0);
     const int xa = px ? (t ? 2 : 0) : (t ? 1 : 0), xb = px ? (t ? 2 : 1) : (t ? 2 : 0);
-    const float* wp = w + ((long long)co * Cin + c) * 9;
+    const float* wp = w + ((long long)co * Cin + ci) * 9;
     float s = 0.f;
     for (int ty = ya; ty <= yb; ++ty)
         for (int tx = xa; tx <= xb; ++tx) s += wp[ty * 3 + tx];
     return s;
+}
+// B of the forward: virtual row v = (column tile (px, 64-channel block), row phase py, channel), k =
+// (16-channel slice, u, t, channel).  B of the data gradient: row = input channel ci, k = (phase, slice
+// of the output channels, window offset (1 - u, 1 - t), channel).  [4 Cout or Cin rows][4 Cin or 4 Cout]
+__device__ __forceinline__ float subpix_value(const float* __restrict__ w, int Cout, int Cin, int dgrad, int v, int k) {
+    const int rem = k & 63, tap = rem >> 4;
+    if (!dgrad) {
+        const int cblk = Cout >> 6;
+        const int ntile = v >> 7, py = (v >> 6) & 1;
+        const int px = ntile / cblk, co = (ntile - px * cblk) * 64 + (v & 63);
+        return subpix_tapsum(w, Cin, co, (k >> 6) * 16 + (rem & 15), py, px, tap >> 1, tap & 1);
+    }
+    const int nslice = Cout >> 4, it = k >> 6;
+    const int ph = it / nslice, co = (it - ph * nslice) * 16 + (rem & 15);
+    return subpix_tapsum(w, Cin, co, v, ph >> 1, ph & 1, 1 - (tap >> 1), 1 - (tap & 1));
 }
 
 }  // namespace dcs

@@ -16,6 +16,13 @@
 // B arrives pre-split (dcs_pack_subpix_h3: hi / lo fp16 planes [4 Co][4 C], k = slice * 64 + u * 32 +
 // t * 16 + c).  One fp32 chain per slice (64 k), added to the running sum (two-level, as conv.hip).
 // LDS: window [2][2 planes][520 px][16] + B [2][2 planes][4 taps][128 rows x 16 + 48] halves (131 KB).
+//
+// Data gradient (MODE 1): dx[i][j] = sum over phases (py, px) and offsets (u, t) of
+// dy[2 (i + 1 - py - u) + py][2 (j + 1 - px - t) + px] . W_phase[u][t]^T: per phase a 2x2 convolution of
+// the phase's dy sub-grid (every other dy pixel) with the transposed phase weights.  The k loop runs
+// over (phase, 16-channel slice of dy); each iteration stages the phase's (R + 1) x (TW + 1) dy window and
+// its B slice, and every wave runs the 4 offsets of that phase (8 waves = 4 pixel x 2 channel blocks of
+// a 256-pixel x 128-input-channel tile).
 #include "common.hpp"
 #include "conv_common.hpp"
 
@@ -28,9 +35,10 @@ constexpr int SP_SLOT = 128 * 16 + 48;      // halves per B tap slot (the four s
 constexpr int SP_UNITS = (2 * SP_PIX + SP_NT - 1) / SP_NT;
 
 struct SubArgs {
-    int N, Hs, Ws, C, Co;  // source NHWC [N][Hs][Ws][C]; output NHWC [N][2 Hs][2 Ws][Co]
+    int N, Hs, Ws, C, Co;  // MODE 0: source NHWC [N][Hs][Ws][C], output [N][2 Hs][2 Ws][Co];
+                           // MODE 1: dy [N][2 Hs][2 Ws][C], dx [N][Hs][Ws][Co]
     int R, TW, tiles_x, tiles;  // tile = R rows x TW columns of the source; tiles per row band / image
-    int gy, cblk;          // column tiles (4 Co / 128), 64-channel blocks (Co / 64)
+    int gy, cblk;          // column tiles (MODE 0: 4 Co / 128, MODE 1: Co / 128), 64-channel blocks (Co / 64)
     int rng_n;
 };
 
@@ -43,7 +51,8 @@ __device__ __forceinline__ int sp_boff(int buf, int pl, int tap, int row, int h)
     return ((buf * 2 + pl) * 4 + tap) * SP_SLOT + row * 16 + 8 * (h ^ ((row >> 3) & 1));
 }
 
-template <int NP>  // 3: f16x3 (lo*hi + hi*lo + hi*hi); 1: f16 (hi planes only)
+// NP 3: f16x3 (lo*hi + hi*lo + hi*hi), 1: f16 (hi planes only); MODE 0: forward, 1: data gradient
+template <int NP, int MODE>
 __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const float* __restrict__ src,
                                                               const _Float16* __restrict__ wh,
                                                               const _Float16* __restrict__ wl,
@@ -59,21 +68,24 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     const int n = mt / a.tiles, tile = mt - n * a.tiles;
     const int tyi = tile / a.tiles_x, txi = tile - tyi * a.tiles_x;
     const int y0 = tyi * a.R, x0 = txi * a.TW;
-    const int px = ntile / a.cblk, cb = ntile - px * a.cblk;
-    const int n0 = ntile * SP_BN;  // first virtual B row of the tile
-    const int TW = a.TW, WP = a.TW + 2, C = a.C;
-    const int K = 4 * C, nslice = C / 16;
-    const int npix = (a.R + 2) * WP;
+    const int px = MODE == 0 ? ntile / a.cblk : 0, cb = ntile - px * a.cblk;
+    const int n0 = ntile * SP_BN;  // first (virtual) B row of the tile
+    const int TW = a.TW, WP = MODE == 0 ? a.TW + 2 : a.TW + 1, C = a.C;
+    const int nslice = C / 16, nit = MODE == 0 ? nslice : 4 * nslice;
+    const int K = 64 * nit;
+    const int npix = (MODE == 0 ? a.R + 2 : a.R + 1) * WP;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid & 3, py = wid >> 2;
+    const int wm = wid & 3, py = wid >> 2;  // MODE 1: py is the wave's 64-channel half of the tile
     const int l32 = lane & 31, kh = lane >> 5;
 
     const int ea = f16x3_exp(rng, a.rng_n);
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
     const float asc = __builtin_ldexpf(1.f, ea);
 
-    // window staging units (pixel, 8-channel half): byte offset of the unit's channel 0 (-1: zero)
+    // window staging units (pixel, 8-channel half).  MODE 0: byte offset of the unit's channel 0 (-1:
+    // zero).  MODE 1: the unit's window (row, column) packed as row * 4096 + column (-1: none); the dy
+    // pixel depends on the iteration's phase
     int uoff[SP_UNITS];
 #pragma unroll
     for (int q = 0; q < SP_UNITS; ++q) {
@@ -82,17 +94,33 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         uoff[q] = -1;
         if (wpix < npix) {
             const int wr = wpix / WP, wc = wpix - wr * WP;
-            const int sy = y0 - 1 + wr, sx = x0 - 1 + wc;
-            if (sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws) uoff[q] = (((n * a.Hs + sy) * a.Ws + sx) * C + 8 * h) * 4;
+            if constexpr (MODE == 0) {
+                const int sy = y0 - 1 + wr, sx = x0 - 1 + wc;
+                if (sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws) uoff[q] = (((n * a.Hs + sy) * a.Ws + sx) * C + 8 * h) * 4;
+            } else {
+                uoff[q] = wr * 4096 + wc;
+            }
         }
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float4 wr_[SP_UNITS][2];
-    auto win_load = [&](int s) {
+    auto unit_off = [&](int q, int it) {  // byte offset of unit q's 8 channels at iteration it (OOB: zero)
+        if constexpr (MODE == 0) {
+            return uoff[q] >= 0 ? uoff[q] + it * 64 : 0x7fffffbf;
+        } else {
+            const int ph = it / nslice, s = it - ph * nslice;
+            const int qy = ph >> 1, qx = ph & 1;  // the phase
+            const int cy = y0 - qy + (uoff[q] >> 12), cx = x0 - qx + (uoff[q] & 4095);  // phase sub-grid pixel
+            const bool ok = uoff[q] >= 0 && cy >= 0 && cy < a.Hs && cx >= 0 && cx < a.Ws;
+            const int h = (tid + q * SP_NT) & 1;
+            return ok ? ((((n * 2 * a.Hs + 2 * cy + qy) * 2 * a.Ws + 2 * cx + qx) * C + 8 * h) * 4 + s * 64) : 0x7fffffbf;
+        }
+    };
+    auto win_load = [&](int it) {
 #pragma unroll
         for (int q = 0; q < SP_UNITS; ++q) {
-            const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+            const int off = unit_off(q, it);
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
             __builtin_memcpy(&wr_[q][0], &v0, 16);
@@ -129,8 +157,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         const _Float16* w = (bg[i] >> 30) ? wl : wh;
         return *reinterpret_cast<const uint4*>(w + g + kb);
     };
-    auto b_load = [&](int s) {
-        const int kb = s * 64;
+    auto b_load = [&](int it) {
+        const int kb = it * 64;
         br0 = b_ld(0, kb);
         br1 = b_ld(1, kb);
         br2 = b_ld(2, kb);
@@ -146,12 +174,13 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 
     // row block i holds source pixels 2m + i of the wave's 64 (TW even: a pair shares a row), so block 0
     // at column offset t + 1 reads the fragment block 1 reads at t.  Window pixel of the lane's block-0
-    // pixel at tap (u, t) = (0, 0) of phase (py, px): window row qy + py + u, column qx + px + t
+    // pixel at tap (u, t) = (0, 0): MODE 0 (phase (py, px)): window row qy + py + u, column qx + px + t;
+    // MODE 1 (window offset (o_r, o_c) = (1 - u, 1 - t)): row qy + o_r, column qx + o_c
     int wbe;
     {
         const int q = wm * 64 + 2 * l32;
         const int qy = q / TW;
-        wbe = (qy + py) * WP + (q - qy * TW) + px;
+        wbe = MODE == 0 ? (qy + py) * WP + (q - qy * TW) + px : qy * WP + (q - qy * TW);
     }
 
     floatx16 acc[2][2], t[2][2];
@@ -169,8 +198,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     __syncthreads();
 
     f16x8 fh[3], fl[3];
-    for (int s = 0; s < nslice; ++s) {
-        const int buf = s & 1, sn = s + 1 < nslice ? s + 1 : s;
+    for (int s = 0; s < nit; ++s) {
+        const int buf = s & 1, sn = s + 1 < nit ? s + 1 : s;
         win_load(sn);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
         b_load(sn);
 #pragma unroll
@@ -221,8 +250,23 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             }
     }
 
-    // epilogue: undo the operand scales, NHWC store of the phase's pixels, IN statistics
     const int eab = -(ea + eb);
+    if constexpr (MODE == 1) {  // dx NHWC store
+        const long long obase = (long long)n * a.Hs * a.Ws * a.Co;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+                    const int qy = q / TW;
+                    const long long pix = (long long)(y0 + qy) * a.Ws + x0 + q - qy * TW;
+                    out[obase + pix * a.Co + n0 + py * 64 + j * 32 + l32] = __builtin_ldexpf(acc[i][j][r], eab);
+                }
+        return;
+    }
+    // epilogue: undo the operand scales, NHWC store of the phase's pixels, IN statistics
     const int Wo = 2 * a.Ws;
     auto opix = [&](int i, int r) {  // output pixel index within the image (increasing along r, then i)
         const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
@@ -299,15 +343,15 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 }
 
 // sub-pixel B pack: the range of the combined weights, then every block derives the exponent and
-// writes the hi / lo planes
-__global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restrict__ w, int Cout, int Cin,
+// writes the hi / lo planes ([4 Cout][4 Cin] forward, [Cin][16 Cout] data gradient)
+__global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
                                                            float* __restrict__ parts) {
     const long long total = 16LL * Cout * Cin;
-    const int K = 4 * Cin;
+    const int K = dgrad ? 16 * Cout : 4 * Cin;
     float m = 0.f;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         const int v = (int)(i / K);
-        m = fmaxf(m, fabsf(subpix_value(w, Cout, Cin, v, (int)(i - (long long)v * K))));
+        m = fmaxf(m, fabsf(subpix_value(w, Cout, Cin, dgrad, v, (int)(i - (long long)v * K))));
     }
     __shared__ float red[4];
     m = wave_max(m);
@@ -318,7 +362,7 @@ __global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restri
         for (int i = gridDim.x + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) parts[i] = 0.f;
 }
 
-__global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restrict__ w, int Cout, int Cin,
+__global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
                                                           const float* __restrict__ parts,
                                                           _Float16* __restrict__ oh, _Float16* __restrict__ ol,
                                                           int* __restrict__ wexp) {
@@ -326,14 +370,265 @@ __global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restric
     const float sc = __builtin_ldexpf(1.f, e);
     if (blockIdx.x == 0 && threadIdx.x == 0) wexp[0] = e;
     const long long total = 16LL * Cout * Cin;
-    const int K = 4 * Cin;
+    const int K = dgrad ? 16 * Cout : 4 * Cin;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         const int v = (int)(i / K);
-        const float f = subpix_value(w, Cout, Cin, v, (int)(i - (long long)v * K)) * sc;
+        const float f = subpix_value(w, Cout, Cin, dgrad, v, (int)(i - (long long)v * K)) * sc;
         const _Float16 h = (_Float16)f;
         oh[i] = h;
         ol[i] = (_Float16)(f - (float)h);
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Weight gradient of the up-convolutions on a rolling source window (f16x3), per phase:
+//   dWp[py][px][u][t][co][ci] = sum_{i, j} dy[2i + py][2j + px][co] * src[i + py + u - 1][j + px + t - 1][ci]
+// folded onto the 3x3 taps by conv.hip's wgrad_subpixel_fold_kernel (slabs [split][phase][co][(u, t), ci]).
+// conv.hip's x6 weight gradient runs the phases as four classes of a 128 x 128 (co, (tap, ci)) tile and
+// gathers the source per tap column group.  Here a workgroup owns 32 co x 64 ci x all 16 (phase, tap)
+// pairs and walks a 64-pixel-wide strip of the low-resolution grid row by row: per row it stages the two
+// dy rows of the strip (128 px each, de-interleaved by column phase) and ONE new source row segment
+// (66 px with the halo) into a ring of four rows, split into hi / lo fp16 once; wave (phase, ci block)
+// reads its dy fragment once per 16-pixel sub-tile and its four taps' source fragments at a per-tap
+// (ring slot, pixel) offset.  MFMA: M = co (32), N = ci (32), K = 16 low-resolution pixels; fragments
+// by ds_read_b64_tr_b16 as conv_win.hip's weight gradient (source ring: its 64-channel swizzled
+// layout; dy: 32-channel rows, conflict-free unswizzled).  Two-level accumulation over row pairs.
+constexpr int SW_NT = 512, SW_SW = 64, SW_WP = SW_SW + 2;
+constexpr int SW_XROW = 2 * SW_WP * 64;      // halves per ring slot (2 planes x 66 px x 64 ci)
+constexpr int SW_DPH = 2 * SW_SW * 32;       // halves per (py, px) dy region (2 planes x 64 px x 32 co)
+constexpr int SW_DBUF = 4 * SW_DPH;          // halves per dy buffer (4 phases)
+constexpr int SW_XU = (SW_WP * 8 + SW_NT - 1) / SW_NT;  // source-row (pixel, 8-channel unit)s per thread: 2
+
+struct SWArgs {
+    int N, H, W, C, Co;  // source NHWC [N][H][W][C] (low resolution); dy NHWC [N][2H][2W][Co]
+    int strips, rchunks, rows_per;
+    int gco, gci;        // 32-channel co tiles, 64-channel ci tiles
+    int rng_a_n, rng_b_n;
+};
+
+__device__ __forceinline__ int sw_swz(int pix) { return ((pix >> 1) & 1) << 2; }
+
+typedef short swshortx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) swshortx4 lds_swshortx4;
+
+// fragment of 8 consecutive pixels of one channel per lane from a pixel-major image of `pitch` halves
+// per pixel (two transposed 4-pixel reads)
+template <int PITCH>
+__device__ __forceinline__ f16x8 sw_frag(const _Float16* p) {
+    const swshortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_swshortx4*)(p));
+    const swshortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_swshortx4*)(p + 4 * PITCH));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int NP>
+__global__ __launch_bounds__(SW_NT, 1) void subpix_wgrad_kernel(SWArgs a, const float* __restrict__ dy,
+                                                                const float* __restrict__ src,
+                                                                const float* __restrict__ rnga,
+                                                                const float* __restrict__ rngb,
+                                                                float* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * SW_XROW + 2 * SW_DBUF];
+    _Float16* const Xr = smem;                 // [4][2][66][64]
+    _Float16* const Dy = smem + 4 * SW_XROW;   // [2][py][px][2][64][32]
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = a.gco * a.gci;
+    const int tile = L % ntile, split = L / ntile;
+    const int co0 = (tile % a.gco) * 32, ci0 = (tile / a.gco) * 64;
+    const int rc = split % a.rchunks, rest = split / a.rchunks;
+    const int strip = rest % a.strips, n = rest / a.strips;
+    const int x0 = strip * SW_SW;
+    const int H = a.H, W = a.W, C = a.C, Co = a.Co;
+    const int y_beg = rc * a.rows_per;
+    const int y_end = y_beg + a.rows_per < H ? y_beg + a.rows_per : H;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int cib = wid & 1, ph = wid >> 1, py = ph >> 1, px = ph & 1;
+
+    const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
+    const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int OOB = 0x7fffffbf;
+
+    // dy: 2 rows x 128 px x 4 units (8 co) = 1024 units, 2 per thread: unit -> (row phase, column
+    // phase, low-res pixel j, unit) with the unit fastest, then j (8 lanes write 128 contiguous bytes)
+    int doff[2], dls[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int u = tid + q * SW_NT;
+        const int cu = u & 3, j = (u >> 2) & 63, qx = (u >> 8) & 1, qy = u >> 9;
+        doff[q] = (qy * 2 * W + 2 * (x0 + j) + qx) * Co * 4 + (co0 + 8 * cu) * 4;  // + row 2y base
+        dls[q] = (qy * 2 + qx) * SW_DPH + j * 32 + 8 * cu;
+    }
+    // source row segment: 66 px (halo included) x 8 units; byte offset within the row (-1: none)
+    int xoff[SW_XU], xls[SW_XU];
+#pragma unroll
+    for (int q = 0; q < SW_XU; ++q) {
+        const int u = tid + q * SW_NT, wc = u >> 3, cu = u & 7;
+        xoff[q] = -1;
+        xls[q] = -1;
+        if (wc < SW_WP) {
+            const int sx = x0 - 1 + wc;
+            if (sx >= 0 && sx < W) xoff[q] = (sx * C + ci0 + 8 * cu) * 4;
+            xls[q] = wc * 64 + 8 * (cu ^ sw_swz(wc));
+        }
+    }
+    float4 dr[2][2], xr[SW_XU][2];
+    auto ld_dy = [&](int y) {  // dy rows 2y, 2y + 1
+        const int rb = ((n * 2 * H + 2 * y) * 2 * W) * Co * 4;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q], 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff[q] + 16, 0, 0);
+            __builtin_memcpy(&dr[q][0], &v0, 16);
+            __builtin_memcpy(&dr[q][1], &v1, 16);
+        }
+    };
+    auto ld_x = [&](int r) {  // logical source row r in [-1, H]: zero outside the image
+        const bool ok = r >= 0 && r < H;
+        const int rb = ((n * H + (ok ? r : 0)) * W) * C * 4;
+#pragma unroll
+        for (int q = 0; q < SW_XU; ++q) {
+            const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
+            __builtin_memcpy(&xr[q][0], &v0, 16);
+            __builtin_memcpy(&xr[q][1], &v1, 16);
+        }
+    };
+    auto st_dy = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            f16x8 hi, lo;
+            split8h(dr[q][0], dr[q][1], asc, hi, lo);
+            *reinterpret_cast<f16x8*>(Dy + buf * SW_DBUF + dls[q]) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * SW_DBUF + dls[q] + SW_SW * 32) = lo;
+        }
+    };
+    auto st_x = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < SW_XU; ++q) {
+            if (xls[q] >= 0) {
+                f16x8 hi, lo;
+                split8h(xr[q][0], xr[q][1], bsc, hi, lo);
+                *reinterpret_cast<f16x8*>(Xr + slot * SW_XROW + xls[q]) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * SW_XROW + SW_WP * 64 + xls[q]) = lo;
+            }
+        }
+    };
+
+    // transposed-read lane offsets (halves), as conv_win.hip's weight gradient
+    const int g16 = lane >> 4;
+    const int rpix = 8 * (g16 >> 1) + ((lane & 15) >> 2);
+    const int rcol = 16 * (g16 & 1) + 4 * (lane & 3);
+    const int aoff = ph * SW_DPH + rpix * 32 + rcol;  // dy region of the wave's phase, its 32 co
+    int boff[2];
+    {
+        const int cb = 32 * cib + rcol;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int p = rpix + px + t;  // window column j + px + t
+            boff[t] = p * 64 + 8 * ((cb >> 3) ^ sw_swz(p)) + (cb & 7);
+        }
+    }
+
+    floatx16 acc[4], tq[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; tq[i][r] = 0.f; }
+
+    // prologue: source rows y_beg-1 .. y_beg+1 into their ring slots, dy rows of y_beg into buffer 0
+#pragma unroll 1
+    for (int r = y_beg - 1; r <= y_beg + 1; ++r) {
+        ld_x(r);
+        st_x(r & 3);
+    }
+    ld_dy(y_beg);
+    st_dy(y_beg & 1);
+    __syncthreads();
+
+#pragma unroll 1
+    for (int y = y_beg; y < y_end; ++y) {
+        ld_dy(y + 1 < y_end ? y + 1 : y);  // unconditional (clamped / zero past the image)
+        ld_x(y + 2);
+        const _Float16* const Db = Dy + (y & 1) * SW_DBUF;
+        const _Float16* Xs[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) Xs[u] = Xr + ((y + 3 + py + u) & 3) * SW_XROW;  // row y + py + u - 1
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // 16-pixel sub-tiles of the strip
+            f16x8 ah, al;
+            ah = sw_frag<32>(Db + aoff + k * 16 * 32);
+            if constexpr (NP == 3) al = sw_frag<32>(Db + SW_SW * 32 + aoff + k * 16 * 32);
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap) {
+                const int u = tap >> 1, t = tap & 1;
+                f16x8 bh, bl;
+                bh = sw_frag<64>(Xs[u] + boff[t] + k * 16 * 64);
+                if constexpr (NP == 3) {
+                    bl = sw_frag<64>(Xs[u] + SW_WP * 64 + boff[t] + k * 16 * 64);
+                    tq[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tq[tap], 0, 0, 0);
+                    tq[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tq[tap], 0, 0, 0);
+                }
+                tq[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tq[tap], 0, 0, 0);
+            }
+            if (k == 1) {  // stage the rows loaded above into the buffers this row does not read
+                st_dy((y + 1) & 1);
+                st_x((y + 2) & 3);
+            }
+        }
+        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                acc[i] += tq[i];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tq[i][r] = 0.f;
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: undo the operand scales, slab [split][phase][co][(u, t) * C + ci]
+    const int eab = -(ea + eb);
+    const long long Ktot = 4LL * C;
+    float* const slab = ws + ((long long)split * 4 + ph) * Co * Ktot;
+    const int col = ci0 + 32 * cib + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            slab[(long long)row * Ktot + i * C + col] = __builtin_ldexpf(acc[i][r], eab);
+        }
+}
+
+struct SWPlan {
+    int strips, rchunks, rows_per, nsplit;
+};
+SWPlan sw_plan(const dcs_conv_desc& d) {
+    SWPlan p;
+    p.strips = d.Ws / SW_SW;
+    const long long base = (long long)d.N * p.strips * (d.Co / 32) * (d.Cs / 64);
+    int rch = (int)cdiv(256, base);  // at least one workgroup per CU
+    const int maxch = d.Hs / 8 > 0 ? d.Hs / 8 : 1;  // >= 8 rows per chunk
+    rch = rch < 1 ? 1 : (rch > maxch ? maxch : rch);
+    p.rows_per = (int)cdiv(d.Hs, rch);
+    p.rchunks = (int)cdiv(d.Hs, p.rows_per);
+    p.nsplit = d.N * p.strips * p.rchunks;
+    return p;
+}
+
+bool tile_geom(int N, int Hs, int Ws, SubArgs* a) {
+    const int TW = Ws < 128 ? Ws : 128;
+    if (N <= 0 || Hs <= 0 || TW < 16 || 256 % TW || Ws % TW || Hs % (256 / TW)) return false;  // (TW even)
+    if (a) {
+        a->N = N; a->Hs = Hs; a->Ws = Ws;
+        a->TW = TW; a->R = 256 / TW; a->tiles_x = Ws / TW; a->tiles = (Hs / a->R) * a->tiles_x;
+    }
+    return true;
 }
 
 bool subpix_geom(const dcs_conv_desc& d, SubArgs* a) {
@@ -345,14 +640,24 @@ bool subpix_geom(const dcs_conv_desc& d, SubArgs* a) {
                     d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
                     d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
                     16LL * d.Co * d.Cs < (1LL << 30);
-    if (!ok) return false;
-    const int TW = d.Ws < 128 ? d.Ws : 128;
-    if (TW < 16 || 256 % TW || d.Ws % TW || d.Hs % (256 / TW)) return false;  // (TW even)
-    if (a) {
-        a->N = d.N; a->Hs = d.Hs; a->Ws = d.Ws; a->C = d.Cs; a->Co = d.Co;
-        a->TW = TW; a->R = 256 / TW; a->tiles_x = d.Ws / TW; a->tiles = (d.Hs / a->R) * a->tiles_x;
-        a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n;
-    }
+    if (!ok || !tile_geom(d.N, d.Hs, d.Ws, a)) return false;
+    if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
+    return true;
+}
+
+// the data gradient's descriptor (modules/hip/ops.py dgrad, the rows pass's form): source = dy [N][Hs][Ws][Cs]
+// (the forward's output), a 4x4 stride-2 zero-pad-1 conv onto dx [N][Ho][Wo][Co] with Hs = 2 Ho, Ws = 2 Wo
+bool subpix_dgrad_geom(const dcs_conv_desc& d, SubArgs* a) {
+    const bool ok = d.parity == 0 && d.up == 1 && d.stride == 2 && d.KH == 4 && d.KW == 4 &&
+                    d.pad_mode == DCS_PAD_ZERO && d.pt == 1 && d.pl == 1 && d.Hs == 2 * d.Ho && d.Ws == 2 * d.Wo &&
+                    d.N > 0 && d.Ho > 0 && d.Wo > 0 && d.Cs % 16 == 0 && d.Cs > 0 && d.Co % 128 == 0 && d.Co > 0 &&
+                    d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+                    d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                    d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
+                    d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+                    16LL * d.Co * d.Cs < (1LL << 30);
+    if (!ok || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
+    if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
     return true;
 }
 
@@ -387,27 +692,89 @@ extern "C" int dcs_subpix_win(const dcs_conv_desc* dp, const float* src, const v
     const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
-        hipLaunchKernelGGL(subpix_win_kernel<1>, dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out,
-                           reinterpret_cast<Part*>(parts));
+        hipLaunchKernelGGL((subpix_win_kernel<1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
+                           out, reinterpret_cast<Part*>(parts));
     else
-        hipLaunchKernelGGL(subpix_win_kernel<3>, dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out,
-                           reinterpret_cast<Part*>(parts));
+        hipLaunchKernelGGL((subpix_win_kernel<3, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
+                           out, reinterpret_cast<Part*>(parts));
     return check_launch("subpix_win");
 }
 
-extern "C" int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, void* out_hi, void* out_lo, float* scratch,
-                                  int* wexp, void* stream) {
+extern "C" int dcs_subpix_win_dgrad_ok(const dcs_conv_desc* dp) { return dp && subpix_dgrad_geom(*dp, nullptr) ? 1 : 0; }
+
+extern "C" int dcs_subpix_win_dgrad(const dcs_conv_desc* dp, const float* dy, const void* w_hi, const void* w_lo,
+                                    const int* wexp, float* dx, void* stream) {
+    if (!dp || !dy || !w_hi || !w_lo || !wexp || !dx) return fail(DCS_E_INVALID, "subpix_win_dgrad: null pointer");
+    SubArgs a;
+    if (!subpix_dgrad_geom(*dp, &a))
+        return fail(DCS_E_INVALID, "subpix_win_dgrad: needs the sub-pixel data-gradient descriptor (4x4 stride-2 "
+                                   "zero-pad-1 over contiguous NHWC dy, Hs = 2 Ho), Cs % 16 == 0, Co % 128 == 0, "
+                                   "min(Wo, 128) dividing 256 and Wo, Ho % (256 / min(Wo, 128)) == 0, f16x3 / f16 with "
+                                   "the dy range record");
+    const unsigned blocks = (unsigned)((long long)a.N * a.tiles * a.gy);
+    hipStream_t s = as_stream(stream);
+    const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
+    const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
+    if (dp->mma == DCS_MMA_F16)
+        hipLaunchKernelGGL((subpix_win_kernel<1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
+                           nullptr);
+    else
+        hipLaunchKernelGGL((subpix_win_kernel<3, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
+                           nullptr);
+    return check_launch("subpix_win_dgrad");
+}
+
+extern "C" int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, int dgrad, void* out_hi, void* out_lo,
+                                  float* scratch, int* wexp, void* stream) {
     if (!w || !out_hi || !out_lo || !scratch || !wexp || Cout <= 0 || Cin <= 0 || Cout % 64 || Cin % 16 ||
-        16LL * Cout * Cin >= (1LL << 30))
-        return fail(DCS_E_INVALID, "pack_subpix_h3: bad arguments (Cout % 64 == 0, Cin % 16 == 0)");
+        16LL * Cout * Cin >= (1LL << 30) || (dgrad && (Cout % 16 || Cin % 128)))
+        return fail(DCS_E_INVALID, "pack_subpix_h3: bad arguments (Cout % 64 == 0, Cin % 16 == 0; data gradient: "
+                                   "Cin % 128 == 0)");
     hipStream_t s = as_stream(stream);
     const long long total = 16LL * Cout * Cin;
     const long long rb = cdiv(total, 2048) < DCS_RANGE_PARTS ? cdiv(total, 2048) : DCS_RANGE_PARTS;
-    hipLaunchKernelGGL(subpix_range_kernel, dim3((unsigned)rb), dim3(256), 0, s, w, Cout, Cin, scratch);
+    hipLaunchKernelGGL(subpix_range_kernel, dim3((unsigned)rb), dim3(256), 0, s, w, Cout, Cin, dgrad ? 1 : 0, scratch);
     int e = check_launch("pack_subpix_h3 range");
     if (e) return e;
     const long long pb = cdiv(total, 2048) < 256 ? cdiv(total, 2048) : 256;
-    hipLaunchKernelGGL(subpix_pack_kernel, dim3((unsigned)pb), dim3(256), 0, s, w, Cout, Cin, scratch,
+    hipLaunchKernelGGL(subpix_pack_kernel, dim3((unsigned)pb), dim3(256), 0, s, w, Cout, Cin, dgrad ? 1 : 0, scratch,
                        reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo), wexp);
     return check_launch("pack_subpix_h3");
 }
+
+namespace dcs {
+// conv.hip's dcs_conv_wgrad: d describes the forward up-convolution (parity 2, the rows pass's form)
+bool subpix_wgrad_check(const dcs_conv_desc& d) {
+    return (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.parity == 2 && d.up == 1 && d.stride == 1 &&
+           d.KH == 3 && d.KW == 3 && d.pad_mode == DCS_PAD_ZERO && d.pt == 1 && d.pl == 1 && d.Ho == 2 * d.Hs &&
+           d.Wo == 2 * d.Ws && d.Cs % 64 == 0 && d.Co % 32 == 0 && d.Ws % SW_SW == 0 && d.Hs >= 1 && d.s_c == 1 &&
+           d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs && d.s_n == (long long)d.Hs * d.Ws * d.Cs &&
+           d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) && d.pro_act == DCS_ACT_NONE && d.rng_a && d.rng_b &&
+           d.rng_a_n > 0 && d.rng_a_n <= 1024 && d.rng_b_n > 0 && d.rng_b_n <= 1024 &&
+           (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+           (long long)d.N * d.Ho * d.Wo * d.Co * 4 < 0x7fffff00LL - 64;
+}
+
+size_t subpix_wgrad_workspace_size(const dcs_conv_desc& d) {
+    const SWPlan p = sw_plan(d);
+    return (size_t)p.nsplit * 4 * d.Co * 4 * d.Cs * sizeof(float);
+}
+
+// partial slabs into ws (subpix_wgrad_workspace_size bytes, wgrad_subpixel_fold_kernel's layout); returns the
+// split count (< 0: error).  rng_a: dy's range record, rng_b: the source's.
+int subpix_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s) {
+    const SWPlan p = sw_plan(d);
+    SWArgs a;
+    a.N = d.N; a.H = d.Hs; a.W = d.Ws; a.C = d.Cs; a.Co = d.Co;
+    a.strips = p.strips; a.rchunks = p.rchunks; a.rows_per = p.rows_per;
+    a.gco = d.Co / 32; a.gci = d.Cs / 64;
+    a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n;
+    const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
+    if (d.mma == DCS_MMA_F16)
+        hipLaunchKernelGGL(subpix_wgrad_kernel<1>, dim3(blocks), dim3(SW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    else
+        hipLaunchKernelGGL(subpix_wgrad_kernel<3>, dim3(blocks), dim3(SW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    const int e = check_launch("subpix_wgrad");
+    return e ? -e : p.nsplit;
+}
+}  // namespace dcs

@@ -78,7 +78,9 @@ SIGNATURES = {
     "dcs_conv3_win_in_stats": (c_int, [DP, P, P, P, P, P, P, c_size_t, P, P]),
     "dcs_pack_split_h3": (c_int, [P, c_int, c_int, P, c_int, P, P]),
     "dcs_pack_plan": (c_int, [P, c_int, POINTER(c_int), POINTER(c_int)]),
-    "dcs_pack_subpix_h3": (c_int, [P, c_int, c_int, P, P, P, P, P]),
+    "dcs_pack_subpix_h3": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
+    "dcs_subpix_win_dgrad_ok": (c_int, [DP]),
+    "dcs_subpix_win_dgrad": (c_int, [DP, P, P, P, P, P, P]),
     "dcs_subpix_win_ok": (c_int, [DP]),
     "dcs_subpix_win_parts_size": (c_size_t, [DP]),
     "dcs_subpix_win": (c_int, [DP, P, P, P, P, P, P, c_size_t, POINTER(c_int), P]),

@@ -35,6 +35,7 @@ _BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"  # pre-split fp16 weight plane
 _STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)
 _PREPACK = os.environ.get("DUCOSY_PREPACK", "1") == "1"  # the step's weight packs in two batched launches
 _SUBWIN = os.environ.get("DUCOSY_SUBWIN", "1") == "1"  # up-conv forwards on the sub-pixel window kernel
+_SUBWIN_D = os.environ.get("DUCOSY_SUBWIN_DGRAD", "1") == "1"  # (diagnostic: their data gradients too)
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -478,15 +479,18 @@ class ConvGeom:
         the pre-split phase weights (_dcs_sp) next to the rows pass's kind-3 pack."""
         return _SUBWIN and _h3() and self.subpixel and self.cout % 64 == 0 and self.cin % 16 == 0
 
-    def _attach_sp(self, wpack: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        hi = torch.empty(4 * self.cout, 4 * self.cin, device=w.device, dtype=torch.float16)
+    def _attach_sp(self, wpack: torch.Tensor, w: torch.Tensor, dgrad: int = 0) -> torch.Tensor:
+        shape = (self.cin, 16 * self.cout) if dgrad else (4 * self.cout, 4 * self.cin)
+        hi = torch.empty(*shape, device=w.device, dtype=torch.float16)
         lo = torch.empty_like(hi)
         wexp = torch.empty(1, device=w.device, dtype=torch.int32)
         scratch = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
         if _BATCH is not None:
-            _BATCH.add(w, h3=2, Cout=self.cout, Cin=self.cin, h3_hi=hi, h3_lo=lo, h3_wexp=wexp, h3_scratch=scratch)
+            _BATCH.add(w, h3=2, Cout=self.cout, Cin=self.cin, h3_flip=dgrad, h3_hi=hi, h3_lo=lo, h3_wexp=wexp,
+                       h3_scratch=scratch)
         else:
-            lib.call("dcs_pack_subpix_h3", _p(w), self.cout, self.cin, _p(hi), _p(lo), _p(scratch), _p(wexp), _stream())
+            lib.call("dcs_pack_subpix_h3", _p(w), self.cout, self.cin, dgrad, _p(hi), _p(lo), _p(scratch), _p(wexp),
+                     _stream())
         wpack._dcs_sp = (hi, lo, wexp)
         return wpack
 
@@ -541,7 +545,8 @@ class ConvGeom:
         if self.to1_dgrad(ci):  # un-flipped taps, K-major: [(ty*K+tx)*cout + co] = w[co][0][ty][tx]
             return self._pack(w, 2, 1, self.k * self.k * self.cout, 1)
         if self.subpixel and ci > 4:
-            return self._pack(w, 4, ci, 16 * self.cout, ci)
+            out = self._pack(w, 4, ci, 16 * self.cout, ci)
+            return self._attach_sp(out, w, 1) if (self.subwin and _SUBWIN_D and ci == self.cin and ci % 128 == 0) else out
         kind = 2 if self.stride == 2 else 1
         K = self.k * self.k * self.cout
         out = self._pack(w, kind, ci, K, ci)
@@ -693,6 +698,17 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
+    def _subpix_dgrad(self, d, dy: torch.Tensor, sp, out: torch.Tensor) -> bool:
+        """The up-conv data gradient on the sub-pixel window kernel (f16x3 in both fp16 modes, as the
+        forward); False where the descriptor is not one it covers (the rows pass runs it)."""
+        mma = d.mma
+        d.mma = lib.MMA_F16X3
+        if not lib.query("dcs_subpix_win_dgrad_ok", ctypes.byref(d)):
+            d.mma = mma
+            return False
+        lib.call("dcs_subpix_win_dgrad", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _stream())
+        return True
+
     def _win_in_stats(self, s: Src, d, h3, nb, want_max):
         """Forward + IN statistics on the f16x3 window kernel (csrc/conv_win.hip)."""
         dev = s.t.device
@@ -805,7 +821,9 @@ class ConvGeom:
             d.stride, d.parity, d.pt, d.pl = 2, 0, 1, 1
             d.Ho, d.Wo = H, W
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
-            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out), _stream())
+            sp = getattr(wpack_d, "_dcs_sp", None)
+            if sp is None or narrow or not self._subpix_dgrad(d, dy, sp, out):
+                lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out), _stream())
             if addend is not None:
                 lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
             return out
@@ -930,6 +948,8 @@ class ConvGeom:
             d.mma = m0
         if not self.narrow and s.t2 is None and _h3() and s.t.is_contiguous():
             _set_mma(d, dy, None, range_rec(s.t, pro))
+            if self.subwin:  # the up-convs on f16x3 operands in both fp16 modes, as their forward (_subpix)
+                d.mma = lib.MMA_F16X3
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
             d.cw = self.cin
         assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)

@@ -91,6 +91,12 @@ def main():
         wd = g.pack_dgrad(w)
         t = timeit(lambda: g.dgrad(dy, wd, H, H), a.reps)
         print(f"{name:8s} {'dgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
+        sp = getattr(wd, "_dcs_sp", None)
+        if sp is not None:  # the up-convs: the rows pass the sub-pixel window kernel replaces
+            del wd._dcs_sp
+            t = timeit(lambda: g.dgrad(dy, wd, H, H), a.reps)
+            wd._dcs_sp = sp
+            print(f"{name:8s} {'dgrow':6s} {t:9.3f} {flop / t / 1e9:9.1f}")
         t = timeit(lambda: g.wgrad(dy, Src.nhwc(x), pro=p, pro_max=pm), a.reps)
         print(f"{name:8s} {'wgrad':6s} {t:9.3f} {flop / t / 1e9:9.1f}", flush=True)
         if name == "head" and pro:  # the data gradient with the IN + ReLU backward of its input

@@ -6,7 +6,11 @@ the same fp32 operands:
     (every tile width the kernel takes: 16, 32, 64, 128 and two column strips);
   * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in both fp16
     modes (the host runs the kernel on f16x3 operands in f16 mode too);
-  * the rows pass on the same pack (the phase planes removed) agrees to the same bound, and the
+  * the data gradient (per phase a 2x2 conv of dy's phase sub-grid with the transposed phase weights)
+    against float64 autograd of upsample + conv, to the same bound;
+  * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
+    against float64 autograd, to the same bound;
+  * the rows pass on the same pack (the phase planes removed) agrees to its own bound, and the
     batched pack (ops.prepack) equals the per-pack launches bit for bit.
 Tolerances written per check below."""
 import pytest
@@ -75,13 +79,61 @@ def test_subpix_forward_and_stats_vs_fp64(ops, mode, tol, cin, cout, N, H, W):
     assert _relmax(y0.permute(0, 3, 1, 2), ref) <= (tol if mode == "f16x3" else 2e-3)  # rows pass: fp16 operands
 
 
-def test_subpix_pack_batched_bit_identical(ops):
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("cin,cout,N,H,W", [(256, 128, 2, 16, 16), (256, 128, 1, 8, 32), (128, 64, 2, 8, 64),
+                                            (128, 64, 1, 2, 256)])
+def test_subpix_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
+    """dL/dx of the up-conv (the adjoint of upsample + conv) from dy, against float64 autograd; the rows
+    pass over the same pack (phase planes removed) to its own bound."""
+    ops.set_mma(mode)
+    g = _geom(ops, cin, cout)
+    x = rnd((N, cin, H, W), 84, "x").double().requires_grad_(True)
+    w = torch.from_numpy(prng.normal(85, "w", (cout, cin, 3, 3), 0, 0.05)).float().double()
+    dy = rnd((N, cout, 2 * H, 2 * W), 86, "dy").double()
+    y = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, padding=1)
+    (ref,) = torch.autograd.grad(y, x, dy)
+    dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wd = g.pack_dgrad(w.float().to(DEV))
+    assert getattr(wd, "_dcs_sp", None) is not None
+    dx = g.dgrad(dyd, wd, H, W)
+    assert _relmax(dx.permute(0, 3, 1, 2), ref) <= 1e-5
+    assert torch.equal(g.dgrad(dyd, wd, H, W), dx)  # deterministic
+    sp = wd._dcs_sp
+    del wd._dcs_sp
+    try:
+        dx0 = g.dgrad(dyd, wd, H, W)
+    finally:
+        wd._dcs_sp = sp
+    assert _relmax(dx0.permute(0, 3, 1, 2), ref) <= (1e-5 if mode == "f16x3" else 2e-3)  # rows pass
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("cin,cout,N,H,W", [(256, 128, 2, 8, 64), (128, 64, 1, 17, 128), (128, 64, 1, 2, 256)])
+def test_subpix_wgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
+    """dL/dW of the up-conv (the phase weight gradients folded onto the 3x3 taps) against float64
+    autograd; strips of 64 source columns (the window kernel), row chunks not dividing H included."""
+    ops.set_mma(mode)
+    g = _geom(ops, cin, cout)
+    x = rnd((N, cin, H, W), 87, "x").double()
+    w = torch.from_numpy(prng.normal(88, "w", (cout, cin, 3, 3), 0, 0.05)).float().double().requires_grad_(True)
+    dy = rnd((N, cout, 2 * H, 2 * W), 89, "dy").double()
+    y = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, padding=1)
+    (ref,) = torch.autograd.grad(y, w, dy)
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dw = g.wgrad(dyd, ops.Src.nhwc(xd))
+    assert _relmax(dw, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_subpix_pack_batched_bit_identical(ops, dgrad):
     ops.set_mma("f16x3")
     g = _geom(ops, 256, 128)
     w = (rnd((128, 256, 3, 3), 83, "w") * 0.05).float().to(DEV)
-    sp = [a.clone() for a in g.pack_fwd(w)._dcs_sp]
+    pack = g.pack_dgrad if dgrad else g.pack_fwd
+    sp = [a.clone() for a in pack(w)._dcs_sp]
     w.mul_(1.0)
     ops.prepack([w])
-    got = g.pack_fwd(w)._dcs_sp
+    got = pack(w)._dcs_sp
     for a, b in zip(got, sp):
         assert torch.equal(a, b)

@@ -166,37 +166,53 @@ def test_pack_cache_follows_weight_updates():
 
 def test_explicit_step_matches_autograd_step():
     """CycleGANSystem's explicit step schedule (fused loss launch, direct backward calls) equals the
-    autograd step over the same kernels: loss values and every parameter after two steps."""
+    autograd step over the same kernels: loss values of each step and the parameters after it.
+
+    Each step starts both schedules from the same state: after a step the explicit system's
+    parameters and Adam moments are copied into the autograd system.  (Carried across steps, the
+    schedules' last-bit gradient differences flip Adam's first, sign-like update of entries whose
+    gradient is near zero, by 2 lr each; the edge / region top-k selections and the CBAM max-pool
+    then turn a few such flips into percent-level differences of the next step's gradient, which
+    says nothing about either schedule.)"""
     from modules import trainer
+    from modules.hip import ops
     n, hw, nb, cin, seed = 2, 64, 1, 3, 611
     seeds = prng.step_model_seeds(seed)
-    res = {}
-    for mode in (False, True):
-        prev = trainer._EXPLICIT_STEP
-        trainer._EXPLICIT_STEP = mode
-        try:
-            s = _system(cin, nb, seeds)
-            outs = []
-            for i in range(2):
-                rA = torch.from_numpy(prng.uniform(seed, f"A{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
-                rB = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
-                mk = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, hw, hw), 0.3)).to(DEV)
-                outs.append({k: float(v) for k, v in s.train_step(rA, rB, mk).items()})
-            params = {f"{t}.{k}": p.detach().clone() for t, m in zip(("GA", "GB", "DA", "DB"), s.models)
-                      for k, p in m.named_parameters()}
-            res[mode] = (outs, params)
-        finally:
-            trainer._EXPLICIT_STEP = prev
-    (oa, pa), (oe, pe) = res[False], res[True]
-    for i in range(2):
-        for k in oa[i]:
-            assert abs(oe[i][k] - oa[i][k]) <= 1e-5 * max(abs(oa[i][k]), 1e-2), (i, k, oe[i][k], oa[i][k])
-    # Adam's first updates are ~lr * sign(g): an entry whose gradient is decided by rounding may
-    # move the other way, so the typical entry must agree and every entry stay within 2 lr / step
-    lr = 2e-4
-    for k in pa:
-        d = (pe[k] - pa[k]).abs().flatten()
-        assert d.median().item() <= 1e-6 and d.max().item() <= 2 * lr * 2 + 1e-6, (k, d.max().item())
+    systems = {}
+    prev = trainer._EXPLICIT_STEP
+    try:
+        for mode in (False, True):
+            trainer._EXPLICIT_STEP = mode
+            systems[mode] = _system(cin, nb, seeds)
+        lr = 2e-4
+        for i in range(2):
+            rA = torch.from_numpy(prng.uniform(seed, f"A{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+            rB = torch.from_numpy(prng.uniform(seed, f"B{i}", (n, 1, hw, hw), -1, 1)).to(DEV)
+            mk = torch.from_numpy(prng.bernoulli(seed, f"M{i}", (n, cin - 1, hw, hw), 0.3)).to(DEV)
+            outs, params = {}, {}
+            for mode in (False, True):
+                trainer._EXPLICIT_STEP = mode
+                s = systems[mode]
+                outs[mode] = {k: float(v) for k, v in s.train_step(rA, rB, mk).items()}
+                params[mode] = {f"{t}.{k}": p.detach().clone() for t, m in zip(("GA", "GB", "DA", "DB"), s.models)
+                                for k, p in m.named_parameters()}
+            oa, oe = outs[False], outs[True]
+            for k in oa:
+                assert abs(oe[k] - oa[k]) <= 1e-5 * max(abs(oa[k]), 1e-2), (i, k, oe[k], oa[k])
+            # Adam's first updates are ~lr * sign(g): an entry whose gradient is decided by rounding may
+            # move the other way, so the typical entry must agree and every entry stay within 2 lr
+            pa, pe = params[False], params[True]
+            for k in pa:
+                d = (pe[k] - pa[k]).abs().flatten()
+                assert d.median().item() <= 1e-6 and d.max().item() <= 2 * lr + 1e-6, (i, k, d.max().item())
+            # the next step from the explicit schedule's state in both
+            for oa_, oe_ in zip(systems[False].optimizers, systems[True].optimizers):
+                oa_.flat_p.copy_(oe_.flat_p)
+                oa_.flat_m.copy_(oe_.flat_m)
+                oa_.flat_v.copy_(oe_.flat_v)
+            ops.bump_weights_epoch()  # parameters written through the flat buffers
+    finally:
+        trainer._EXPLICIT_STEP = prev
 
 
 
