@@ -2314,7 +2314,7 @@ __global__ __launch_bounds__(256) void pack_batch1_kernel(const dcs_pack_job* __
     float* rng;
     if (jb.h3 == 2) {  // sub-pixel phase weights: the range of the combined values
         const long long n = 16LL * jb.Cout * jb.Cin;
-        const int K = jb.h3_flip ? 16 * jb.Cout : 4 * jb.Cin;
+        const int K = subpix_K(jb.Cout, jb.Cin, jb.h3_flip);
         for (long long i = (long long)lb * 256 + threadIdx.x; i < n; i += (long long)nb * 256) {
             const int v = (int)(i / K);
             m = fmaxf(m, fabsf(subpix_value(jb.w, jb.Cout, jb.Cin, jb.h3_flip, v, (int)(i - (long long)v * K))));
@@ -2355,7 +2355,7 @@ __global__ __launch_bounds__(256) void pack_batch2_kernel(const dcs_pack_job* __
         const float sc = __builtin_ldexpf(1.f, e);
         if (lb == 0 && threadIdx.x == 0) jb.h3_wexp[0] = e;
         const long long total = 16LL * jb.Cout * jb.Cin;
-        const int K = jb.h3_flip ? 16 * jb.Cout : 4 * jb.Cin;
+        const int K = subpix_K(jb.Cout, jb.Cin, jb.h3_flip);
         _Float16* oh = reinterpret_cast<_Float16*>(jb.h3_hi);
         _Float16* ol = reinterpret_cast<_Float16*>(jb.h3_lo);
         for (long long i = (long long)lb * 256 + threadIdx.x; i < total; i += (long long)nb * 256) {
@@ -2417,11 +2417,8 @@ extern "C" int dcs_pack_plan(dcs_pack_job* jobs, int njobs, int* g1, int* g2) {
         if (!jb.w) return fail(DCS_E_INVALID, "pack_plan: job without weights");
         long long n1, n2 = 0, cap2 = 1;
         if (jb.h3 == 2) {
-            if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || jb.Cout <= 0 || jb.Cin <= 0 ||
-                jb.Cout % 64 || jb.Cin % 16 || 16LL * jb.Cout * jb.Cin >= (1LL << 30) ||
-                (jb.h3_flip && jb.Cin % 128))
-                return fail(DCS_E_INVALID, "pack_plan: sub-pixel job (Cout % 64 == 0, Cin % 16 == 0; data gradient: "
-                                           "Cin % 128 == 0)");
+            if (!jb.h3_hi || !jb.h3_lo || !jb.h3_wexp || !jb.h3_scratch || !subpix_pack_ok(jb.Cout, jb.Cin, jb.h3_flip))
+                return fail(DCS_E_INVALID, "pack_plan: window phase-kernel job (dcs_pack_subpix_h3's shape rules)");
             n1 = n2 = cdiv(16LL * jb.Cout * jb.Cin, 2048);  // dcs_pack_subpix_h3's launches
             cap2 = 256;
         } else if (jb.h3) {

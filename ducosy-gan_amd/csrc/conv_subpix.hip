@@ -51,8 +51,12 @@ __device__ __forceinline__ int sp_boff(int buf, int pl, int tap, int row, int h)
     return ((buf * 2 + pl) * 4 + tap) * SP_SLOT + row * 16 + 8 * (h ^ ((row >> 3) & 1));
 }
 
-// NP 3: f16x3 (lo*hi + hi*lo + hi*hi), 1: f16 (hi planes only); MODE 0: forward, 1: data gradient
-template <int NP, int MODE>
+// NP 3: f16x3 (lo*hi + hi*lo + hi*hi), 1: f16 (hi planes only); MODE 0: phases over the output columns
+// (sub-pixel forward; S2: the stride-2 data gradient), MODE 1: phases over k (sub-pixel data gradient;
+// S2: the stride-2 forward).  S2 kernels skip the (phase, offset) pairs no 3x3 tap reaches (weights 0).
+// PXC >= 0: the launch covers the column tiles of column phase PXC only (the stride-2 data gradient runs
+// one launch per phase, so the phase's skipped column offset is known at compile time)
+template <int NP, int MODE, int S2, int PXC = -1>
 __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const float* __restrict__ src,
                                                               const _Float16* __restrict__ wh,
                                                               const _Float16* __restrict__ wl,
@@ -64,7 +68,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     _Float16* const Bs = smem + 2 * 2 * SP_PIX * 16;
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int ntile = L % a.gy, mt = L / a.gy;
+    const int gyl = PXC >= 0 ? a.cblk : a.gy;
+    const int ntile = (PXC >= 0 ? PXC * a.cblk : 0) + L % gyl, mt = L / gyl;
     const int n = mt / a.tiles, tile = mt - n * a.tiles;
     const int tyi = tile / a.tiles_x, txi = tile - tyi * a.tiles_x;
     const int y0 = tyi * a.R, x0 = txi * a.TW;
@@ -205,6 +210,18 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 #pragma unroll
         for (int tap = 0; tap < 4; ++tap) {
             const int u = tap >> 1, tx = tap & 1;
+            // S2: the pairs no tap reaches (wave-uniform: py per wave, px per workgroup, the class per
+            // iteration)
+            bool skip_row = false, skip_col = false;
+            if constexpr (S2 && MODE == 0) {
+                skip_row = py == 0 && u == 0;
+                skip_col = PXC == 0 && tx == 0;  // (both runtime: the allocator spills)
+            } else if constexpr (S2) {
+                const int ph = s / nslice;
+                skip_row = (ph >> 1) == 0 && u == 1;
+                skip_col = (ph & 1) == 0 && tx == 1;
+            }
+            if (skip_row) continue;
             f16x8 ah[2], al[2], bh[2], bl_[2];
             if (tx == 0) {  // fragments of window pixels wbe + u * WP + 0 .. 2 (block i, offset t: f = t + i)
 #pragma unroll
@@ -214,6 +231,7 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                     if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 1, wpix, kh));
                 }
             }
+            if (skip_col) continue;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 ah[i] = fh[tx + i];
@@ -250,31 +268,18 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             }
     }
 
+    // epilogue: undo the operand scales, NHWC store, IN statistics.  MODE 0: the phase's pixels of the
+    // 2 Hs x 2 Ws output, channels co0 + j * 32 + lane; MODE 1: the Hs x Ws output, channels n0 + py * 64 + ...
     const int eab = -(ea + eb);
-    if constexpr (MODE == 1) {  // dx NHWC store
-        const long long obase = (long long)n * a.Hs * a.Ws * a.Co;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
-                    const int qy = q / TW;
-                    const long long pix = (long long)(y0 + qy) * a.Ws + x0 + q - qy * TW;
-                    out[obase + pix * a.Co + n0 + py * 64 + j * 32 + l32] = __builtin_ldexpf(acc[i][j][r], eab);
-                }
-        return;
-    }
-    // epilogue: undo the operand scales, NHWC store of the phase's pixels, IN statistics
-    const int Wo = 2 * a.Ws;
+    const int Wo = MODE == 0 ? 2 * a.Ws : a.Ws;
     auto opix = [&](int i, int r) {  // output pixel index within the image (increasing along r, then i)
         const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
         const int qy = q / TW;
-        return (2 * (y0 + qy) + py) * Wo + 2 * (x0 + q - qy * TW) + px;
+        if constexpr (MODE == 0) return (2 * (y0 + qy) + py) * Wo + 2 * (x0 + q - qy * TW) + px;
+        else return (y0 + qy) * Wo + x0 + q - qy * TW;
     };
-    const long long obase = (long long)n * (2 * a.Hs) * Wo * a.Co;
-    const int co0 = cb * 64;
+    const long long obase = (long long)n * (MODE == 0 ? 4LL : 1LL) * a.Hs * a.Ws * a.Co;
+    const int co0 = MODE == 0 ? cb * 64 : n0 + py * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -336,22 +341,26 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             p.cnt = tot;
             if (b.mx > p.mx || (b.mx == p.mx && b.amax < p.amax)) { p.mx = b.mx; p.amax = b.amax; }
         }
-        const int nchunk = 4 * a.tiles;
-        const int chunk = tile * 4 + px * 2 + (tid >> 6);
-        parts[((long long)n * nchunk + chunk) * a.Co + co0 + (tid & 63)] = p;
+        if constexpr (MODE == 0) {
+            const int nchunk = 4 * a.tiles;
+            const int chunk = tile * 4 + px * 2 + (tid >> 6);
+            parts[((long long)n * nchunk + chunk) * a.Co + co0 + (tid & 63)] = p;
+        } else {
+            parts[((long long)n * a.tiles + tile) * a.Co + n0 + tid] = p;
+        }
     }
 }
 
 // sub-pixel B pack: the range of the combined weights, then every block derives the exponent and
 // writes the hi / lo planes ([4 Cout][4 Cin] forward, [Cin][16 Cout] data gradient)
-__global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+__global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restrict__ w, int Cout, int Cin, int kind,
                                                            float* __restrict__ parts) {
     const long long total = 16LL * Cout * Cin;
-    const int K = dgrad ? 16 * Cout : 4 * Cin;
+    const int K = subpix_K(Cout, Cin, kind);
     float m = 0.f;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         const int v = (int)(i / K);
-        m = fmaxf(m, fabsf(subpix_value(w, Cout, Cin, dgrad, v, (int)(i - (long long)v * K))));
+        m = fmaxf(m, fabsf(subpix_value(w, Cout, Cin, kind, v, (int)(i - (long long)v * K))));
     }
     __shared__ float red[4];
     m = wave_max(m);
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(256) void subpix_range_kernel(const float* __restri
         for (int i = gridDim.x + threadIdx.x; i < DCS_RANGE_PARTS; i += blockDim.x) parts[i] = 0.f;
 }
 
-__global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+__global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int kind,
                                                           const float* __restrict__ parts,
                                                           _Float16* __restrict__ oh, _Float16* __restrict__ ol,
                                                           int* __restrict__ wexp) {
@@ -370,10 +379,10 @@ __global__ __launch_bounds__(256) void subpix_pack_kernel(const float* __restric
     const float sc = __builtin_ldexpf(1.f, e);
     if (blockIdx.x == 0 && threadIdx.x == 0) wexp[0] = e;
     const long long total = 16LL * Cout * Cin;
-    const int K = dgrad ? 16 * Cout : 4 * Cin;
+    const int K = subpix_K(Cout, Cin, kind);
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         const int v = (int)(i / K);
-        const float f = subpix_value(w, Cout, Cin, dgrad, v, (int)(i - (long long)v * K)) * sc;
+        const float f = subpix_value(w, Cout, Cin, kind, v, (int)(i - (long long)v * K)) * sc;
         const _Float16 h = (_Float16)f;
         oh[i] = h;
         ol[i] = (_Float16)(f - (float)h);
@@ -661,6 +670,31 @@ bool subpix_dgrad_geom(const dcs_conv_desc& d, SubArgs* a) {
     return true;
 }
 
+// the down-convolutions (stride-2 3x3 zero-pad-1, the rows pass's descriptors): forward (parity 0, source
+// [N][Hs][Ws][Cs] with Hs = 2 Ho) on the class kernel (MODE 1), data gradient (parity 1, dy [N][Hs][Ws][Cs]
+// onto dx [N][2 Hs][2 Ws][Co]) on the phase kernel (MODE 0)
+bool s2_geom(const dcs_conv_desc& d, SubArgs* a) {
+    const bool common = d.up == 1 && d.stride == 2 && d.KH == 3 && d.KW == 3 && d.pad_mode == DCS_PAD_ZERO &&
+                        d.pt == 1 && d.pl == 1 && d.N > 0 && d.Hs > 0 && d.Ws > 0 && d.Cs % 16 == 0 && d.Cs > 0 &&
+                        d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+                        d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                        d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
+                        d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+                        d.Co > 0 && 16LL * d.Co * d.Cs < (1LL << 30);
+    if (!common) return false;
+    if (d.parity == 0) {  // forward
+        if (d.Hs != 2 * d.Ho || d.Ws != 2 * d.Wo || d.Co % 128 || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
+        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
+        return true;
+    }
+    if (d.parity == 1) {  // data gradient
+        if (d.Ho != 2 * d.Hs || d.Wo != 2 * d.Ws || d.Co % 64 || !tile_geom(d.N, d.Hs, d.Ws, a)) return false;
+        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
+        return true;
+    }
+    return false;
+}
+
 }  // namespace
 }  // namespace dcs
 
@@ -692,10 +726,10 @@ extern "C" int dcs_subpix_win(const dcs_conv_desc* dp, const float* src, const v
     const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
-        hipLaunchKernelGGL((subpix_win_kernel<1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
+        hipLaunchKernelGGL((subpix_win_kernel<1, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
                            out, reinterpret_cast<Part*>(parts));
     else
-        hipLaunchKernelGGL((subpix_win_kernel<3, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
+        hipLaunchKernelGGL((subpix_win_kernel<3, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
                            out, reinterpret_cast<Part*>(parts));
     return check_launch("subpix_win");
 }
@@ -716,28 +750,27 @@ extern "C" int dcs_subpix_win_dgrad(const dcs_conv_desc* dp, const float* dy, co
     const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
-        hipLaunchKernelGGL((subpix_win_kernel<1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
+        hipLaunchKernelGGL((subpix_win_kernel<1, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
                            nullptr);
     else
-        hipLaunchKernelGGL((subpix_win_kernel<3, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
+        hipLaunchKernelGGL((subpix_win_kernel<3, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
                            nullptr);
     return check_launch("subpix_win_dgrad");
 }
 
-extern "C" int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, int dgrad, void* out_hi, void* out_lo,
+extern "C" int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, int kind, void* out_hi, void* out_lo,
                                   float* scratch, int* wexp, void* stream) {
-    if (!w || !out_hi || !out_lo || !scratch || !wexp || Cout <= 0 || Cin <= 0 || Cout % 64 || Cin % 16 ||
-        16LL * Cout * Cin >= (1LL << 30) || (dgrad && (Cout % 16 || Cin % 128)))
-        return fail(DCS_E_INVALID, "pack_subpix_h3: bad arguments (Cout % 64 == 0, Cin % 16 == 0; data gradient: "
-                                   "Cin % 128 == 0)");
+    if (!w || !out_hi || !out_lo || !scratch || !wexp || !subpix_pack_ok(Cout, Cin, kind))
+        return fail(DCS_E_INVALID, "pack_subpix_h3: bad arguments (kind 0: Cout % 64, Cin % 16; 1: Cout % 16, "
+                                   "Cin % 128; 2: Cin % 64, Cout % 16; 3: Cout % 128, Cin % 16)");
     hipStream_t s = as_stream(stream);
     const long long total = 16LL * Cout * Cin;
     const long long rb = cdiv(total, 2048) < DCS_RANGE_PARTS ? cdiv(total, 2048) : DCS_RANGE_PARTS;
-    hipLaunchKernelGGL(subpix_range_kernel, dim3((unsigned)rb), dim3(256), 0, s, w, Cout, Cin, dgrad ? 1 : 0, scratch);
+    hipLaunchKernelGGL(subpix_range_kernel, dim3((unsigned)rb), dim3(256), 0, s, w, Cout, Cin, kind, scratch);
     int e = check_launch("pack_subpix_h3 range");
     if (e) return e;
     const long long pb = cdiv(total, 2048) < 256 ? cdiv(total, 2048) : 256;
-    hipLaunchKernelGGL(subpix_pack_kernel, dim3((unsigned)pb), dim3(256), 0, s, w, Cout, Cin, dgrad ? 1 : 0, scratch,
+    hipLaunchKernelGGL(subpix_pack_kernel, dim3((unsigned)pb), dim3(256), 0, s, w, Cout, Cin, kind, scratch,
                        reinterpret_cast<_Float16*>(out_hi), reinterpret_cast<_Float16*>(out_lo), wexp);
     return check_launch("pack_subpix_h3");
 }
@@ -778,3 +811,47 @@ int subpix_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x,
     return e ? -e : p.nsplit;
 }
 }  // namespace dcs
+
+extern "C" int dcs_stride2_win_ok(const dcs_conv_desc* dp) { return dp && s2_geom(*dp, nullptr) ? 1 : 0; }
+
+extern "C" size_t dcs_stride2_win_parts_size(const dcs_conv_desc* dp) {
+    SubArgs a;
+    if (!dp || dp->parity != 0 || !s2_geom(*dp, &a)) return 0;
+    return (size_t)a.N * a.tiles * a.Co * sizeof(Part);
+}
+
+extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
+                               const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
+    if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "stride2_win: null pointer");
+    SubArgs a;
+    if (!s2_geom(*dp, &a))
+        return fail(DCS_E_INVALID, "stride2_win: needs a stride-2 3x3 zero-pad-1 rows descriptor over contiguous NHWC "
+                                   "(parity 0: forward, Co % 128 == 0; parity 1: data gradient, Co % 64 == 0), "
+                                   "Cs % 16 == 0, the low-resolution grid tileable (min(W, 128) dividing 256 and W), "
+                                   "f16x3 / f16 with the source range record");
+    if (parts) {
+        if (dp->parity != 0 || !nchunk || parts_bytes < dcs_stride2_win_parts_size(dp))
+            return fail(DCS_E_WORKSPACE, "stride2_win: statistics only for the forward, parts buffer too small");
+        *nchunk = a.tiles;
+    }
+    const unsigned blocks = (unsigned)((long long)a.N * a.tiles * a.gy);
+    hipStream_t s = as_stream(stream);
+    const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
+    const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
+    Part* pp = reinterpret_cast<Part*>(parts);
+    const bool f16 = dp->mma == DCS_MMA_F16;
+    if (dp->parity == 0) {
+        if (f16) hipLaunchKernelGGL((subpix_win_kernel<1, 1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, pp);
+        else hipLaunchKernelGGL((subpix_win_kernel<3, 1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, pp);
+    } else {  // one launch per column phase
+        const dim3 g2(blocks / 2);
+        if (f16) {
+            hipLaunchKernelGGL((subpix_win_kernel<1, 0, 1, 0>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+            hipLaunchKernelGGL((subpix_win_kernel<1, 0, 1, 1>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+        } else {
+            hipLaunchKernelGGL((subpix_win_kernel<3, 0, 1, 0>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+            hipLaunchKernelGGL((subpix_win_kernel<3, 0, 1, 1>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+        }
+    }
+    return check_launch("stride2_win");
+}

@@ -36,6 +36,7 @@ _STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its M
 _PREPACK = os.environ.get("DUCOSY_PREPACK", "1") == "1"  # the step's weight packs in two batched launches
 _SUBWIN = os.environ.get("DUCOSY_SUBWIN", "1") == "1"  # up-conv forwards on the sub-pixel window kernel
 _SUBWIN_D = os.environ.get("DUCOSY_SUBWIN_DGRAD", "1") == "1"  # (diagnostic: their data gradients too)
+_S2WIN = os.environ.get("DUCOSY_S2WIN", "1") == "1"  # the down-convs on the same window phase kernels
 
 
 # residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
@@ -479,17 +480,28 @@ class ConvGeom:
         the pre-split phase weights (_dcs_sp) next to the rows pass's kind-3 pack."""
         return _SUBWIN and _h3() and self.subpixel and self.cout % 64 == 0 and self.cin % 16 == 0
 
-    def _attach_sp(self, wpack: torch.Tensor, w: torch.Tensor, dgrad: int = 0) -> torch.Tensor:
-        shape = (self.cin, 16 * self.cout) if dgrad else (4 * self.cout, 4 * self.cin)
+    @property
+    def s2win(self) -> bool:
+        """The window phase kernels for this stride-2 3x3 zero-pad-1 conv (the down-convs): forward over
+        the source's parity classes, data gradient over dx's."""
+        return (_SUBWIN and _S2WIN and _h3() and self.stride == 2 and self.k == 3 and self.up == 1 and
+                self.pads == (1, 1, 1, 1) and self.pad_mode == DCS_PAD_ZERO and self.cout % 128 == 0 and
+                self.cin % 64 == 0)
+
+    def _attach_sp(self, wpack: torch.Tensor, w: torch.Tensor, kind: int = 0) -> torch.Tensor:
+        """Pre-split planes of the window phase kernels (dcs_pack_subpix_h3 kind: 0 / 1 sub-pixel forward /
+        data gradient, 2 / 3 stride-2 data gradient / forward) on the pack as _dcs_sp."""
+        shape = {0: (4 * self.cout, 4 * self.cin), 1: (self.cin, 16 * self.cout), 2: (4 * self.cin, 4 * self.cout),
+                 3: (self.cout, 16 * self.cin)}[kind]
         hi = torch.empty(*shape, device=w.device, dtype=torch.float16)
         lo = torch.empty_like(hi)
         wexp = torch.empty(1, device=w.device, dtype=torch.int32)
         scratch = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)
         if _BATCH is not None:
-            _BATCH.add(w, h3=2, Cout=self.cout, Cin=self.cin, h3_flip=dgrad, h3_hi=hi, h3_lo=lo, h3_wexp=wexp,
+            _BATCH.add(w, h3=2, Cout=self.cout, Cin=self.cin, h3_flip=kind, h3_hi=hi, h3_lo=lo, h3_wexp=wexp,
                        h3_scratch=scratch)
         else:
-            lib.call("dcs_pack_subpix_h3", _p(w), self.cout, self.cin, dgrad, _p(hi), _p(lo), _p(scratch), _p(wexp),
+            lib.call("dcs_pack_subpix_h3", _p(w), self.cout, self.cin, kind, _p(hi), _p(lo), _p(scratch), _p(wexp),
                      _stream())
         wpack._dcs_sp = (hi, lo, wexp)
         return wpack
@@ -520,6 +532,8 @@ class ConvGeom:
             return self._attach_sp(out, w) if self.subwin else out
         K = self.k * self.k * self.cin
         out = self._pack(w, 0, self.cin, K, self.cout)
+        if self.s2win:
+            return self._attach_sp(out, w, 3)
         return self._attach_h3(out, w, 0) if self.win else out
 
     @property
@@ -550,6 +564,8 @@ class ConvGeom:
         kind = 2 if self.stride == 2 else 1
         K = self.k * self.k * self.cout
         out = self._pack(w, kind, ci, K, ci)
+        if self.s2win and ci == self.cin:
+            return self._attach_sp(out, w, 2)
         return self._attach_h3(out, w, 1) if (self.win and ci == self.cin) else out
 
     def _pack(self, w, kind, ci_count, K, ncols):
@@ -629,7 +645,7 @@ class ConvGeom:
         if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
             return self._win_in_stats(s, d, h3, nb, want_max)
         sp = getattr(wpack, "_dcs_sp", None)
-        if nb and sp is not None and bias is None and lib.query("dcs_subpix_win_ok", ctypes.byref(d)):
+        if nb and sp is not None and bias is None and self._phase_win_ok(d):
             return self._subpix(s, d, sp, True, want_max)
         if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
@@ -675,17 +691,26 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
+    def _phase_win_ok(self, d) -> bool:
+        """d (a forward descriptor) is one the window phase kernels cover, with f16x3 operands."""
+        mma = d.mma
+        d.mma = lib.MMA_F16X3
+        ok = lib.query("dcs_subpix_win_ok" if self.subpixel else "dcs_stride2_win_ok", ctypes.byref(d))
+        d.mma = mma
+        return bool(ok)
+
     def _subpix(self, s: Src, d, sp, stats: bool, want_max: bool = False):
-        """An up-conv forward (+ the IN statistics of its output when ``stats``) on the sub-pixel window
-        kernel (csrc/conv_subpix.hip); f16x3 operands in both fp16 modes, as the stem and head (the f16
-        step's edge-loss selection sits at its tolerance with fp16 up-convs)."""
+        """An up- or down-conv forward (+ the IN statistics of its output when ``stats``) on the window
+        phase kernels (csrc/conv_subpix.hip); f16x3 operands in both fp16 modes, as the stem and head
+        (the f16 step's edge-loss selection sits at its tolerance with fp16 up-convs)."""
         dev = s.t.device
         d.mma = lib.MMA_F16X3
         Ho, Wo = self.out_hw(s.H, s.W)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
-        parts = workspace(lib.query("dcs_subpix_win_parts_size", ctypes.byref(d)), dev) if stats else None
+        api = "dcs_subpix_win" if self.subpixel else "dcs_stride2_win"
+        parts = workspace(lib.query(api + "_parts_size", ctypes.byref(d)), dev) if stats else None
         nchunk = ctypes.c_int(0)
-        lib.call("dcs_subpix_win", ctypes.byref(d), _p(s.t), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _p(parts),
+        lib.call(api, ctypes.byref(d), _p(s.t), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _p(parts),
                  parts.numel() if stats else 0, ctypes.byref(nchunk), _stream())
         if not stats:
             return out
@@ -698,16 +723,22 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
-    def _subpix_dgrad(self, d, dy: torch.Tensor, sp, out: torch.Tensor) -> bool:
-        """The up-conv data gradient on the sub-pixel window kernel (f16x3 in both fp16 modes, as the
-        forward); False where the descriptor is not one it covers (the rows pass runs it)."""
+    def _phase_win(self, d, dy: torch.Tensor, sp, out: torch.Tensor) -> bool:
+        """An up- or down-conv data gradient on the window phase kernels (csrc/conv_subpix.hip; f16x3 in
+        both fp16 modes, as the forward); False where the descriptor is not one they cover (the rows pass
+        runs it)."""
         mma = d.mma
         d.mma = lib.MMA_F16X3
-        if not lib.query("dcs_subpix_win_dgrad_ok", ctypes.byref(d)):
-            d.mma = mma
-            return False
-        lib.call("dcs_subpix_win_dgrad", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _stream())
-        return True
+        if self.subpixel and lib.query("dcs_subpix_win_dgrad_ok", ctypes.byref(d)):
+            lib.call("dcs_subpix_win_dgrad", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out),
+                     _stream())
+            return True
+        if self.stride == 2 and lib.query("dcs_stride2_win_ok", ctypes.byref(d)):
+            lib.call("dcs_stride2_win", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), None, 0,
+                     None, _stream())
+            return True
+        d.mma = mma
+        return False
 
     def _win_in_stats(self, s: Src, d, h3, nb, want_max):
         """Forward + IN statistics on the f16x3 window kernel (csrc/conv_win.hip)."""
@@ -753,7 +784,7 @@ class ConvGeom:
             if _STEM and bias is None and lib.query("dcs_stem_fwd_ok", ctypes.byref(d)):
                 return self._stem(s, d, wpack, False)
             sp = getattr(wpack, "_dcs_sp", None)
-            if sp is not None and bias is None and lib.query("dcs_subpix_win_ok", ctypes.byref(d)):
+            if sp is not None and bias is None and self._phase_win_ok(d):
                 return self._subpix(s, d, sp, False)
         h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
@@ -822,7 +853,7 @@ class ConvGeom:
             d.Ho, d.Wo = H, W
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
             sp = getattr(wpack_d, "_dcs_sp", None)
-            if sp is None or narrow or not self._subpix_dgrad(d, dy, sp, out):
+            if sp is None or narrow or not self._phase_win(d, dy, sp, out):
                 lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out), _stream())
             if addend is not None:
                 lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
@@ -832,8 +863,10 @@ class ConvGeom:
             d.stride, d.parity, d.pt, d.pl = 2, 1, t, l
             d.Ho, d.Wo = H, W
             out = torch.empty(N, H, W, ci, device=dev, dtype=torch.float32)
-            lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out),
-                     _stream())
+            sp = getattr(wpack_d, "_dcs_sp", None)
+            if sp is None or narrow or not self._phase_win(d, dy, sp, out):
+                lib.call(fn, ctypes.byref(d), _p(dy), None, _p(wpack_d), None, None, None, _p(out),
+                         _stream())
             if addend is not None:
                 lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
             return out

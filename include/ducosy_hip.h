@@ -231,16 +231,19 @@ int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* d, const float* dy, const fl
  * phase, a 64-channel block, both row phases) and stages the source window once per 16-channel slice.
  * dcs_pack_subpix_h3: the phase weights (sums of the 3x3 taps that land on one source pixel) pre-split
  * into hi / lo fp16 planes, scaled by 2^wexp[0] of their own range; scratch: DCS_RANGE_PARTS floats.
- * dgrad = 0: [4 Cout][4 Cin] (row = ((px * Cout / 64 + co / 64) * 2 + py) * 64 + co % 64, k = (c / 16) * 64 +
- * (u * 2 + t) * 16 + c % 16 for source offset (u, t)); Cout % 64 == 0, Cin % 16 == 0.  dgrad = 1: the
+ * kind 0: [4 Cout][4 Cin] (row = ((px * Cout / 64 + co / 64) * 2 + py) * 64 + co % 64, k = (c / 16) * 64 +
+ * (u * 2 + t) * 16 + c % 16 for source offset (u, t)); Cout % 64 == 0, Cin % 16 == 0.  kind 1: the
  * transposed phase weights of the data gradient [Cin][16 Cout] (row = input channel, k = ((py * 2 + px) *
- * Cout / 16 + co / 16) * 64 + ((1 - u) * 2 + (1 - t)) * 16 + co % 16); also Cin % 128 == 0.
+ * Cout / 16 + co / 16) * 64 + ((1 - u) * 2 + (1 - t)) * 16 + co % 16); Cout % 16 == 0, Cin % 128 == 0.
+ * kinds 2 and 3: the stride-2 convolution's taps in kind 0's layout over dx's parity classes (its data
+ * gradient, [4 Cin][4 Cout]; Cin % 64 == 0, Cout % 16 == 0) and in kind 1's layout over the source's
+ * parity classes (its forward, [Cout][16 Cin]; Cout % 128 == 0, Cin % 16 == 0), zero where no tap lands.
  * dcs_subpix_win_ok(d): 1 if d is a sub-pixel rows descriptor (parity 2, as the rows pass takes it:
  * up = 1, Ho = 2 Hs) these kernels cover (contiguous NHWC, Cs % 16 == 0, Co % 64 == 0, min(Ws, 128)
  * dividing 256 and Ws, Hs % (256 / min(Ws, 128)) == 0, f16x3 / f16 with rng_a set, no prologue).
  * dcs_subpix_win: forward (+ IN statistics partials as dcs_conv_rows_in_stats when parts != NULL,
  * dcs_subpix_win_parts_size bytes; *nchunk = 4 x tiles per image). */
-int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, int dgrad, void* out_hi, void* out_lo, float* scratch,
+int dcs_pack_subpix_h3(const float* w, int Cout, int Cin, int kind, void* out_hi, void* out_lo, float* scratch,
                        int* wexp, void* stream);
 int dcs_subpix_win_ok(const dcs_conv_desc* d);
 size_t dcs_subpix_win_parts_size(const dcs_conv_desc* d);
@@ -254,6 +257,17 @@ int dcs_subpix_win(const dcs_conv_desc* d, const float* src, const void* w_hi, c
 int dcs_subpix_win_dgrad_ok(const dcs_conv_desc* d);
 int dcs_subpix_win_dgrad(const dcs_conv_desc* d, const float* dy, const void* w_hi, const void* w_lo, const int* wexp,
                          float* dx, void* stream);
+/* The down-convolutions (stride-2 3x3 zero-pad-1, modules/model.py:100-106) on the same two kernels: the
+ * forward as a sum over the source's four parity classes of <= 2x2 convolutions of the class sub-grids
+ * (the sub-pixel data gradient's kernel; + IN statistics partials when parts != NULL,
+ * dcs_stride2_win_parts_size bytes, *nchunk = tiles per image), the data gradient as four <= 2x2 phase
+ * convolutions of dy onto dx's parity classes (the sub-pixel forward's kernel); the (class, offset) pairs
+ * no tap reaches are skipped.  d: the rows pass's descriptor (parity 0: forward, Hs = 2 Ho, Co % 128 == 0;
+ * parity 1: data gradient, Ho = 2 Hs, Co % 64 == 0), planes from dcs_pack_subpix_h3 kind 3 / 2. */
+int dcs_stride2_win_ok(const dcs_conv_desc* d);
+size_t dcs_stride2_win_parts_size(const dcs_conv_desc* d);
+int dcs_stride2_win(const dcs_conv_desc* d, const float* src, const void* w_hi, const void* w_lo, const int* wexp,
+                    float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream);
 /* The same data gradient dx = da of a layer a = act(InstanceNorm(y)) (the first conv of a residual
  * block, modules/model.py:74-76), with the InstanceNorm backward's partial sums fused: the window
  * epilogue sums g = da * act'(xhat) and g * xhat (xhat = y * scale + shift) per (256-pixel tile,
@@ -433,7 +447,7 @@ int dcs_pack_split_h3(const float* wpack, int rows, int ldb, const float* rng, i
  * A job is either a dcs_pack_weights_r pack (kind >= 0: w, Cout .. nmajor, out, rng as there; planes:
  * optional dcs_pack_split_h3 output of that pack, rows = ncols) or, with h3 = 1, a dcs_pack_weights_h3
  * pack (w, Cout, Cin, h3_flip, h3_ncols, h3_hi, h3_lo, h3_wexp, h3_scratch as there) or, with h3 = 2, a
- * dcs_pack_subpix_h3 pack (w, Cout, Cin, h3_flip = dgrad, h3_hi, h3_lo, h3_wexp, h3_scratch).  Results are
+ * dcs_pack_subpix_h3 pack (w, Cout, Cin, h3_flip = kind, h3_hi, h3_lo, h3_wexp, h3_scratch).  Results are
  * bit-identical to the per-pack calls.  jobs_dev: device copy of jobs[0 .. njobs) (the caller stages it;
  * jobs only supplies the host-side block counts); the b0 / b1 / p0 / p1 fields are filled here. */
 typedef struct dcs_pack_job {

@@ -10,6 +10,8 @@ the same fp32 operands:
     against float64 autograd of upsample + conv, to the same bound;
   * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
     against float64 autograd, to the same bound;
+  * the down-convs (stride-2 3x3 zero-pad-1) on the same kernels: forward + statistics over the
+    source's parity classes, data gradient over dx's, to the same bound;
   * the rows pass on the same pack (the phase planes removed) agrees to its own bound, and the
     batched pack (ops.prepack) equals the per-pack launches bit for bit.
 Tolerances written per check below."""
@@ -125,11 +127,58 @@ def test_subpix_wgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     assert _relmax(dw, ref) <= 1e-5
 
 
-@pytest.mark.parametrize("dgrad", [False, True])
-def test_subpix_pack_batched_bit_identical(ops, dgrad):
+def _s2(ops, cin, cout):
+    from modules.hip.lib import DCS_PAD_ZERO
+    return ops.ConvGeom(cin, cout, 3, 2, (1, 1, 1, 1), DCS_PAD_ZERO)
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("cin,cout,N,H,W", [(64, 128, 2, 32, 32), (128, 256, 1, 64, 64), (64, 128, 1, 16, 256)])
+def test_stride2_forward_stats_and_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
+    """The down-convs (stride-2 3x3 zero-pad-1) on the window phase kernels: forward + IN statistics
+    over the source's parity classes, data gradient over dx's, against float64; the rows pass over the
+    same packs (phase planes removed) to its own bound."""
+    ops.set_mma(mode)
+    g = _s2(ops, cin, cout)
+    assert g.s2win
+    x = rnd((N, cin, H, W), 91, "x").double().requires_grad_(True)
+    w = torch.from_numpy(prng.normal(92, "w", (cout, cin, 3, 3), 0, 0.05)).float().double()
+    ref = F.conv2d(x, w, stride=2, padding=1)
+    dy = rnd(tuple(ref.shape), 93, "dy").double()
+    (dref,) = torch.autograd.grad(ref, x, dy)
+    ref = ref.detach()
+    mean, var = ref.mean(dim=(2, 3)), ref.var(dim=(2, 3), unbiased=False)
+    xd = x.detach().float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
+    assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
+    y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
+    assert _relmax(y.permute(0, 3, 1, 2), ref) <= 1e-5
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    assert _relmax(st.scale, rstd) <= 1e-5
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= 1e-5 * float((mean * rstd).abs().max() + 1)
+    assert _relmax(st.xmax, ref.flatten(2).max(dim=2).values) <= 1e-5
+    assert torch.equal(g.forward(ops.Src.nhwc(xd), wp), y)
+    dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dx = g.dgrad(dyd, wd, H, W)
+    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= 1e-5
+    assert torch.equal(g.dgrad(dyd, wd, H, W), dx)  # deterministic
+    rows_tol = 1e-5 if mode == "f16x3" else 2e-3
+    for pk in (wp, wd):
+        del pk._dcs_sp
+    assert _relmax(g.forward(ops.Src.nhwc(xd), wp).permute(0, 3, 1, 2), ref) <= rows_tol
+    assert _relmax(g.dgrad(dyd, wd, H, W).permute(0, 3, 1, 2), dref) <= rows_tol
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_subpix_pack_batched_bit_identical(ops, kind):
     ops.set_mma("f16x3")
-    g = _geom(ops, 256, 128)
-    w = (rnd((128, 256, 3, 3), 83, "w") * 0.05).float().to(DEV)
+    dgrad = kind in (1, 2)
+    if kind < 2:
+        g = _geom(ops, 256, 128)
+        w = (rnd((128, 256, 3, 3), 83, "w") * 0.05).float().to(DEV)
+    else:
+        g = _s2(ops, 128, 256)
+        w = (rnd((256, 128, 3, 3), 83, "w") * 0.05).float().to(DEV)
     pack = g.pack_dgrad if dgrad else g.pack_fwd
     sp = [a.clone() for a in pack(w)._dcs_sp]
     w.mul_(1.0)
