@@ -69,6 +69,11 @@ __device__ __forceinline__ float subpix_tapsum(const float* __restrict__ w, int 
 // a = 0 takes ty = 1 at o = 0; a = 1 takes ty = 0 at o = 0 and ty = 2 at o = 1.
 __device__ __forceinline__ int s2_dgrad_tap(int a, int u) { return a ? (u ? 0 : 2) : (u ? 1 : -1); }
 __device__ __forceinline__ int s2_fwd_tap(int a, int o) { return a ? (o ? 2 : 0) : (o ? -1 : 1); }
+// 4x4 stride-2 pad-1 (the PatchGAN layers): every (class, offset) pair is a tap.  Data gradient: a = 0
+// takes ty = 3 at u = 0 and 1 at u = 1, a = 1 takes 2 at u = 0 and 0 at u = 1; forward: a = 0 takes 1 at
+// o = 0 and 3 at o = 1, a = 1 takes 0 at o = 0 and 2 at o = 1.
+__device__ __forceinline__ int k4_dgrad_tap(int a, int u) { return a ? (u ? 0 : 2) : (u ? 1 : 3); }
+__device__ __forceinline__ int k4_fwd_tap(int a, int o) { return a ? (o ? 2 : 0) : (o ? 3 : 1); }
 
 // B of the window phase kernels (conv_subpix.hip), kind:
 //  0: sub-pixel forward, [4 Cout][4 Cin]: virtual row v = (column tile (px, 64-channel block), row
@@ -76,38 +81,41 @@ __device__ __forceinline__ int s2_fwd_tap(int a, int o) { return a ? (o ? 2 : 0)
 //  1: sub-pixel data gradient, [Cin][16 Cout]: row = input channel, k = (phase, slice of the output
 //     channels, window offset (1 - u, 1 - t), channel);
 //  2: stride-2 data gradient, [4 Cin][4 Cout]: kind 0's layout over dx's parity classes;
-//  3: stride-2 forward, [Cout][16 Cin]: kind 1's layout over the source's parity classes.
+//  3: stride-2 forward, [Cout][16 Cin]: kind 1's layout over the source's parity classes;
+//  4 / 5: the 4x4 stride-2 convolution's forward / data gradient in kind 3's / kind 2's layout.
 __device__ __forceinline__ float subpix_value(const float* __restrict__ w, int Cout, int Cin, int kind, int v, int k) {
     const int rem = k & 63, tap = rem >> 4;
-    if (kind == 0 || kind == 2) {
+    if (kind == 0 || kind == 2 || kind == 5) {
         const int Cv = kind == 0 ? Cout : Cin;  // the kernel's output channels
         const int cblk = Cv >> 6;
         const int ntile = v >> 7, py = (v >> 6) & 1;
         const int px = ntile / cblk, oc = (ntile - px * cblk) * 64 + (v & 63);
         const int rc = (k >> 6) * 16 + (rem & 15);  // reduction channel
         if (kind == 0) return subpix_tapsum(w, Cin, oc, rc, py, px, tap >> 1, tap & 1);
+        if (kind == 5) return w[((long long)rc * Cin + oc) * 16 + k4_dgrad_tap(py, tap >> 1) * 4 + k4_dgrad_tap(px, tap & 1)];
         const int ty = s2_dgrad_tap(py, tap >> 1), tx = s2_dgrad_tap(px, tap & 1);
         return (ty < 0 || tx < 0) ? 0.f : w[((long long)rc * Cin + oc) * 9 + ty * 3 + tx];
     }
     const int nslice = (kind == 1 ? Cout : Cin) >> 4, it = k >> 6;
     const int ph = it / nslice, rc = (it - ph * nslice) * 16 + (rem & 15);
     if (kind == 1) return subpix_tapsum(w, Cin, rc, v, ph >> 1, ph & 1, 1 - (tap >> 1), 1 - (tap & 1));
+    if (kind == 4) return w[((long long)v * Cin + rc) * 16 + k4_fwd_tap(ph >> 1, tap >> 1) * 4 + k4_fwd_tap(ph & 1, tap & 1)];
     const int ty = s2_fwd_tap(ph >> 1, tap >> 1), tx = s2_fwd_tap(ph & 1, tap & 1);
     return (ty < 0 || tx < 0) ? 0.f : w[((long long)v * Cin + rc) * 9 + ty * 3 + tx];
 }
 // shapes each kind takes (the kernels' channel tiling)
 inline bool subpix_pack_ok(int Cout, int Cin, int kind) {
-    if (Cout <= 0 || Cin <= 0 || 16LL * Cout * Cin >= (1LL << 30) || kind < 0 || kind > 3) return false;
+    if (Cout <= 0 || Cin <= 0 || 16LL * Cout * Cin >= (1LL << 30) || kind < 0 || kind > 5) return false;
     switch (kind) {
         case 0: return Cout % 64 == 0 && Cin % 16 == 0;
         case 1: return Cout % 16 == 0 && Cin % 128 == 0;
-        case 2: return Cin % 64 == 0 && Cout % 16 == 0;
-        default: return Cout % 128 == 0 && Cin % 16 == 0;
+        case 2: case 5: return Cin % 64 == 0 && Cout % 16 == 0;
+        default: return Cout % 128 == 0 && Cin % 16 == 0;  // 3, 4
     }
 }
 // rows and k of a kind's planes (rows x K = 16 Cout Cin)
 __device__ __host__ __forceinline__ int subpix_K(int Cout, int Cin, int kind) {
-    return kind == 0 ? 4 * Cin : kind == 1 ? 16 * Cout : kind == 2 ? 4 * Cout : 16 * Cin;
+    return kind == 0 ? 4 * Cin : kind == 1 ? 16 * Cout : (kind == 2 || kind == 5) ? 4 * Cout : 16 * Cin;
 }
 
 }  // namespace dcs

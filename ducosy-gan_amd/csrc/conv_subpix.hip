@@ -40,7 +40,9 @@ struct SubArgs {
     int R, TW, tiles_x, tiles;  // tile = R rows x TW columns of the source; tiles per row band / image
     int gy, cblk;          // column tiles (MODE 0: 4 Co / 128, MODE 1: Co / 128), 64-channel blocks (Co / 64)
     int rng_n;
+    int pro_act;           // PRO: the source prologue's activation (DCS_ACT_AFFINE / _RELU / _LRELU)
 };
+constexpr int SP_PROC = 512;  // PRO: source channels the prologue table holds
 
 // window: pixel pairs swap on odd groups of 8 pixels, 16-byte halves on odd groups of 16 (conflict-free
 // reads of every other pixel: the MFMA row blocks interleave, as conv_win.hip)
@@ -56,14 +58,18 @@ __device__ __forceinline__ int sp_boff(int buf, int pl, int tap, int row, int h)
 // S2: the stride-2 forward).  S2 kernels skip the (phase, offset) pairs no 3x3 tap reaches (weights 0).
 // PXC >= 0: the launch covers the column tiles of column phase PXC only (the stride-2 data gradient runs
 // one launch per phase, so the phase's skipped column offset is known at compile time)
-template <int NP, int MODE, int S2, int PXC = -1>
+// PRO (MODE 1): the source is y of a layer a = act(y * scale + shift) (per image and channel, the
+// PatchGAN's InstanceNorm + LeakyReLU): the window staging applies it, zero padding outside the image.
+template <int NP, int MODE, int S2, int PXC = -1, int PRO = 0>
 __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const float* __restrict__ src,
                                                               const _Float16* __restrict__ wh,
                                                               const _Float16* __restrict__ wl,
                                                               const float* __restrict__ rng,
                                                               const int* __restrict__ wexp, float* __restrict__ out,
-                                                              Part* __restrict__ parts) {
+                                                              Part* __restrict__ parts, const float* __restrict__ psc,
+                                                              const float* __restrict__ psh) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * SP_PIX * 16 + 2 * 2 * 4 * SP_SLOT];
+    __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 2 * SP_PROC : 4];  // [scale | shift][channel]
     _Float16* const Wn = smem;
     _Float16* const Bs = smem + 2 * 2 * SP_PIX * 16;
 
@@ -87,6 +93,13 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     const int ea = f16x3_exp(rng, a.rng_n);
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
     const float asc = __builtin_ldexpf(1.f, ea);
+    if constexpr (PRO) {  // the image's prologue scale / shift (read before the first staging barrier)
+        for (int c = tid; c < C; c += SP_NT) {
+            pro_s[c] = psc[(long long)n * C + c];
+            pro_s[SP_PROC + c] = psh[(long long)n * C + c];
+        }
+        __syncthreads();
+    }
 
     // window staging units (pixel, 8-channel half).  MODE 0: byte offset of the unit's channel 0 (-1:
     // zero).  MODE 1: the unit's window (row, column) packed as row * 4096 + column (-1: none); the dy
@@ -110,6 +123,7 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float4 wr_[SP_UNITS][2];
+    int vmask = 0, vit = 0;  // PRO: the staged units inside the image, and their iteration
     auto unit_off = [&](int q, int it) {  // byte offset of unit q's 8 channels at iteration it (OOB: zero)
         if constexpr (MODE == 0) {
             return uoff[q] >= 0 ? uoff[q] + it * 64 : 0x7fffffbf;
@@ -123,9 +137,11 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         }
     };
     auto win_load = [&](int it) {
+        if constexpr (PRO) { vmask = 0; vit = it; }
 #pragma unroll
         for (int q = 0; q < SP_UNITS; ++q) {
             const int off = unit_off(q, it);
+            if constexpr (PRO) vmask |= (off != 0x7fffffbf) << q;
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
             __builtin_memcpy(&wr_[q][0], &v0, 16);
@@ -138,6 +154,19 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             const int u = tid + q * SP_NT;
             const int wpix = u >> 1, h = u & 1;
             if (wpix < npix) {
+                if constexpr (PRO) {  // a = act(y * scale + shift) inside the image, 0 in the padding
+                    const int c0 = (vit % nslice) * 16 + 8 * h;
+                    const float4 s0 = *reinterpret_cast<const float4*>(pro_s + c0);
+                    const float4 s1 = *reinterpret_cast<const float4*>(pro_s + c0 + 4);
+                    const float4 b0 = *reinterpret_cast<const float4*>(pro_s + SP_PROC + c0);
+                    const float4 b1 = *reinterpret_cast<const float4*>(pro_s + SP_PROC + c0 + 4);
+                    const bool ok = (vmask >> q) & 1;
+                    auto f = [&](float v, float sc, float sh) { return ok ? act_apply(fmaf(v, sc, sh), a.pro_act) : 0.f; };
+                    wr_[q][0] = make_float4(f(wr_[q][0].x, s0.x, b0.x), f(wr_[q][0].y, s0.y, b0.y),
+                                            f(wr_[q][0].z, s0.z, b0.z), f(wr_[q][0].w, s0.w, b0.w));
+                    wr_[q][1] = make_float4(f(wr_[q][1].x, s1.x, b1.x), f(wr_[q][1].y, s1.y, b1.y),
+                                            f(wr_[q][1].z, s1.z, b1.z), f(wr_[q][1].w, s1.w, b1.w));
+                }
                 f16x8 hi, lo;
                 split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
                 *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 0, wpix, h)) = hi;
@@ -674,22 +703,26 @@ bool subpix_dgrad_geom(const dcs_conv_desc& d, SubArgs* a) {
 // [N][Hs][Ws][Cs] with Hs = 2 Ho) on the class kernel (MODE 1), data gradient (parity 1, dy [N][Hs][Ws][Cs]
 // onto dx [N][2 Hs][2 Ws][Co]) on the phase kernel (MODE 0)
 bool s2_geom(const dcs_conv_desc& d, SubArgs* a) {
-    const bool common = d.up == 1 && d.stride == 2 && d.KH == 3 && d.KW == 3 && d.pad_mode == DCS_PAD_ZERO &&
+    const bool k3 = d.KH == 3 && d.KW == 3, k4 = d.KH == 4 && d.KW == 4;
+    const bool pro_ok = d.pro_act == DCS_ACT_NONE ||
+                        (d.parity == 0 && d.Cs <= SP_PROC &&
+                         (d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU || d.pro_act == DCS_ACT_LRELU));
+    const bool common = d.up == 1 && d.stride == 2 && (k3 || k4) && d.pad_mode == DCS_PAD_ZERO &&
                         d.pt == 1 && d.pl == 1 && d.N > 0 && d.Hs > 0 && d.Ws > 0 && d.Cs % 16 == 0 && d.Cs > 0 &&
                         d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
-                        d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE &&
+                        d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && pro_ok &&
                         d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
                         d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
                         d.Co > 0 && 16LL * d.Co * d.Cs < (1LL << 30);
     if (!common) return false;
     if (d.parity == 0) {  // forward
         if (d.Hs != 2 * d.Ho || d.Ws != 2 * d.Wo || d.Co % 128 || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
-        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
+        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; a->pro_act = d.pro_act; }
         return true;
     }
     if (d.parity == 1) {  // data gradient
         if (d.Ho != 2 * d.Hs || d.Wo != 2 * d.Ws || d.Co % 64 || !tile_geom(d.N, d.Hs, d.Ws, a)) return false;
-        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
+        if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; a->pro_act = 0; }
         return true;
     }
     return false;
@@ -727,10 +760,10 @@ extern "C" int dcs_subpix_win(const dcs_conv_desc* dp, const float* src, const v
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
         hipLaunchKernelGGL((subpix_win_kernel<1, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
-                           out, reinterpret_cast<Part*>(parts));
+                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr);
     else
         hipLaunchKernelGGL((subpix_win_kernel<3, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
-                           out, reinterpret_cast<Part*>(parts));
+                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr);
     return check_launch("subpix_win");
 }
 
@@ -751,10 +784,10 @@ extern "C" int dcs_subpix_win_dgrad(const dcs_conv_desc* dp, const float* dy, co
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
         hipLaunchKernelGGL((subpix_win_kernel<1, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
-                           nullptr);
+                           nullptr, nullptr, nullptr);
     else
         hipLaunchKernelGGL((subpix_win_kernel<3, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
-                           nullptr);
+                           nullptr, nullptr, nullptr);
     return check_launch("subpix_win_dgrad");
 }
 
@@ -820,15 +853,19 @@ extern "C" size_t dcs_stride2_win_parts_size(const dcs_conv_desc* dp) {
     return (size_t)a.N * a.tiles * a.Co * sizeof(Part);
 }
 
-extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const void* w_hi, const void* w_lo,
-                               const int* wexp, float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream) {
+extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const float* pro_scale,
+                               const float* pro_shift, const void* w_hi, const void* w_lo, const int* wexp, float* out,
+                               void* parts, size_t parts_bytes, int* nchunk, void* stream) {
     if (!dp || !src || !w_hi || !w_lo || !wexp || !out) return fail(DCS_E_INVALID, "stride2_win: null pointer");
     SubArgs a;
     if (!s2_geom(*dp, &a))
-        return fail(DCS_E_INVALID, "stride2_win: needs a stride-2 3x3 zero-pad-1 rows descriptor over contiguous NHWC "
-                                   "(parity 0: forward, Co % 128 == 0; parity 1: data gradient, Co % 64 == 0), "
-                                   "Cs % 16 == 0, the low-resolution grid tileable (min(W, 128) dividing 256 and W), "
-                                   "f16x3 / f16 with the source range record");
+        return fail(DCS_E_INVALID, "stride2_win: needs a stride-2 3x3 or 4x4 zero-pad-1 rows descriptor over contiguous "
+                                   "NHWC (parity 0: forward, Co % 128 == 0, an optional affine / ReLU / LeakyReLU "
+                                   "prologue for Cs <= 512; parity 1: data gradient, Co % 64 == 0), Cs % 16 == 0, the "
+                                   "low-resolution grid tileable (min(W, 128) dividing 256 and W), f16x3 / f16 with "
+                                   "the source range record");
+    const bool pro = dp->pro_act != DCS_ACT_NONE;
+    if (pro && (!pro_scale || !pro_shift)) return fail(DCS_E_INVALID, "stride2_win: prologue needs scale and shift");
     if (parts) {
         if (dp->parity != 0 || !nchunk || parts_bytes < dcs_stride2_win_parts_size(dp))
             return fail(DCS_E_WORKSPACE, "stride2_win: statistics only for the forward, parts buffer too small");
@@ -840,18 +877,29 @@ extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const 
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     Part* pp = reinterpret_cast<Part*>(parts);
     const bool f16 = dp->mma == DCS_MMA_F16;
+    const bool k3 = dp->KH == 3;  // 3x3: the unreached (class, offset) pairs skipped; 4x4: every pair a tap
+#define DCS_S2_FWD(NP_, S2_, PRO_)                                                                                   \
+    hipLaunchKernelGGL((subpix_win_kernel<NP_, 1, S2_, -1, PRO_>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l,      \
+                       dp->rng_a, wexp, out, pp, pro_scale, pro_shift)
+#define DCS_S2_DG(NP_, S2_, PXC_)                                                                                    \
+    hipLaunchKernelGGL((subpix_win_kernel<NP_, 0, S2_, PXC_>), dim3(blocks / 2), dim3(SP_NT), 0, s, a, src, h, l,     \
+                       dp->rng_a, wexp, out, nullptr, nullptr, nullptr)
     if (dp->parity == 0) {
-        if (f16) hipLaunchKernelGGL((subpix_win_kernel<1, 1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, pp);
-        else hipLaunchKernelGGL((subpix_win_kernel<3, 1, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, pp);
-    } else {  // one launch per column phase
-        const dim3 g2(blocks / 2);
         if (f16) {
-            hipLaunchKernelGGL((subpix_win_kernel<1, 0, 1, 0>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
-            hipLaunchKernelGGL((subpix_win_kernel<1, 0, 1, 1>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+            if (k3) { if (pro) DCS_S2_FWD(1, 1, 1); else DCS_S2_FWD(1, 1, 0); }
+            else { if (pro) DCS_S2_FWD(1, 0, 1); else DCS_S2_FWD(1, 0, 0); }
         } else {
-            hipLaunchKernelGGL((subpix_win_kernel<3, 0, 1, 0>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
-            hipLaunchKernelGGL((subpix_win_kernel<3, 0, 1, 1>), g2, dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp, out, nullptr);
+            if (k3) { if (pro) DCS_S2_FWD(3, 1, 1); else DCS_S2_FWD(3, 1, 0); }
+            else { if (pro) DCS_S2_FWD(3, 0, 1); else DCS_S2_FWD(3, 0, 0); }
+        }
+    } else {  // one launch per column phase
+        if (f16) {
+            if (k3) { DCS_S2_DG(1, 1, 0); DCS_S2_DG(1, 1, 1); } else { DCS_S2_DG(1, 0, 0); DCS_S2_DG(1, 0, 1); }
+        } else {
+            if (k3) { DCS_S2_DG(3, 1, 0); DCS_S2_DG(3, 1, 1); } else { DCS_S2_DG(3, 0, 0); DCS_S2_DG(3, 0, 1); }
         }
     }
+#undef DCS_S2_FWD
+#undef DCS_S2_DG
     return check_launch("stride2_win");
 }

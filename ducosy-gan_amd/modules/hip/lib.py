@@ -83,7 +83,7 @@ SIGNATURES = {
     "dcs_subpix_win_dgrad": (c_int, [DP, P, P, P, P, P, P]),
     "dcs_stride2_win_ok": (c_int, [DP]),
     "dcs_stride2_win_parts_size": (c_size_t, [DP]),
-    "dcs_stride2_win": (c_int, [DP, P, P, P, P, P, P, c_size_t, POINTER(c_int), P]),
+    "dcs_stride2_win": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, POINTER(c_int), P]),
     "dcs_subpix_win_ok": (c_int, [DP]),
     "dcs_subpix_win_parts_size": (c_size_t, [DP]),
     "dcs_subpix_win": (c_int, [DP, P, P, P, P, P, P, c_size_t, POINTER(c_int), P]),

@@ -482,9 +482,9 @@ class ConvGeom:
 
     @property
     def s2win(self) -> bool:
-        """The window phase kernels for this stride-2 3x3 zero-pad-1 conv (the down-convs): forward over
-        the source's parity classes, data gradient over dx's."""
-        return (_SUBWIN and _S2WIN and _h3() and self.stride == 2 and self.k == 3 and self.up == 1 and
+        """The window phase kernels for this stride-2 3x3 or 4x4 zero-pad-1 conv (the down-convs, the
+        PatchGAN layers): forward over the source's parity classes, data gradient over dx's."""
+        return (_SUBWIN and _S2WIN and _h3() and self.stride == 2 and self.k in (3, 4) and self.up == 1 and
                 self.pads == (1, 1, 1, 1) and self.pad_mode == DCS_PAD_ZERO and self.cout % 128 == 0 and
                 self.cin % 64 == 0)
 
@@ -492,7 +492,7 @@ class ConvGeom:
         """Pre-split planes of the window phase kernels (dcs_pack_subpix_h3 kind: 0 / 1 sub-pixel forward /
         data gradient, 2 / 3 stride-2 data gradient / forward) on the pack as _dcs_sp."""
         shape = {0: (4 * self.cout, 4 * self.cin), 1: (self.cin, 16 * self.cout), 2: (4 * self.cin, 4 * self.cout),
-                 3: (self.cout, 16 * self.cin)}[kind]
+                 3: (self.cout, 16 * self.cin), 4: (self.cout, 16 * self.cin), 5: (4 * self.cin, 4 * self.cout)}[kind]
         hi = torch.empty(*shape, device=w.device, dtype=torch.float16)
         lo = torch.empty_like(hi)
         wexp = torch.empty(1, device=w.device, dtype=torch.int32)
@@ -533,7 +533,7 @@ class ConvGeom:
         K = self.k * self.k * self.cin
         out = self._pack(w, 0, self.cin, K, self.cout)
         if self.s2win:
-            return self._attach_sp(out, w, 3)
+            return self._attach_sp(out, w, 3 if self.k == 3 else 4)
         return self._attach_h3(out, w, 0) if self.win else out
 
     @property
@@ -565,7 +565,7 @@ class ConvGeom:
         K = self.k * self.k * self.cout
         out = self._pack(w, kind, ci, K, ci)
         if self.s2win and ci == self.cin:
-            return self._attach_sp(out, w, 2)
+            return self._attach_sp(out, w, 2 if self.k == 3 else 5)
         return self._attach_h3(out, w, 1) if (self.win and ci == self.cin) else out
 
     def _pack(self, w, kind, ci_count, K, ncols):
@@ -645,8 +645,8 @@ class ConvGeom:
         if nb and h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):
             return self._win_in_stats(s, d, h3, nb, want_max)
         sp = getattr(wpack, "_dcs_sp", None)
-        if nb and sp is not None and bias is None and self._phase_win_ok(d):
-            return self._subpix(s, d, sp, True, want_max)
+        if nb and sp is not None and bias is None and s.t2 is None and self._phase_win_ok(d):
+            return self._subpix(s, d, sp, True, want_max, pro)
         if nb == 0:
             out = self.forward(s, wpack, bias, pro, epi_act)
             return out, in_stats(out, want_max)
@@ -699,7 +699,7 @@ class ConvGeom:
         d.mma = mma
         return bool(ok)
 
-    def _subpix(self, s: Src, d, sp, stats: bool, want_max: bool = False):
+    def _subpix(self, s: Src, d, sp, stats: bool, want_max: bool = False, pro=None):
         """An up- or down-conv forward (+ the IN statistics of its output when ``stats``) on the window
         phase kernels (csrc/conv_subpix.hip); f16x3 operands in both fp16 modes, as the stem and head
         (the f16 step's edge-loss selection sits at its tolerance with fp16 up-convs)."""
@@ -710,7 +710,8 @@ class ConvGeom:
         api = "dcs_subpix_win" if self.subpixel else "dcs_stride2_win"
         parts = workspace(lib.query(api + "_parts_size", ctypes.byref(d)), dev) if stats else None
         nchunk = ctypes.c_int(0)
-        lib.call(api, ctypes.byref(d), _p(s.t), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _p(parts),
+        pre = () if self.subpixel else (_p(pro[0]) if pro else None, _p(pro[1]) if pro else None)
+        lib.call(api, ctypes.byref(d), _p(s.t), *pre, _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), _p(parts),
                  parts.numel() if stats else 0, ctypes.byref(nchunk), _stream())
         if not stats:
             return out
@@ -734,8 +735,8 @@ class ConvGeom:
                      _stream())
             return True
         if self.stride == 2 and lib.query("dcs_stride2_win_ok", ctypes.byref(d)):
-            lib.call("dcs_stride2_win", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out), None, 0,
-                     None, _stream())
+            lib.call("dcs_stride2_win", ctypes.byref(d), _p(dy), None, None, _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out),
+                     None, 0, None, _stream())
             return True
         d.mma = mma
         return False
@@ -785,7 +786,7 @@ class ConvGeom:
                 return self._stem(s, d, wpack, False)
             sp = getattr(wpack, "_dcs_sp", None)
             if sp is not None and bias is None and self._phase_win_ok(d):
-                return self._subpix(s, d, sp, False)
+                return self._subpix(s, d, sp, False, pro=pro)
         h3 = getattr(wpack, "_dcs_h3", None)
         e0 = PROBE.begin() if _is_res_geom(self) else None
         if h3 is not None and bias is None and lib.query("dcs_conv3_win_ok", ctypes.byref(d), 0):

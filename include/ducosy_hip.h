@@ -235,9 +235,10 @@ int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* d, const float* dy, const fl
  * (u * 2 + t) * 16 + c % 16 for source offset (u, t)); Cout % 64 == 0, Cin % 16 == 0.  kind 1: the
  * transposed phase weights of the data gradient [Cin][16 Cout] (row = input channel, k = ((py * 2 + px) *
  * Cout / 16 + co / 16) * 64 + ((1 - u) * 2 + (1 - t)) * 16 + co % 16); Cout % 16 == 0, Cin % 128 == 0.
- * kinds 2 and 3: the stride-2 convolution's taps in kind 0's layout over dx's parity classes (its data
- * gradient, [4 Cin][4 Cout]; Cin % 64 == 0, Cout % 16 == 0) and in kind 1's layout over the source's
- * parity classes (its forward, [Cout][16 Cin]; Cout % 128 == 0, Cin % 16 == 0), zero where no tap lands.
+ * kinds 2 and 3: the stride-2 3x3 convolution's taps in kind 0's layout over dx's parity classes (its
+ * data gradient, [4 Cin][4 Cout]; Cin % 64 == 0, Cout % 16 == 0) and in kind 1's layout over the source's
+ * parity classes (its forward, [Cout][16 Cin]; Cout % 128 == 0, Cin % 16 == 0), zero where no tap lands;
+ * kinds 5 and 4: the same for a 4x4 stride-2 convolution (w [Cout][Cin][4][4]).
  * dcs_subpix_win_ok(d): 1 if d is a sub-pixel rows descriptor (parity 2, as the rows pass takes it:
  * up = 1, Ho = 2 Hs) these kernels cover (contiguous NHWC, Cs % 16 == 0, Co % 64 == 0, min(Ws, 128)
  * dividing 256 and Ws, Hs % (256 / min(Ws, 128)) == 0, f16x3 / f16 with rng_a set, no prologue).
@@ -257,17 +258,21 @@ int dcs_subpix_win(const dcs_conv_desc* d, const float* src, const void* w_hi, c
 int dcs_subpix_win_dgrad_ok(const dcs_conv_desc* d);
 int dcs_subpix_win_dgrad(const dcs_conv_desc* d, const float* dy, const void* w_hi, const void* w_lo, const int* wexp,
                          float* dx, void* stream);
-/* The down-convolutions (stride-2 3x3 zero-pad-1, modules/model.py:100-106) on the same two kernels: the
+/* The down-convolutions (stride-2 3x3 zero-pad-1, modules/model.py:100-106) and the PatchGAN's stride-2
+ * 4x4 zero-pad-1 layers (modules/model.py:118-131; every class offset a tap) on the same two kernels: the
  * forward as a sum over the source's four parity classes of <= 2x2 convolutions of the class sub-grids
  * (the sub-pixel data gradient's kernel; + IN statistics partials when parts != NULL,
  * dcs_stride2_win_parts_size bytes, *nchunk = tiles per image), the data gradient as four <= 2x2 phase
  * convolutions of dy onto dx's parity classes (the sub-pixel forward's kernel); the (class, offset) pairs
  * no tap reaches are skipped.  d: the rows pass's descriptor (parity 0: forward, Hs = 2 Ho, Co % 128 == 0;
- * parity 1: data gradient, Ho = 2 Hs, Co % 64 == 0), planes from dcs_pack_subpix_h3 kind 3 / 2. */
+ * parity 1: data gradient, Ho = 2 Hs, Co % 64 == 0), planes from dcs_pack_subpix_h3 kind 3 / 2 (3x3) or
+ * 4 / 5 (4x4).  The forward takes the rows pass's prologue (d.pro_act AFFINE / RELU / LRELU with
+ * pro_scale / pro_shift [N][Cs], Cs <= 512): a = act(y * scale + shift) staged, zero in the padding. */
 int dcs_stride2_win_ok(const dcs_conv_desc* d);
 size_t dcs_stride2_win_parts_size(const dcs_conv_desc* d);
-int dcs_stride2_win(const dcs_conv_desc* d, const float* src, const void* w_hi, const void* w_lo, const int* wexp,
-                    float* out, void* parts, size_t parts_bytes, int* nchunk, void* stream);
+int dcs_stride2_win(const dcs_conv_desc* d, const float* src, const float* pro_scale, const float* pro_shift,
+                    const void* w_hi, const void* w_lo, const int* wexp, float* out, void* parts, size_t parts_bytes,
+                    int* nchunk, void* stream);
 /* The same data gradient dx = da of a layer a = act(InstanceNorm(y)) (the first conv of a residual
  * block, modules/model.py:74-76), with the InstanceNorm backward's partial sums fused: the window
  * epilogue sums g = da * act'(xhat) and g * xhat (xhat = y * scale + shift) per (256-pixel tile,

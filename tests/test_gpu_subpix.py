@@ -10,8 +10,9 @@ the same fp32 operands:
     against float64 autograd of upsample + conv, to the same bound;
   * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
     against float64 autograd, to the same bound;
-  * the down-convs (stride-2 3x3 zero-pad-1) on the same kernels: forward + statistics over the
-    source's parity classes, data gradient over dx's, to the same bound;
+  * the down-convs (stride-2 3x3 zero-pad-1) and the PatchGAN layers (4x4, with the previous layer's
+    IN + LeakyReLU staged as a prologue) on the same kernels: forward + statistics over the source's
+    parity classes, data gradient over dx's, to the same bound;
   * the rows pass on the same pack (the phase planes removed) agrees to its own bound, and the
     batched pack (ops.prepack) equals the per-pack launches bit for bit.
 Tolerances written per check below."""
@@ -169,16 +170,60 @@ def test_stride2_forward_stats_and_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     assert _relmax(g.dgrad(dyd, wd, H, W).permute(0, 3, 1, 2), dref) <= rows_tol
 
 
-@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("cin,cout,N,H,W", [(64, 128, 2, 64, 64), (256, 512, 1, 64, 64), (128, 256, 1, 32, 256)])
+def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
+    """A PatchGAN layer (4x4 stride-2 zero-pad-1, modules/model.py:118-131) on the window phase kernels:
+    forward with the previous layer's InstanceNorm + LeakyReLU as the staged prologue and the IN
+    statistics of its output, and the data gradient, against float64."""
+    from modules.hip.lib import ACT_LRELU, DCS_PAD_ZERO
+    ops.set_mma(mode)
+    g = ops.ConvGeom(cin, cout, 4, 2, (1, 1, 1, 1), DCS_PAD_ZERO)
+    assert g.s2win
+    y = rnd((N, cin, H, W), 94, "y").double()
+    sc = (torch.from_numpy(prng.uniform(95, "sc", (N, cin), 0.5, 2.0))).double()
+    sh = (torch.from_numpy(prng.uniform(95, "sh", (N, cin), -0.5, 0.5))).double()
+    a = F.leaky_relu(y * sc[:, :, None, None] + sh[:, :, None, None], 0.2).requires_grad_(True)
+    w = torch.from_numpy(prng.normal(96, "w", (cout, cin, 4, 4), 0, 0.05)).float().double()
+    ref = F.conv2d(a, w, stride=2, padding=1)
+    dy = rnd(tuple(ref.shape), 97, "dy").double()
+    (dref,) = torch.autograd.grad(ref, a, dy)
+    ref = ref.detach()
+    mean, var = ref.mean(dim=(2, 3)), ref.var(dim=(2, 3), unbiased=False)
+    yd = y.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    pro = (sc.float().to(DEV).contiguous(), sh.float().to(DEV).contiguous(), ACT_LRELU)
+    wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
+    assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
+    out, st = g.forward_in_stats(ops.Src.nhwc(yd), wp, pro=pro)
+    assert _relmax(out.permute(0, 3, 1, 2), ref) <= 1e-5
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    assert _relmax(st.scale, rstd) <= 1e-5
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= 1e-5 * float((mean * rstd).abs().max() + 1)
+    assert torch.equal(g.forward(ops.Src.nhwc(yd), wp, pro=pro), out)
+    dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dx = g.dgrad(dyd, wd, H, W)
+    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= 1e-5
+    rows_tol = 1e-5 if mode == "f16x3" else 2e-3
+    for pk in (wp, wd):
+        del pk._dcs_sp
+    assert _relmax(g.forward(ops.Src.nhwc(yd), wp, pro=pro).permute(0, 3, 1, 2), ref) <= rows_tol
+    assert _relmax(g.dgrad(dyd, wd, H, W).permute(0, 3, 1, 2), dref) <= rows_tol
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
 def test_subpix_pack_batched_bit_identical(ops, kind):
     ops.set_mma("f16x3")
-    dgrad = kind in (1, 2)
+    dgrad = kind in (1, 2, 5)
     if kind < 2:
         g = _geom(ops, 256, 128)
         w = (rnd((128, 256, 3, 3), 83, "w") * 0.05).float().to(DEV)
-    else:
+    elif kind < 4:
         g = _s2(ops, 128, 256)
         w = (rnd((256, 128, 3, 3), 83, "w") * 0.05).float().to(DEV)
+    else:
+        from modules.hip.lib import DCS_PAD_ZERO
+        g = ops.ConvGeom(128, 256, 4, 2, (1, 1, 1, 1), DCS_PAD_ZERO)
+        w = (rnd((256, 128, 4, 4), 83, "w") * 0.05).float().to(DEV)
     pack = g.pack_dgrad if dgrad else g.pack_fwd
     sp = [a.clone() for a in pack(w)._dcs_sp]
     w.mul_(1.0)
