@@ -3098,14 +3098,19 @@ namespace dcs {
 bool wgrad_win_check(const dcs_conv_desc& d);
 size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
 int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
-// conv_subpix.hip: the f16x3 window weight gradient of the up-convolutions (a VARIANT build with
-// EXTRA=-DDCS_SUBPIX_WGRAD=0 runs the x6 phase classes instead, for A/B)
+// conv_subpix.hip: the f16x3 window weight gradients of the up- and stride-2 convolutions (a VARIANT build
+// with EXTRA=-DDCS_SUBPIX_WGRAD=0 runs the x6 kernels instead, for A/B)
 #ifndef DCS_SUBPIX_WGRAD
 #define DCS_SUBPIX_WGRAD 1
 #endif
 bool subpix_wgrad_check(const dcs_conv_desc& d);
 size_t subpix_wgrad_workspace_size(const dcs_conv_desc& d);
 int subpix_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
+// conv_subpix.hip: the f16x3 window weight gradient of the stride-2 convolutions (3x3 and 4x4)
+bool s2_wgrad_check(const dcs_conv_desc& d);
+size_t s2_wgrad_workspace_size(const dcs_conv_desc& d);
+int s2_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh,
+                    float* ws, hipStream_t s);
 }  // namespace dcs
 
 extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
@@ -3118,6 +3123,10 @@ extern "C" size_t dcs_conv_wgrad_workspace_size(const dcs_conv_desc* dp) {
     }
     if (DCS_SUBPIX_WGRAD && subpix_wgrad_check(*dp)) {
         const size_t nw = subpix_wgrad_workspace_size(*dp);
+        n = nw > n ? nw : n;
+    }
+    if (DCS_SUBPIX_WGRAD && s2_wgrad_check(*dp)) {
+        const size_t nw = s2_wgrad_workspace_size(*dp);
         n = nw > n ? nw : n;
     }
     return n;
@@ -3156,6 +3165,14 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         hipLaunchKernelGGL(wgrad_subpixel_fold_kernel, dim3((unsigned)cdiv(tot9, 256)), dim3(256), 0, s, w, ns, d.Co,
                            d.Cs, dw);
         return check_launch("wgrad_subpixel_fold");
+    }
+    if (DCS_SUBPIX_WGRAD && s2_wgrad_check(d) && !x2) {  // f16x3 stride-2 conv: the rolling class-window kernel
+        const int ns = s2_wgrad_launch(d, dy, x, psc, psh, w, s);
+        if (ns < 0) return -ns;
+        const long long total = (long long)d.Co * d.KH * d.KW * d.Cs;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, w, ns, d.Co, d.Cs,
+                           d.KH, d.KW, d.Cs, dw);
+        return check_launch("conv_wgrad_reduce");
     }
     const bool res = d.Cs == 256 && d.KH == 3 && d.KW == 3 && d.up == 1 && d.stride == 1 && !d.parity &&
                      d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE;

@@ -643,6 +643,254 @@ __global__ __launch_bounds__(SW_NT, 1) void subpix_wgrad_kernel(SWArgs a, const 
         }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight gradient of the stride-2 convolutions (down-convs 3x3, PatchGAN 4x4; zero pad 1) on a rolling
+// window of the full-resolution source (f16x3):
+//   dW[co][ci][ty][tx] = sum_{i, j} dy[i][j][co] * x[2i + ty - 1][2j + tx - 1][ci]
+// A workgroup owns 64 co x 32 ci x all KK taps and walks a 64-pixel strip of the low-resolution grid row
+// by row.  Per row it stages the dy row segment (64 px x 64 co, conv_win.hip's swizzled pixel-major
+// layout) and the two new source rows 2i + 1, 2i + 2 of the strip, each split by column parity into an
+// odd array O[p] = x[2 (x0 + p) - 1] and an even array E[p] = x[2 (x0 + p)] (65 px x 32 ci, 64-byte
+// pixel rows), into a ring of six rows; tap (ty, tx) reads row 2i + ty - 1 at O[j + tx / 2] (tx even) or
+// E[j + (tx - 1) / 2] (tx odd).  Waves: 2 co blocks x 4 tap groups (4x4: four taps each; 3x3: 3, 2, 2, 2),
+// M = co (32), N = ci (32), K = 16 low-resolution pixels; fragments by ds_read_b64_tr_b16.  An optional
+// source prologue a = act(y * scale + shift) (the PatchGAN's IN + LeakyReLU) is applied at staging, zero
+// in the padding.  Partial slabs [split][co][tap * C + ci] for conv.hip's wgrad_reduce_kernel.
+constexpr int S2W_NT = 512, S2W_SW = 64, S2W_P = 65;
+constexpr int S2W_XCLS = 2 * S2W_P * 32;     // halves per (row, class): 2 planes x 65 px x 32 ci
+constexpr int S2W_XROW = 2 * S2W_XCLS;       // halves per ring slot (2 classes)
+constexpr int S2W_DROW = 2 * S2W_SW * 64;    // halves per dy buffer (2 planes x 64 px x 64 co)
+constexpr int S2W_XU = (2 * S2W_P * 4 + S2W_NT - 1) / S2W_NT;  // source (class, pixel, 8-ci unit)s per thread per row
+
+struct S2WArgs {
+    int N, H, W, C, Co;  // dy NHWC [N][H][W][Co] (low resolution); source [N][2H][2W][C]
+    int KK;              // 3 or 4
+    int strips, rchunks, rows_per;
+    int gco, gci;        // 64-channel co tiles, 32-channel ci tiles
+    int rng_a_n, rng_b_n;
+    int pro_act;
+};
+
+template <int NP, int KK, int PRO>
+__global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const float* __restrict__ dy,
+                                                             const float* __restrict__ src,
+                                                             const float* __restrict__ rnga,
+                                                             const float* __restrict__ rngb,
+                                                             const float* __restrict__ psc,
+                                                             const float* __restrict__ psh, float* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[6 * S2W_XROW + 2 * S2W_DROW];
+    __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 64 : 4];  // the ci block's scale | shift
+    _Float16* const Xr = smem;                 // [6 rows][class][2 planes][65 px][32 ci]
+    _Float16* const Dy = smem + 6 * S2W_XROW;  // [2][2 planes][64 px][64 co]
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = a.gco * a.gci;
+    const int tile = L % ntile, split = L / ntile;
+    const int co0 = (tile % a.gco) * 64, ci0 = (tile / a.gco) * 32;
+    const int rc = split % a.rchunks, rest = split / a.rchunks;
+    const int strip = rest % a.strips, n = rest / a.strips;
+    const int x0 = strip * S2W_SW;
+    const int H = a.H, W = a.W, C = a.C, Co = a.Co;
+    const int y_beg = rc * a.rows_per;
+    const int y_end = y_beg + a.rows_per < H ? y_beg + a.rows_per : H;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int cob = wid & 1, grp = wid >> 1;
+    constexpr int NT = KK == 4 ? 4 : 3;  // taps per wave (3x3: 3, 2, 2, 2)
+    const int t0 = KK == 4 ? grp * 4 : (grp == 0 ? 0 : 1 + 2 * grp);
+    const int nt = KK == 4 ? 4 : (grp == 0 ? 3 : 2);
+
+    const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
+    const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+    if constexpr (PRO) {
+        if (tid < 32) {
+            pro_s[tid] = psc[(long long)n * C + ci0 + tid];
+            pro_s[32 + tid] = psh[(long long)n * C + ci0 + tid];
+        }
+        __syncthreads();
+    }
+
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int OOB = 0x7fffffbf;
+
+    // dy row segment: 64 px x 8 units, one per thread
+    int doff, dls;
+    {
+        const int pix = tid >> 3, cu = tid & 7;
+        doff = ((x0 + pix) * Co + co0 + 8 * cu) * 4;
+        dls = pix * 64 + 8 * (cu ^ sw_swz(pix));
+    }
+    // source row segment: 2 classes x 65 px x 4 units; unit -> (class, p, cu); byte offset within the row
+    // of the full-resolution column (-1: outside the image), LDS offset within the slot (-1: none)
+    const int W2 = 2 * W;
+    int xoff[S2W_XU], xls[S2W_XU];
+#pragma unroll
+    for (int q = 0; q < S2W_XU; ++q) {
+        const int u = tid + q * S2W_NT;
+        const int cu = u & 3, p = (u >> 2) % S2W_P, cls = (u >> 2) / S2W_P;  // cls 0: odd, 1: even
+        xoff[q] = -1;
+        xls[q] = -1;
+        if (cls < 2) {
+            const int col = cls == 0 ? 2 * (x0 + p) - 1 : 2 * (x0 + p);
+            if (col >= 0 && col < W2) xoff[q] = (col * C + ci0 + 8 * cu) * 4;
+            xls[q] = cls * S2W_XCLS + p * 32 + 8 * cu;
+        }
+    }
+    float4 dr[2], xr[2][S2W_XU][2];
+    auto ld_dy = [&](int y) {
+        const int rb = ((n * H + y) * W) * Co * 4;
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff + 16, 0, 0);
+        __builtin_memcpy(&dr[0], &v0, 16);
+        __builtin_memcpy(&dr[1], &v1, 16);
+    };
+    auto ld_x = [&](int slot, int r) {  // full-resolution source row r (zero outside the image)
+        const bool ok = r >= 0 && r < 2 * H;
+        const int rb = ((n * 2 * H + (ok ? r : 0)) * W2) * C * 4;
+#pragma unroll
+        for (int q = 0; q < S2W_XU; ++q) {
+            const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
+            if constexpr (PRO) {  // the prologue applies inside the image only
+                if (!(ok && xoff[q] >= 0)) { v0 = u32x4{0, 0, 0, 0}; v1 = u32x4{0, 0, 0, 0}; }
+            }
+            __builtin_memcpy(&xr[slot][q][0], &v0, 16);
+            __builtin_memcpy(&xr[slot][q][1], &v1, 16);
+        }
+    };
+    auto st_dy = [&](int buf) {
+        f16x8 hi, lo;
+        split8h(dr[0], dr[1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(Dy + buf * S2W_DROW + dls) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * S2W_DROW + S2W_SW * 64 + dls) = lo;
+    };
+    auto st_x = [&](int slot, int rs, int r) {  // register set rs -> ring slot of row r
+        const bool ok = r >= 0 && r < 2 * H;
+#pragma unroll
+        for (int q = 0; q < S2W_XU; ++q) {
+            if (xls[q] >= 0) {
+                float4 v0 = xr[rs][q][0], v1 = xr[rs][q][1];
+                if constexpr (PRO) {
+                    if (ok && xoff[q] >= 0) {
+                        const int c0 = 8 * (tid + q * S2W_NT & 3);
+                        auto f = [&](float v, int c) { return act_apply(fmaf(v, pro_s[c], pro_s[32 + c]), a.pro_act); };
+                        v0 = make_float4(f(v0.x, c0), f(v0.y, c0 + 1), f(v0.z, c0 + 2), f(v0.w, c0 + 3));
+                        v1 = make_float4(f(v1.x, c0 + 4), f(v1.y, c0 + 5), f(v1.z, c0 + 6), f(v1.w, c0 + 7));
+                    }
+                }
+                f16x8 hi, lo;
+                split8h(v0, v1, bsc, hi, lo);
+                const int cls = xls[q] >= S2W_XCLS ? 1 : 0;
+                const int base = slot * S2W_XROW + cls * S2W_XCLS;
+                const int off = xls[q] - cls * S2W_XCLS;
+                *reinterpret_cast<f16x8*>(Xr + base + off) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + base + S2W_P * 32 + off) = lo;
+            }
+        }
+    };
+
+    // transposed-read lane offsets (halves), as conv_win.hip's weight gradient
+    const int g16 = lane >> 4;
+    const int rpix = 8 * (g16 >> 1) + ((lane & 15) >> 2);
+    const int rcol = 16 * (g16 & 1) + 4 * (lane & 3);
+    int aoff;
+    {
+        const int c = 32 * cob + rcol;
+        aoff = rpix * 64 + 8 * ((c >> 3) ^ sw_swz(rpix)) + (c & 7);
+    }
+    // per tap of the wave: ring row offset (ty - 1 relative to 2i) and class array offset
+    int tdy[NT], tb[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+        const int tap = t0 + (k < nt ? k : 0);
+        const int ty = tap / KK, tx = tap - (tap / KK) * KK;
+        tdy[k] = ty - 1;
+        const int cls = (tx & 1) ? 1 : 0;  // tx odd: even class (column 2j + tx - 1 even)
+        const int po = (tx & 1) ? (tx - 1) / 2 : tx / 2;
+        tb[k] = cls * S2W_XCLS + (rpix + po) * 32 + rcol;
+    }
+
+    floatx16 acc[NT], tq[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; tq[i][r] = 0.f; }
+
+    auto slot_of = [](int r) { return ((r % 6) + 6) % 6; };
+    // prologue: rows 2 y_beg - 1 .. 2 y_beg + KK - 2 into their slots, dy row y_beg into buffer 0
+#pragma unroll 1
+    for (int r = 2 * y_beg - 1; r <= 2 * y_beg + KK - 2; ++r) {
+        ld_x(0, r);
+        st_x(slot_of(r), 0, r);
+    }
+    ld_dy(y_beg);
+    st_dy(y_beg & 1);
+    __syncthreads();
+
+#pragma unroll 1
+    for (int y = y_beg; y < y_end; ++y) {
+        // next step's rows in flight: dy row y + 1 and source rows 2y + KK - 1, 2y + KK
+        const int rn = 2 * y + KK - 1;
+        ld_dy(y + 1 < y_end ? y + 1 : y);
+        ld_x(0, rn);
+        ld_x(1, rn + 1);
+        const _Float16* const Db = Dy + (y & 1) * S2W_DROW;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // 16-pixel sub-tiles of the strip
+            f16x8 ah, al;
+            ah = sw_frag<64>(Db + aoff + k * 16 * 64);
+            if constexpr (NP == 3) al = sw_frag<64>(Db + S2W_SW * 64 + aoff + k * 16 * 64);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (t < nt) {
+                    const _Float16* xs = Xr + slot_of(2 * y + tdy[t]) * S2W_XROW + tb[t] + k * 16 * 32;
+                    f16x8 bh, bl;
+                    bh = sw_frag<32>(xs);
+                    if constexpr (NP == 3) {
+                        bl = sw_frag<32>(xs + S2W_P * 32);
+                        tq[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tq[t], 0, 0, 0);
+                        tq[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tq[t], 0, 0, 0);
+                    }
+                    tq[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tq[t], 0, 0, 0);
+                }
+            }
+        }
+        // stage the loaded rows into the slots this row does not read (rows 2y - 3, 2y - 2 modulo 6)
+        st_dy((y + 1) & 1);
+        st_x(slot_of(rn), 0, rn);
+        st_x(slot_of(rn + 1), 1, rn + 1);
+        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                acc[i] += tq[i];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tq[i][r] = 0.f;
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: undo the operand scales, slab [split][co][tap * C + ci]
+    const int eab = -(ea + eb);
+    const long long Ktot = (long long)KK * KK * C;
+    float* const slab = ws + (long long)split * Co * Ktot;
+    const int col = ci0 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        if (i < nt) {
+            const int tap = t0 + i;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = co0 + 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                slab[(long long)row * Ktot + tap * C + col] = __builtin_ldexpf(acc[i][r], eab);
+            }
+        }
+    }
+}
+
 struct SWPlan {
     int strips, rchunks, rows_per, nsplit;
 };
@@ -903,3 +1151,67 @@ extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const 
 #undef DCS_S2_DG
     return check_launch("stride2_win");
 }
+
+namespace dcs {
+namespace {
+SWPlan s2w_plan(const dcs_conv_desc& d) {
+    SWPlan p;
+    p.strips = d.Wo / S2W_SW;
+    const long long base = (long long)d.N * p.strips * (d.Co / 64) * (d.Cs / 32);
+    int rch = (int)cdiv(256, base);
+    const int maxch = d.Ho / 8 > 0 ? d.Ho / 8 : 1;  // >= 8 rows per chunk
+    rch = rch < 1 ? 1 : (rch > maxch ? maxch : rch);
+    p.rows_per = (int)cdiv(d.Ho, rch);
+    p.rchunks = (int)cdiv(d.Ho, p.rows_per);
+    p.nsplit = d.N * p.strips * p.rchunks;
+    return p;
+}
+}  // namespace
+
+// conv.hip's dcs_conv_wgrad: d describes the forward stride-2 conv (parity 0; source [N][Hs][Ws][Cs], Hs = 2 Ho)
+bool s2_wgrad_check(const dcs_conv_desc& d) {
+    return (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.parity == 0 && d.up == 1 && d.stride == 2 &&
+           ((d.KH == 3 && d.KW == 3) || (d.KH == 4 && d.KW == 4)) && d.pad_mode == DCS_PAD_ZERO && d.pt == 1 &&
+           d.pl == 1 && d.Hs == 2 * d.Ho && d.Ws == 2 * d.Wo && d.Cs % 32 == 0 && d.Co % 64 == 0 &&
+           d.Wo % S2W_SW == 0 && d.Ho >= 1 && d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
+           d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) &&
+           (d.pro_act == DCS_ACT_NONE || d.pro_act == DCS_ACT_AFFINE || d.pro_act == DCS_ACT_RELU ||
+            d.pro_act == DCS_ACT_LRELU) &&
+           d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_a_n <= 1024 && d.rng_b_n > 0 && d.rng_b_n <= 1024 &&
+           (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
+           (long long)d.N * d.Ho * d.Wo * d.Co * 4 < 0x7fffff00LL - 64;
+}
+
+size_t s2_wgrad_workspace_size(const dcs_conv_desc& d) {
+    const SWPlan p = s2w_plan(d);
+    return (size_t)p.nsplit * d.Co * d.KH * d.KW * d.Cs * sizeof(float);
+}
+
+// partial slabs [split][co][tap * C + ci] into ws; returns the split count (< 0: error).  rng_a: dy's range
+// record, rng_b: the (prologued) source's.
+int s2_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, const float* psc, const float* psh,
+                    float* ws, hipStream_t s) {
+    const SWPlan p = s2w_plan(d);
+    S2WArgs a;
+    a.N = d.N; a.H = d.Ho; a.W = d.Wo; a.C = d.Cs; a.Co = d.Co; a.KK = d.KH;
+    a.strips = p.strips; a.rchunks = p.rchunks; a.rows_per = p.rows_per;
+    a.gco = d.Co / 64; a.gci = d.Cs / 32;
+    a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n; a.pro_act = d.pro_act;
+    const bool pro = d.pro_act != DCS_ACT_NONE;
+    if (pro && (!psc || !psh)) return -fail(DCS_E_INVALID, "conv_wgrad: prologue needs scale and shift");
+    const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
+    const bool f16 = d.mma == DCS_MMA_F16;
+#define DCS_S2W(NP_, KK_, PRO_) \
+    hipLaunchKernelGGL((s2_wgrad_kernel<NP_, KK_, PRO_>), dim3(blocks), dim3(S2W_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, psc, psh, ws)
+    if (d.KH == 3) {
+        if (f16) { if (pro) DCS_S2W(1, 3, 1); else DCS_S2W(1, 3, 0); }
+        else { if (pro) DCS_S2W(3, 3, 1); else DCS_S2W(3, 3, 0); }
+    } else {
+        if (f16) { if (pro) DCS_S2W(1, 4, 1); else DCS_S2W(1, 4, 0); }
+        else { if (pro) DCS_S2W(3, 4, 1); else DCS_S2W(3, 4, 0); }
+    }
+#undef DCS_S2W
+    const int e = check_launch("s2_wgrad");
+    return e ? -e : p.nsplit;
+}
+}  // namespace dcs

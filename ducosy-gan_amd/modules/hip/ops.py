@@ -982,7 +982,7 @@ class ConvGeom:
             d.mma = m0
         if not self.narrow and s.t2 is None and _h3() and s.t.is_contiguous():
             _set_mma(d, dy, None, range_rec(s.t, pro))
-            if self.subwin:  # the up-convs on f16x3 operands in both fp16 modes, as their forward (_subpix)
+            if self.subwin or self.s2win:  # f16x3 operands in both fp16 modes, as their forward (_subpix)
                 d.mma = lib.MMA_F16X3
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
             d.cw = self.cin

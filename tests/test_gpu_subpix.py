@@ -13,6 +13,7 @@ the same fp32 operands:
   * the down-convs (stride-2 3x3 zero-pad-1) and the PatchGAN layers (4x4, with the previous layer's
     IN + LeakyReLU staged as a prologue) on the same kernels: forward + statistics over the source's
     parity classes, data gradient over dx's, to the same bound;
+  * the weight gradients of those stride-2 layers on the rolling class-window kernel, to the same bound;
   * the rows pass on the same pack (the phase planes removed) agrees to its own bound, and the
     batched pack (ops.prepack) equals the per-pack launches bit for bit.
 Tolerances written per check below."""
@@ -208,6 +209,35 @@ def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
         del pk._dcs_sp
     assert _relmax(g.forward(ops.Src.nhwc(yd), wp, pro=pro).permute(0, 3, 1, 2), ref) <= rows_tol
     assert _relmax(g.dgrad(dyd, wd, H, W).permute(0, 3, 1, 2), dref) <= rows_tol
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+@pytest.mark.parametrize("k,cin,cout,N,H,W,pro", [(3, 64, 128, 1, 128, 128, False), (3, 128, 256, 2, 34, 128, False),
+                                                  (4, 64, 128, 1, 64, 128, True), (4, 256, 512, 1, 32, 128, True)])
+def test_stride2_wgrad_vs_fp64(ops, mode, k, cin, cout, N, H, W, pro):
+    """dL/dW of a down-conv (3x3) or a PatchGAN layer (4x4, with the IN + LeakyReLU prologue of its
+    source) on the rolling class-window kernel, against float64 autograd; row chunks that do not
+    divide the output rows included (Ho = 17)."""
+    from modules.hip.lib import ACT_LRELU, DCS_PAD_ZERO
+    ops.set_mma(mode)
+    g = ops.ConvGeom(cin, cout, k, 2, (1, 1, 1, 1), DCS_PAD_ZERO)
+    assert g.s2win
+    y = rnd((N, cin, H, W), 98, "y").double()
+    if pro:
+        sc = torch.from_numpy(prng.uniform(99, "sc", (N, cin), 0.5, 2.0)).double()
+        sh = torch.from_numpy(prng.uniform(99, "sh", (N, cin), -0.5, 0.5)).double()
+        a = F.leaky_relu(y * sc[:, :, None, None] + sh[:, :, None, None], 0.2)
+        prod = (sc.float().to(DEV).contiguous(), sh.float().to(DEV).contiguous(), ACT_LRELU)
+    else:
+        a, prod = y, None
+    w = torch.from_numpy(prng.normal(100, "w", (cout, cin, k, k), 0, 0.05)).float().double().requires_grad_(True)
+    out = F.conv2d(a, w, stride=2, padding=1)
+    dy = rnd(tuple(out.shape), 101, "dy").double()
+    (ref,) = torch.autograd.grad(out, w, dy)
+    yd = y.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    dw = g.wgrad(dyd, ops.Src.nhwc(yd), pro=prod)
+    assert _relmax(dw, ref) <= 1e-5
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
