@@ -894,13 +894,12 @@ __global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const fl
 struct SWPlan {
     int strips, rchunks, rows_per, nsplit;
 };
+int rolling_rchunks(long long base, int rows);
 SWPlan sw_plan(const dcs_conv_desc& d) {
     SWPlan p;
     p.strips = d.Ws / SW_SW;
     const long long base = (long long)d.N * p.strips * (d.Co / 32) * (d.Cs / 64);
-    int rch = (int)cdiv(256, base);  // at least one workgroup per CU
-    const int maxch = d.Hs / 8 > 0 ? d.Hs / 8 : 1;  // >= 8 rows per chunk
-    rch = rch < 1 ? 1 : (rch > maxch ? maxch : rch);
+    const int rch = rolling_rchunks(base, d.Hs);
     p.rows_per = (int)cdiv(d.Hs, rch);
     p.rchunks = (int)cdiv(d.Hs, p.rows_per);
     p.nsplit = d.N * p.strips * p.rchunks;
@@ -1154,13 +1153,24 @@ extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const 
 
 namespace dcs {
 namespace {
+// row chunks per strip: the count that minimises (dispatch rounds of one workgroup per CU) x (rows per
+// workgroup), >= 8 rows per chunk, fewer chunks (less slab traffic) on ties
+int rolling_rchunks(long long base, int rows) {
+    const int maxch = rows / 8 > 0 ? rows / 8 : 1;
+    int best = 1;
+    long long best_cost = -1;
+    for (int rch = 1; rch <= maxch && rch <= 64; ++rch) {
+        const long long cost = cdiv(base * rch, 256) * cdiv(rows, rch);
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = rch; }
+    }
+    return best;
+}
+
 SWPlan s2w_plan(const dcs_conv_desc& d) {
     SWPlan p;
     p.strips = d.Wo / S2W_SW;
     const long long base = (long long)d.N * p.strips * (d.Co / 64) * (d.Cs / 32);
-    int rch = (int)cdiv(256, base);
-    const int maxch = d.Ho / 8 > 0 ? d.Ho / 8 : 1;  // >= 8 rows per chunk
-    rch = rch < 1 ? 1 : (rch > maxch ? maxch : rch);
+    const int rch = rolling_rchunks(base, d.Ho);
     p.rows_per = (int)cdiv(d.Ho, rch);
     p.rchunks = (int)cdiv(d.Ho, p.rows_per);
     p.nsplit = d.N * p.strips * p.rchunks;
@@ -1170,8 +1180,10 @@ SWPlan s2w_plan(const dcs_conv_desc& d) {
 
 // conv.hip's dcs_conv_wgrad: d describes the forward stride-2 conv (parity 0; source [N][Hs][Ws][Cs], Hs = 2 Ho)
 bool s2_wgrad_check(const dcs_conv_desc& d) {
+    // (the PatchGAN's 4x4 layers measured slower here than on the x6 kernel in the bench step's 8-image
+    // calls: 217 vs 174 us, profiles/r04af; the kernel takes them, the dispatch keeps them on x6)
     return (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.parity == 0 && d.up == 1 && d.stride == 2 &&
-           ((d.KH == 3 && d.KW == 3) || (d.KH == 4 && d.KW == 4)) && d.pad_mode == DCS_PAD_ZERO && d.pt == 1 &&
+           d.KH == 3 && d.KW == 3 && d.pad_mode == DCS_PAD_ZERO && d.pt == 1 &&
            d.pl == 1 && d.Hs == 2 * d.Ho && d.Ws == 2 * d.Wo && d.Cs % 32 == 0 && d.Co % 64 == 0 &&
            d.Wo % S2W_SW == 0 && d.Ho >= 1 && d.s_c == 1 && d.s_w == d.Cs && d.s_h == (long long)d.Ws * d.Cs &&
            d.s_n == (long long)d.Hs * d.Ws * d.Cs && d.csplit == d.Cs && (d.cw == 0 || d.cw == d.Cs) &&
@@ -1203,13 +1215,8 @@ int s2_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, con
     const bool f16 = d.mma == DCS_MMA_F16;
 #define DCS_S2W(NP_, KK_, PRO_) \
     hipLaunchKernelGGL((s2_wgrad_kernel<NP_, KK_, PRO_>), dim3(blocks), dim3(S2W_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, psc, psh, ws)
-    if (d.KH == 3) {
-        if (f16) { if (pro) DCS_S2W(1, 3, 1); else DCS_S2W(1, 3, 0); }
-        else { if (pro) DCS_S2W(3, 3, 1); else DCS_S2W(3, 3, 0); }
-    } else {
-        if (f16) { if (pro) DCS_S2W(1, 4, 1); else DCS_S2W(1, 4, 0); }
-        else { if (pro) DCS_S2W(3, 4, 1); else DCS_S2W(3, 4, 0); }
-    }
+    if (f16) { if (pro) DCS_S2W(1, 3, 1); else DCS_S2W(1, 3, 0); }  // (3x3 only: s2_wgrad_check)
+    else { if (pro) DCS_S2W(3, 3, 1); else DCS_S2W(3, 3, 0); }
 #undef DCS_S2W
     const int e = check_launch("s2_wgrad");
     return e ? -e : p.nsplit;

@@ -5,7 +5,8 @@ the same fp32 operands:
     epilogue partials) for up1 (256 -> 128) and up2 (128 -> 64) shapes, source widths 16 .. 256
     (every tile width the kernel takes: 16, 32, 64, 128 and two column strips);
   * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in both fp16
-    modes (the host runs the kernel on f16x3 operands in f16 mode too);
+    modes for the up-convs (the host runs them on f16x3 operands in f16 mode too); the stride-2 layers
+    run in the step's mode (f16: 2e-3, fp16 operands);
   * the data gradient (per phase a 2x2 conv of dy's phase sub-grid with the transposed phase weights)
     against float64 autograd of upsample + conv, to the same bound;
   * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
@@ -153,16 +154,17 @@ def test_stride2_forward_stats_and_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     xd = x.detach().float().to(DEV).permute(0, 2, 3, 1).contiguous()
     wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
     assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
+    tol = 1e-5 if mode == "f16x3" else 2e-3  # the stride-2 layers run in the step's operand mode
     y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
-    assert _relmax(y.permute(0, 3, 1, 2), ref) <= 1e-5
+    assert _relmax(y.permute(0, 3, 1, 2), ref) <= tol
     rstd = 1.0 / torch.sqrt(var + 1e-5)
-    assert _relmax(st.scale, rstd) <= 1e-5
-    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= 1e-5 * float((mean * rstd).abs().max() + 1)
-    assert _relmax(st.xmax, ref.flatten(2).max(dim=2).values) <= 1e-5
+    assert _relmax(st.scale, rstd) <= tol
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= tol * float((mean * rstd).abs().max() + 1)
+    assert _relmax(st.xmax, ref.flatten(2).max(dim=2).values) <= tol
     assert torch.equal(g.forward(ops.Src.nhwc(xd), wp), y)
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dx = g.dgrad(dyd, wd, H, W)
-    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= 1e-5
+    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= tol
     assert torch.equal(g.dgrad(dyd, wd, H, W), dx)  # deterministic
     rows_tol = 1e-5 if mode == "f16x3" else 2e-3
     for pk in (wp, wd):
@@ -195,15 +197,16 @@ def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
     pro = (sc.float().to(DEV).contiguous(), sh.float().to(DEV).contiguous(), ACT_LRELU)
     wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
     assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
+    tol = 1e-5 if mode == "f16x3" else 2e-3  # the stride-2 layers run in the step's operand mode
     out, st = g.forward_in_stats(ops.Src.nhwc(yd), wp, pro=pro)
-    assert _relmax(out.permute(0, 3, 1, 2), ref) <= 1e-5
+    assert _relmax(out.permute(0, 3, 1, 2), ref) <= tol
     rstd = 1.0 / torch.sqrt(var + 1e-5)
-    assert _relmax(st.scale, rstd) <= 1e-5
-    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= 1e-5 * float((mean * rstd).abs().max() + 1)
+    assert _relmax(st.scale, rstd) <= tol
+    assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= tol * float((mean * rstd).abs().max() + 1)
     assert torch.equal(g.forward(ops.Src.nhwc(yd), wp, pro=pro), out)
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dx = g.dgrad(dyd, wd, H, W)
-    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= 1e-5
+    assert _relmax(dx.permute(0, 3, 1, 2), dref) <= tol
     rows_tol = 1e-5 if mode == "f16x3" else 2e-3
     for pk in (wp, wd):
         del pk._dcs_sp
@@ -215,9 +218,9 @@ def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
 @pytest.mark.parametrize("k,cin,cout,N,H,W,pro", [(3, 64, 128, 1, 128, 128, False), (3, 128, 256, 2, 34, 128, False),
                                                   (4, 64, 128, 1, 64, 128, True), (4, 256, 512, 1, 32, 128, True)])
 def test_stride2_wgrad_vs_fp64(ops, mode, k, cin, cout, N, H, W, pro):
-    """dL/dW of a down-conv (3x3) or a PatchGAN layer (4x4, with the IN + LeakyReLU prologue of its
-    source) on the rolling class-window kernel, against float64 autograd; row chunks that do not
-    divide the output rows included (Ho = 17)."""
+    """dL/dW of a down-conv (3x3, the rolling class-window kernel) or a PatchGAN layer (4x4, with the
+    IN + LeakyReLU prologue of its source; the x6 kernel) against float64 autograd; row chunks that do
+    not divide the output rows included (Ho = 17)."""
     from modules.hip.lib import ACT_LRELU, DCS_PAD_ZERO
     ops.set_mma(mode)
     g = ops.ConvGeom(cin, cout, k, 2, (1, 1, 1, 1), DCS_PAD_ZERO)
@@ -237,7 +240,7 @@ def test_stride2_wgrad_vs_fp64(ops, mode, k, cin, cout, N, H, W, pro):
     yd = y.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dw = g.wgrad(dyd, ops.Src.nhwc(yd), pro=prod)
-    assert _relmax(dw, ref) <= 1e-5
+    assert _relmax(dw, ref) <= (1e-5 if mode == "f16x3" else 2e-3)  # the step's operand mode
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
