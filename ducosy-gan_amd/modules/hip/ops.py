@@ -691,20 +691,27 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
+    def _phase_mma(self, d) -> None:
+        """Operand mode of the window phase kernels' forward and data gradient: the up-convs and the
+        PatchGAN layers on f16x3 in both fp16 modes, as the stem and head (with fp16 operands the
+        config-5 fixture's f16 step misses its bar: the edge term for the up-convs, the lung
+        Discriminator loss for the PatchGAN layers, profiles/r04ah); the down-convs in the step's mode."""
+        if self.subpixel or self.k == 4:
+            d.mma = lib.MMA_F16X3
+
     def _phase_win_ok(self, d) -> bool:
-        """d (a forward descriptor) is one the window phase kernels cover, with f16x3 operands."""
+        """d (a forward descriptor) is one the window phase kernels cover, in their operand mode."""
         mma = d.mma
-        d.mma = lib.MMA_F16X3
+        self._phase_mma(d)
         ok = lib.query("dcs_subpix_win_ok" if self.subpixel else "dcs_stride2_win_ok", ctypes.byref(d))
         d.mma = mma
         return bool(ok)
 
     def _subpix(self, s: Src, d, sp, stats: bool, want_max: bool = False, pro=None):
-        """An up- or down-conv forward (+ the IN statistics of its output when ``stats``) on the window
-        phase kernels (csrc/conv_subpix.hip); f16x3 operands in both fp16 modes, as the stem and head
-        (the f16 step's edge-loss selection sits at its tolerance with fp16 up-convs)."""
+        """An up- or down-conv (or PatchGAN layer) forward (+ the IN statistics of its output when
+        ``stats``) on the window phase kernels (csrc/conv_subpix.hip), operand mode as _phase_mma."""
         dev = s.t.device
-        d.mma = lib.MMA_F16X3
+        self._phase_mma(d)
         Ho, Wo = self.out_hw(s.H, s.W)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=dev, dtype=torch.float32)
         api = "dcs_subpix_win" if self.subpixel else "dcs_stride2_win"
@@ -725,11 +732,11 @@ class ConvGeom:
         return out, INStats(scale, shift, xmax, xam)
 
     def _phase_win(self, d, dy: torch.Tensor, sp, out: torch.Tensor) -> bool:
-        """An up- or down-conv data gradient on the window phase kernels (csrc/conv_subpix.hip; f16x3 in
-        both fp16 modes, as the forward); False where the descriptor is not one they cover (the rows pass
-        runs it)."""
+        """An up- or down-conv (or PatchGAN layer) data gradient on the window phase kernels
+        (csrc/conv_subpix.hip; operand mode as the forward, _phase_mma); False where the descriptor is not
+        one they cover (the rows pass runs it)."""
         mma = d.mma
-        d.mma = lib.MMA_F16X3
+        self._phase_mma(d)
         if self.subpixel and lib.query("dcs_subpix_win_dgrad_ok", ctypes.byref(d)):
             lib.call("dcs_subpix_win_dgrad", ctypes.byref(d), _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out),
                      _stream())
@@ -981,9 +988,7 @@ class ConvGeom:
                 return out
             d.mma = m0
         if not self.narrow and s.t2 is None and _h3() and s.t.is_contiguous():
-            _set_mma(d, dy, None, range_rec(s.t, pro))
-            if self.subwin or self.s2win:  # f16x3 operands in both fp16 modes, as their forward (_subpix)
-                d.mma = lib.MMA_F16X3
+            _set_mma(d, dy, None, range_rec(s.t, pro))  # (weight gradients in the step's mode)
         if s.C != self.cin:  # zero-padded source channels (4-channel stem): weights have cin
             d.cw = self.cin
         assert tuple(dy.shape) == (s.N, d.Ho, d.Wo, self.cout), (dy.shape, d.Ho, d.Wo)

@@ -4,9 +4,10 @@ the same fp32 operands:
   * forward + the InstanceNorm statistics of its output (scale / shift / max / argmax from the
     epilogue partials) for up1 (256 -> 128) and up2 (128 -> 64) shapes, source widths 16 .. 256
     (every tile width the kernel takes: 16, 32, 64, 128 and two column strips);
-  * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in both fp16
-    modes (the host runs the window phase kernels on f16x3 operands in f16 mode too: with fp16
-    operands the config-5 fixture's f16 step misses its bar, profiles/r04ah);
+  * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in f16x3 mode;
+    in f16 mode the up-convs and PatchGAN layers stay on f16x3 operands (with fp16 the config-5
+    fixture's f16 step misses its bar, profiles/r04ah), the down-convs and every weight gradient
+    run on fp16 operands (2e-3);
   * the data gradient (per phase a 2x2 conv of dy's phase sub-grid with the transposed phase weights)
     against float64 autograd of upsample + conv, to the same bound;
   * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
@@ -127,7 +128,7 @@ def test_subpix_wgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dw = g.wgrad(dyd, ops.Src.nhwc(xd))
-    assert _relmax(dw, ref) <= 1e-5
+    assert _relmax(dw, ref) <= (1e-5 if mode == "f16x3" else 2e-3)  # weight gradients in the step's mode
 
 
 def _s2(ops, cin, cout):
@@ -154,7 +155,7 @@ def test_stride2_forward_stats_and_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     xd = x.detach().float().to(DEV).permute(0, 2, 3, 1).contiguous()
     wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
     assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
-    tol = 1e-5  # f16x3 operands in both fp16 modes
+    tol = 1e-5 if mode == "f16x3" else 2e-3  # the down-convs run in the step's operand mode
     y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
     assert _relmax(y.permute(0, 3, 1, 2), ref) <= tol
     rstd = 1.0 / torch.sqrt(var + 1e-5)
@@ -240,7 +241,7 @@ def test_stride2_wgrad_vs_fp64(ops, mode, k, cin, cout, N, H, W, pro):
     yd = y.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dw = g.wgrad(dyd, ops.Src.nhwc(yd), pro=prod)
-    assert _relmax(dw, ref) <= 1e-5
+    assert _relmax(dw, ref) <= (1e-5 if mode == "f16x3" else 2e-3)  # weight gradients in the step's mode
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
