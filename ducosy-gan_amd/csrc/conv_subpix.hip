@@ -44,6 +44,17 @@ struct SubArgs {
 };
 constexpr int SP_PROC = 512;  // PRO: source channels the prologue table holds
 
+// the InstanceNorm backward's partial sums of a data gradient's output da (a layer a = act(IN(y)) whose
+// input gradient this is): per (chunk, channel) sum g and sum g * xhat, g = da * act'(xhat),
+// xhat = y * scale + shift (the same quantities as conv_win.hip's IbwArgs)
+struct PhIbw {
+    const float* y;
+    const float* sc;
+    const float* sh;
+    Sum2* parts;  // [N][nchunk][Co]
+    int act;
+};
+
 // window: pixel pairs swap on odd groups of 8 pixels, 16-byte halves on odd groups of 16 (conflict-free
 // reads of every other pixel: the MFMA row blocks interleave, as conv_win.hip)
 __device__ __forceinline__ int sp_woff(int buf, int pl, int wpix, int h) {
@@ -60,14 +71,15 @@ __device__ __forceinline__ int sp_boff(int buf, int pl, int tap, int row, int h)
 // one launch per phase, so the phase's skipped column offset is known at compile time)
 // PRO (MODE 1): the source is y of a layer a = act(y * scale + shift) (per image and channel, the
 // PatchGAN's InstanceNorm + LeakyReLU): the window staging applies it, zero padding outside the image.
-template <int NP, int MODE, int S2, int PXC = -1, int PRO = 0>
+// IBW: the IN-backward partial sums of the output (data gradients; chunk = (tile, phase) as the statistics)
+template <int NP, int MODE, int S2, int PXC = -1, int PRO = 0, int IBW = 0>
 __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const float* __restrict__ src,
                                                               const _Float16* __restrict__ wh,
                                                               const _Float16* __restrict__ wl,
                                                               const float* __restrict__ rng,
                                                               const int* __restrict__ wexp, float* __restrict__ out,
                                                               Part* __restrict__ parts, const float* __restrict__ psc,
-                                                              const float* __restrict__ psh) {
+                                                              const float* __restrict__ psh, PhIbw ib) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * SP_PIX * 16 + 2 * 2 * 4 * SP_SLOT];
     __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 2 * SP_PROC : 4];  // [scale | shift][channel]
     _Float16* const Wn = smem;
@@ -318,6 +330,46 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                 acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
                 out[obase + (long long)opix(i, r) * a.Co + co0 + j * 32 + l32] = acc[i][j][r];
             }
+    if constexpr (IBW) {  // per WG column: sums over the wave's 64 pixels, then the 4 pixel waves in order
+        Sum2* ss = reinterpret_cast<Sum2*>(smem);  // [4][128]; the loop's last barrier freed the LDS
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ch = co0 + j * 32 + l32;
+            const float sc = ib.sc[(long long)n * a.Co + ch], sh = ib.sh[(long long)n * a.Co + ch];
+            float yv[2][16];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) yv[i][r] = ib.y[obase + (long long)opix(i, r) * a.Co + ch];
+            float sa = 0.f, sb = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float xh = fmaf(yv[i][r], sc, sh);
+                    const float g = acc[i][j][r] * act_grad(xh, ib.act);
+                    sa += g;
+                    sb = fmaf(g, xh, sb);
+                }
+            sa += __shfl_xor(sa, 32, 64);  // the same operand pair on both lanes: order-free
+            sb += __shfl_xor(sb, 32, 64);
+            if (kh == 0) ss[wm * SP_BN + py * 64 + j * 32 + l32] = Sum2{sa, sb};
+        }
+        __syncthreads();
+        if (tid < SP_BN) {
+            Sum2 t = ss[tid];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) {
+                t.a += ss[w * SP_BN + tid].a;
+                t.b += ss[w * SP_BN + tid].b;
+            }
+            if constexpr (MODE == 0)
+                ib.parts[((long long)n * 4 * a.tiles + tile * 4 + px * 2 + (tid >> 6)) * a.Co + co0 + (tid & 63)] = t;
+            else
+                ib.parts[((long long)n * a.tiles + tile) * a.Co + n0 + tid] = t;
+        }
+        return;
+    }
     if (!parts) return;  // kernel argument: block-uniform
     // per virtual column: count / mean / M2 / max / first argmax over the wave's 64 pixels, then the
     // four pixel waves merged in a fixed order; chunk = (tile, px, py) of the image
@@ -1007,10 +1059,10 @@ extern "C" int dcs_subpix_win(const dcs_conv_desc* dp, const float* src, const v
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
         hipLaunchKernelGGL((subpix_win_kernel<1, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
-                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr);
+                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr, PhIbw{});
     else
         hipLaunchKernelGGL((subpix_win_kernel<3, 0, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l, dp->rng_a, wexp,
-                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr);
+                           out, reinterpret_cast<Part*>(parts), nullptr, nullptr, PhIbw{});
     return check_launch("subpix_win");
 }
 
@@ -1031,10 +1083,10 @@ extern "C" int dcs_subpix_win_dgrad(const dcs_conv_desc* dp, const float* dy, co
     const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
     if (dp->mma == DCS_MMA_F16)
         hipLaunchKernelGGL((subpix_win_kernel<1, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
-                           nullptr, nullptr, nullptr);
+                           nullptr, nullptr, nullptr, PhIbw{});
     else
         hipLaunchKernelGGL((subpix_win_kernel<3, 1, 0>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx,
-                           nullptr, nullptr, nullptr);
+                           nullptr, nullptr, nullptr, PhIbw{});
     return check_launch("subpix_win_dgrad");
 }
 
@@ -1127,10 +1179,10 @@ extern "C" int dcs_stride2_win(const dcs_conv_desc* dp, const float* src, const 
     const bool k3 = dp->KH == 3;  // 3x3: the unreached (class, offset) pairs skipped; 4x4: every pair a tap
 #define DCS_S2_FWD(NP_, S2_, PRO_)                                                                                   \
     hipLaunchKernelGGL((subpix_win_kernel<NP_, 1, S2_, -1, PRO_>), dim3(blocks), dim3(SP_NT), 0, s, a, src, h, l,      \
-                       dp->rng_a, wexp, out, pp, pro_scale, pro_shift)
+                       dp->rng_a, wexp, out, pp, pro_scale, pro_shift, PhIbw{})
 #define DCS_S2_DG(NP_, S2_, PXC_)                                                                                    \
     hipLaunchKernelGGL((subpix_win_kernel<NP_, 0, S2_, PXC_>), dim3(blocks / 2), dim3(SP_NT), 0, s, a, src, h, l,     \
-                       dp->rng_a, wexp, out, nullptr, nullptr, nullptr)
+                       dp->rng_a, wexp, out, nullptr, nullptr, nullptr, PhIbw{})
     if (dp->parity == 0) {
         if (f16) {
             if (k3) { if (pro) DCS_S2_FWD(1, 1, 1); else DCS_S2_FWD(1, 1, 0); }
@@ -1222,3 +1274,60 @@ int s2_wgrad_launch(const dcs_conv_desc& d, const float* dy, const float* x, con
     return e ? -e : p.nsplit;
 }
 }  // namespace dcs
+
+namespace {
+// chunks per image of the fused IN-backward partial sums: the subpixel data gradient (MODE 1) writes one
+// per tile, the stride-2 data gradient (MODE 0) one per (tile, column phase, row phase)
+bool phase_ibw_geom(const dcs_conv_desc& d, int subpixel, SubArgs* a, int* nchunk) {
+    if (subpixel ? !subpix_dgrad_geom(d, a) : (d.parity != 1 || !s2_geom(d, a))) return false;
+    *nchunk = subpixel ? a->tiles : 4 * a->tiles;
+    return true;
+}
+}  // namespace
+
+extern "C" size_t dcs_phase_win_dgrad_inbwd_parts_size(const dcs_conv_desc* dp, int subpixel) {
+    SubArgs a;
+    int nch = 0;
+    if (!dp || !phase_ibw_geom(*dp, subpixel, &a, &nch)) return 0;
+    return (size_t)a.N * nch * a.Co * sizeof(Sum2);
+}
+
+extern "C" int dcs_phase_win_dgrad_inbwd(const dcs_conv_desc* dp, int subpixel, const float* dy, const void* w_hi,
+                                         const void* w_lo, const int* wexp, float* dx, const float* y,
+                                         const float* scale, const float* shift, int act, void* parts,
+                                         size_t parts_bytes, int* nchunk, void* stream) {
+    if (!dp || !dy || !w_hi || !w_lo || !wexp || !dx || !y || !scale || !shift || !parts || !nchunk)
+        return fail(DCS_E_INVALID, "phase_win_dgrad_inbwd: null pointer");
+    SubArgs a;
+    int nch = 0;
+    if (!phase_ibw_geom(*dp, subpixel, &a, &nch))
+        return fail(DCS_E_INVALID, "phase_win_dgrad_inbwd: a dcs_subpix_win_dgrad (subpixel = 1) or dcs_stride2_win "
+                                   "data-gradient (subpixel = 0, parity 1) descriptor expected");
+    if (act != DCS_ACT_AFFINE && act != DCS_ACT_RELU && act != DCS_ACT_LRELU)
+        return fail(DCS_E_INVALID, "phase_win_dgrad_inbwd: act must be DCS_ACT_AFFINE / _RELU / _LRELU");
+    if (parts_bytes < dcs_phase_win_dgrad_inbwd_parts_size(dp, subpixel))
+        return fail(DCS_E_WORKSPACE, "phase_win_dgrad_inbwd: parts buffer too small");
+    *nchunk = nch;
+    const PhIbw ib{y, scale, shift, reinterpret_cast<Sum2*>(parts), act};
+    const unsigned blocks = (unsigned)((long long)a.N * a.tiles * a.gy);
+    hipStream_t s = as_stream(stream);
+    const _Float16* h = reinterpret_cast<const _Float16*>(w_hi);
+    const _Float16* l = reinterpret_cast<const _Float16*>(w_lo);
+    const bool f16 = dp->mma == DCS_MMA_F16;
+    if (subpixel) {
+        if (f16) hipLaunchKernelGGL((subpix_win_kernel<1, 1, 0, -1, 0, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx, nullptr, nullptr, nullptr, ib);
+        else hipLaunchKernelGGL((subpix_win_kernel<3, 1, 0, -1, 0, 1>), dim3(blocks), dim3(SP_NT), 0, s, a, dy, h, l, dp->rng_a, wexp, dx, nullptr, nullptr, nullptr, ib);
+        return check_launch("subpix_win_dgrad_inbwd");
+    }
+    const bool k3 = dp->KH == 3;
+#define DCS_S2_DGI(NP_, S2_, PXC_)                                                                                   \
+    hipLaunchKernelGGL((subpix_win_kernel<NP_, 0, S2_, PXC_, 0, 1>), dim3(blocks / 2), dim3(SP_NT), 0, s, a, dy, h, l, \
+                       dp->rng_a, wexp, dx, nullptr, nullptr, nullptr, ib)
+    if (f16) {
+        if (k3) { DCS_S2_DGI(1, 1, 0); DCS_S2_DGI(1, 1, 1); } else { DCS_S2_DGI(1, 0, 0); DCS_S2_DGI(1, 0, 1); }
+    } else {
+        if (k3) { DCS_S2_DGI(3, 1, 0); DCS_S2_DGI(3, 1, 1); } else { DCS_S2_DGI(3, 0, 0); DCS_S2_DGI(3, 0, 1); }
+    }
+#undef DCS_S2_DGI
+    return check_launch("stride2_win_dgrad_inbwd");
+}

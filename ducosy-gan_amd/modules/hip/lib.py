@@ -81,6 +81,8 @@ SIGNATURES = {
     "dcs_pack_subpix_h3": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P]),
     "dcs_subpix_win_dgrad_ok": (c_int, [DP]),
     "dcs_subpix_win_dgrad": (c_int, [DP, P, P, P, P, P, P]),
+    "dcs_phase_win_dgrad_inbwd_parts_size": (c_size_t, [DP, c_int]),
+    "dcs_phase_win_dgrad_inbwd": (c_int, [DP, c_int, P, P, P, P, P, P, P, P, c_int, P, c_size_t, POINTER(c_int), P]),
     "dcs_stride2_win_ok": (c_int, [DP]),
     "dcs_stride2_win_parts_size": (c_size_t, [DP]),
     "dcs_stride2_win": (c_int, [DP, P, P, P, P, P, P, P, P, c_size_t, POINTER(c_int), P]),

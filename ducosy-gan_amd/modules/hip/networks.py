@@ -230,6 +230,19 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
     return out, saved
 
 
+def _dgrad_in_act(g, dy, w, H, Wd, y, st):
+    """dL/dy of a layer a = relu(IN(y)) whose activation feeds conv g: g's data gradient, then the IN +
+    ReLU backward; the backward's partial sums come from the data gradient's epilogue where the window
+    phase kernels run it (ConvGeom.dgrad(..., inbwd=...))."""
+    if _FUSE_IBW:
+        da, parts, nch = g.dgrad(dy, g.pack_dgrad(w), H, Wd, inbwd=(y, st, ACT_RELU))
+        if parts is not None:
+            return ops.in_act_backward_parts(da, y, st, ACT_RELU, parts, nch)
+    else:
+        da = g.dgrad(dy, g.pack_dgrad(w), H, Wd)
+    return ops.in_act_backward(da, y, st, ACT_RELU)
+
+
 def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, dx_from: int = 0,
                        params: Optional[Dict[str, torch.Tensor]] = None, slice_only: bool = False):
     """Returns (dx NHWC [N,H,W,dx_channels] or None, _GradSink keyed like gen_param_names: .get(k)
@@ -255,12 +268,12 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     del dpre
     # up2
     grads.put("up2.w", lambda o: L["up2"].wgrad(dy, Src.nhwc(S["au1"]), out=o))
-    da = L["up2"].dgrad(dy, L["up2"].pack_dgrad(W["up2.w"]), H // 2, Wd // 2)
-    # up1
-    dy = ops.in_act_backward(da, S["yu1"], su1, ACT_RELU)
+    # up1's input gradient: up2's data gradient with the IN + ReLU backward's partial sums fused where the
+    # window phase kernels run it
+    dy = _dgrad_in_act(L["up2"], dy, W["up2.w"], H // 2, Wd // 2, S["yu1"], su1)
     grads.put("up1.w", lambda o: L["up1"].wgrad(dy, Src.nhwc(S["h"]), out=o))
     dh = L["up1"].dgrad(dy, L["up1"].pack_dgrad(W["up1.w"]), H // 4, Wd // 4)
-    del dy, da
+    del dy
     # residual blocks
     for b in reversed(range(nb)):
         dh = _res_block_backward(L, W, b, S["blocks"][b], dh, use_cbam, grads)
@@ -269,12 +282,9 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     s2, s1, s0 = S["s2"], S["s1"], S["s0"]
     dy = ops.in_act_backward(dh, S["y2"], s2, ACT_RELU)
     grads.put("down2.w", lambda o: L["down2"].wgrad(dy, Src.nhwc(S["a1"]), out=o))
-    da = L["down2"].dgrad(dy, L["down2"].pack_dgrad(W["down2.w"]), H // 2, Wd // 2)
-    dy = ops.in_act_backward(da, S["y1"], s1, ACT_RELU)
+    dy = _dgrad_in_act(L["down2"], dy, W["down2.w"], H // 2, Wd // 2, S["y1"], s1)
     grads.put("down1.w", lambda o: L["down1"].wgrad(dy, Src.nhwc(S["a0"]), out=o))
-    da = L["down1"].dgrad(dy, L["down1"].pack_dgrad(W["down1.w"]), H, Wd)
-    dy = ops.in_act_backward(da, S["y0"], s0, ACT_RELU)
-    del da
+    dy = _dgrad_in_act(L["down1"], dy, W["down1.w"], H, Wd, S["y0"], s0)
     grads.put("stem.w", lambda o: L["stem"].wgrad(dy, S["xs"], out=o))
     dx = None
     if need_dx:

@@ -814,6 +814,8 @@ class ConvGeom:
         (dx, parts, nchunk) for in_act_backward_parts, else (dx, None, 0)."""
         if inbwd is not None:
             r = self._dgrad_inbwd(dy, wpack_d, H, W, inbwd)
+            if r is None:
+                r = self._phase_dgrad_inbwd(dy, wpack_d, H, W, inbwd)
             if r is not None:
                 return r
             return self.dgrad(dy, wpack_d, H, W, ci_count, addend), None, 0
@@ -929,6 +931,43 @@ class ConvGeom:
         if addend is not None:
             lib.call("dcs_scale_add", _p(out), _p(addend), 1.0, out.numel(), _stream())
         return out
+
+    def _phase_dgrad_inbwd(self, dy, wpack_d, H, W, inbwd):
+        """The up- / down-conv data gradient on the window phase kernels with the IN-backward partial sums
+        of its output fused (dcs_phase_win_dgrad_inbwd); None where they do not apply."""
+        sp = getattr(wpack_d, "_dcs_sp", None)
+        if sp is None or not dy.is_contiguous() or not (self.subpixel or self.stride == 2):
+            return None
+        N, Ho, Wo, Co = dy.shape
+        d = lib.ConvDesc()
+        d.N, d.Hs, d.Ws, d.Cs = N, Ho, Wo, Co
+        d.s_n, d.s_c, d.s_h, d.s_w = Ho * Wo * Co, 1, Wo * Co, Co
+        d.csplit = Co
+        d.up, d.pad_mode = 1, DCS_PAD_ZERO
+        d.ldb, d.pro_act, d.epi_act = wpack_d.shape[1], ACT_NONE, ACT_NONE
+        d.mma = _fallback() if _h3() else _MMA
+        _set_mma(d, dy, None, _wrng(wpack_d), wpack_d)
+        d.korder = lib.KORDER_TAP
+        d.Co = self.cin
+        if self.subpixel:
+            d.KH = d.KW = 4
+            d.stride, d.parity, d.pt, d.pl = 2, 0, 1, 1
+        else:
+            d.KH = d.KW = self.k
+            d.stride, d.parity, d.pt, d.pl = 2, 1, self.pads[0], self.pads[1]
+        d.Ho, d.Wo = H, W
+        self._phase_mma(d)
+        sub = 1 if self.subpixel else 0
+        nb = lib.query("dcs_phase_win_dgrad_inbwd_parts_size", ctypes.byref(d), sub)
+        if nb == 0:
+            return None
+        y, st, act = inbwd
+        out = torch.empty(N, H, W, self.cin, device=dy.device, dtype=torch.float32)
+        parts = torch.empty(nb // 4, device=dy.device, dtype=torch.float32)
+        nchunk = ctypes.c_int(0)
+        lib.call("dcs_phase_win_dgrad_inbwd", ctypes.byref(d), sub, _p(dy), _p(sp[0]), _p(sp[1]), _p(sp[2]), _p(out),
+                 _p(y), _p(st.scale), _p(st.shift), act, _p(parts), nb, ctypes.byref(nchunk), _stream())
+        return out, parts, nchunk.value
 
     def _dgrad_inbwd(self, dy, wpack_d, H, W, inbwd):
         h3 = getattr(wpack_d, "_dcs_h3", None)

@@ -268,6 +268,17 @@ int dcs_subpix_win_dgrad(const dcs_conv_desc* d, const float* dy, const void* w_
  * parity 1: data gradient, Ho = 2 Hs, Co % 64 == 0), planes from dcs_pack_subpix_h3 kind 3 / 2 (3x3) or
  * 4 / 5 (4x4).  The forward takes the rows pass's prologue (d.pro_act AFFINE / RELU / LRELU with
  * pro_scale / pro_shift [N][Cs], Cs <= 512): a = act(y * scale + shift) staged, zero in the padding. */
+/* Either data gradient (subpixel = 1: dcs_subpix_win_dgrad's descriptor and planes; 0: dcs_stride2_win's
+ * parity-1 descriptor and planes) with the InstanceNorm backward's partial sums of its output fused, for
+ * dx = da of a layer a = act(InstanceNorm(y)) (the down-convs' and up2's inputs): per (chunk, channel)
+ * sum g and sum g * xhat, g = da * act'(xhat), xhat = y * scale + shift, into parts (Sum2 {float a, b}
+ * [N][*nchunk][Co], dcs_phase_win_dgrad_inbwd_parts_size bytes) for dcs_in_act_backward_parts;
+ * act DCS_ACT_AFFINE / _RELU / _LRELU, y NHWC like dx. */
+size_t dcs_phase_win_dgrad_inbwd_parts_size(const dcs_conv_desc* d, int subpixel);
+int dcs_phase_win_dgrad_inbwd(const dcs_conv_desc* d, int subpixel, const float* dy, const void* w_hi,
+                              const void* w_lo, const int* wexp, float* dx, const float* y, const float* scale,
+                              const float* shift, int act, void* parts, size_t parts_bytes, int* nchunk,
+                              void* stream);
 int dcs_stride2_win_ok(const dcs_conv_desc* d);
 size_t dcs_stride2_win_parts_size(const dcs_conv_desc* d);
 int dcs_stride2_win(const dcs_conv_desc* d, const float* src, const float* pro_scale, const float* pro_shift,

@@ -16,6 +16,7 @@ the same fp32 operands:
     IN + LeakyReLU staged as a prologue) on the same kernels: forward + statistics over the source's
     parity classes, data gradient over dx's, to the same bound;
   * the weight gradients of those stride-2 layers on the rolling class-window kernel, to the same bound;
+  * the data gradients with the IN-backward partial sums fused equal the separate passes;
   * the rows pass on the same pack (the phase planes removed) agrees to its own bound, and the
     batched pack (ops.prepack) equals the per-pack launches bit for bit.
 Tolerances written per check below."""
@@ -242,6 +243,33 @@ def test_stride2_wgrad_vs_fp64(ops, mode, k, cin, cout, N, H, W, pro):
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dw = g.wgrad(dyd, ops.Src.nhwc(yd), pro=prod)
     assert _relmax(dw, ref) <= (1e-5 if mode == "f16x3" else 2e-3)  # weight gradients in the step's mode
+
+
+@pytest.mark.parametrize("layer", ["up2", "up1", "down1", "down2"])
+def test_phase_dgrad_fused_in_backward(ops, layer):
+    """The phase kernels' data gradient with the IN + ReLU backward's partial sums fused
+    (dcs_phase_win_dgrad_inbwd -> in_act_backward_parts) equals the data gradient followed by the
+    separate IN backward (in_act_backward), and the data gradient itself is bit-identical."""
+    from modules.hip.lib import ACT_RELU, DCS_PAD_ZERO
+    ops.set_mma("f16x3")
+    cin, cout, H, W, g = {"up2": (128, 64, 32, 32, None), "up1": (256, 128, 16, 16, None),
+                          "down1": (64, 128, 64, 64, 1), "down2": (128, 256, 32, 32, 1)}[layer]
+    geo = _geom(ops, cin, cout) if g is None else _s2(ops, cin, cout)
+    N = 2
+    w = (rnd((cout, cin, 3, 3), 102, "w") * 0.05).float().to(DEV)
+    wd = geo.pack_dgrad(w)
+    assert getattr(wd, "_dcs_sp", None) is not None
+    Ho, Wo = (2 * H, 2 * W) if g is None else (H // 2, W // 2)
+    dy = rnd((N, Ho, Wo, cout), 103, "dy").float().to(DEV)
+    y = rnd((N, H, W, cin), 104, "y").float().to(DEV)
+    st = ops.in_stats(y)
+    dx, parts, nch = geo.dgrad(dy, wd, H, W, inbwd=(y, st, ACT_RELU))
+    assert parts is not None and nch > 0
+    fused = ops.in_act_backward_parts(dx, y, st, ACT_RELU, parts, nch)
+    dx0 = geo.dgrad(dy, wd, H, W)
+    assert torch.equal(dx, dx0)
+    sep = ops.in_act_backward(dx0, y, st, ACT_RELU)
+    torch.testing.assert_close(fused, sep, rtol=1e-4, atol=1e-5 * float(sep.abs().max()))
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
