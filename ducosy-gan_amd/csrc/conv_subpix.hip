@@ -731,7 +731,6 @@ __global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const fl
                                                              const float* __restrict__ psc,
                                                              const float* __restrict__ psh, float* __restrict__ ws) {
     __shared__ __attribute__((aligned(16))) _Float16 smem[6 * S2W_XROW + 2 * S2W_DROW];
-    __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 64 : 4];  // the ci block's scale | shift
     _Float16* const Xr = smem;                 // [6 rows][class][2 planes][65 px][32 ci]
     _Float16* const Dy = smem + 6 * S2W_XROW;  // [2][2 planes][64 px][64 co]
 
@@ -754,12 +753,16 @@ __global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const fl
 
     const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
     const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+    // PRO: the scale / shift of this thread's 8 source channels (every unit of a thread has the same
+    // 8-channel group: unit index % 4 == tid % 4), kept in registers
+    float psv[PRO ? 8 : 1], pbv[PRO ? 8 : 1];
     if constexpr (PRO) {
-        if (tid < 32) {
-            pro_s[tid] = psc[(long long)n * C + ci0 + tid];
-            pro_s[32 + tid] = psh[(long long)n * C + ci0 + tid];
+        const int c0 = ci0 + 8 * (tid & 3);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            psv[k] = psc[(long long)n * C + c0 + k];
+            pbv[k] = psh[(long long)n * C + c0 + k];
         }
-        __syncthreads();
     }
 
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
@@ -806,9 +809,6 @@ __global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const fl
             const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
-            if constexpr (PRO) {  // the prologue applies inside the image only
-                if (!(ok && xoff[q] >= 0)) { v0 = u32x4{0, 0, 0, 0}; v1 = u32x4{0, 0, 0, 0}; }
-            }
             __builtin_memcpy(&xr[slot][q][0], &v0, 16);
             __builtin_memcpy(&xr[slot][q][1], &v1, 16);
         }
@@ -825,13 +825,12 @@ __global__ __launch_bounds__(S2W_NT, 1) void s2_wgrad_kernel(S2WArgs a, const fl
         for (int q = 0; q < S2W_XU; ++q) {
             if (xls[q] >= 0) {
                 float4 v0 = xr[rs][q][0], v1 = xr[rs][q][1];
-                if constexpr (PRO) {
-                    if (ok && xoff[q] >= 0) {
-                        const int c0 = 8 * (tid + q * S2W_NT & 3);
-                        auto f = [&](float v, int c) { return act_apply(fmaf(v, pro_s[c], pro_s[32 + c]), a.pro_act); };
-                        v0 = make_float4(f(v0.x, c0), f(v0.y, c0 + 1), f(v0.z, c0 + 2), f(v0.w, c0 + 3));
-                        v1 = make_float4(f(v1.x, c0 + 4), f(v1.y, c0 + 5), f(v1.z, c0 + 6), f(v1.w, c0 + 7));
-                    }
+                if constexpr (PRO) {  // the prologue applies inside the image only (0 in the padding); the
+                    // selection sits here, not after the load, so the row prefetch is not waited on early
+                    const bool in = ok && xoff[q] >= 0;
+                    auto f = [&](float v, int k) { return in ? act_apply(fmaf(v, psv[k], pbv[k]), a.pro_act) : 0.f; };
+                    v0 = make_float4(f(v0.x, 0), f(v0.y, 1), f(v0.z, 2), f(v0.w, 3));
+                    v1 = make_float4(f(v1.x, 4), f(v1.y, 5), f(v1.z, 6), f(v1.w, 7));
                 }
                 f16x8 hi, lo;
                 split8h(v0, v1, bsc, hi, lo);

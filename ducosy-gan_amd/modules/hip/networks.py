@@ -66,6 +66,7 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
 # the InstanceNorm backward's partial sums of each residual block's first IN fused into the data
 # gradient that produces its input gradient (window path); "0" = separate partial-sum pass (A/B)
 _FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
+_PRO_DOWN = os.environ.get("DUCOSY_PRO_DOWN", "1") == "1"  # the down-convs' source activation as a prologue
 
 # parameter gradients written in place into freshly zeroed .grad buffers; "0" = always through autograd (A/B)
 _GRAD_SINK = os.environ.get("DUCOSY_GRAD_SINK", "1") == "1"
@@ -186,6 +187,24 @@ def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
     return res.dgrad(dy1, res.pack_dgrad(W[f"r{b}.c1.w"]), H, Wd, addend=dout)
 
 
+def _down_forward(g, y, st, wpack):
+    """Down-conv over a = relu(IN(y)): with the prologue staged by the window phase kernels (a is not
+    materialised: returns None for it), else over a = in_apply(y)."""
+    if g.s2win and _PRO_DOWN and st.xmax is not None:
+        ops.attach_act_range(st, ACT_RELU)
+        out, so = g.forward_in_stats(Src.nhwc(y), wpack, pro=(st.scale, st.shift, ACT_RELU), want_max=True)
+        return out, so, None
+    a = ops.in_apply(y, st, ACT_RELU)
+    out, so = g.forward_in_stats(Src.nhwc(a), wpack, want_max=True)
+    return out, so, a
+
+
+def _down_wgrad(g, dy, y, st, a, o):
+    if a is None:
+        return g.wgrad(dy, Src.nhwc(y), pro=(st.scale, st.shift, ACT_RELU), out=o)
+    return g.wgrad(dy, Src.nhwc(a), out=o)
+
+
 def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[torch.Tensor],
                       nb: int, use_cbam: bool, keep: bool):
     """x: NCHW image (or full concat input); x2: optional NCHW mask channels (concat fused).
@@ -205,11 +224,11 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
         pk[f"r{b}.c2.w"] = L["res"].pack_fwd(W[f"r{b}.c2.w"])
     N, H, Wd = stem_src.N, stem_src.H, stem_src.W
     # every conv followed by an InstanceNorm returns its statistics (fused into the conv epilogue)
-    y0, s0 = L["stem"].forward_in_stats(stem_src, pk["stem.w"])
-    a0 = ops.in_apply(y0, s0, ACT_RELU)
-    y1, s1 = L["down1"].forward_in_stats(Src.nhwc(a0), pk["down1.w"])
-    a1 = ops.in_apply(y1, s1, ACT_RELU)
-    y2, s2 = L["down2"].forward_in_stats(Src.nhwc(a1), pk["down2.w"])
+    y0, s0 = L["stem"].forward_in_stats(stem_src, pk["stem.w"], want_max=True)
+    # the down-convs take relu(IN(y)) of their source as a staged prologue where the window phase
+    # kernels run them: the activation is never written (its range record from the IN statistics)
+    y1, s1, a0 = _down_forward(L["down1"], y0, s0, pk["down1.w"])
+    y2, s2, a1 = _down_forward(L["down2"], y1, s1, pk["down2.w"])
     h = ops.in_apply(y2, s2, ACT_RELU)
     blocks = []
     for b in range(nb):
@@ -281,9 +300,9 @@ def generator_backward(S, dout: torch.Tensor, need_dx: bool, dx_channels: int, d
     # x0 = relu(IN(y2))
     s2, s1, s0 = S["s2"], S["s1"], S["s0"]
     dy = ops.in_act_backward(dh, S["y2"], s2, ACT_RELU)
-    grads.put("down2.w", lambda o: L["down2"].wgrad(dy, Src.nhwc(S["a1"]), out=o))
+    grads.put("down2.w", lambda o: _down_wgrad(L["down2"], dy, S["y1"], s1, S["a1"], o))
     dy = _dgrad_in_act(L["down2"], dy, W["down2.w"], H // 2, Wd // 2, S["y1"], s1)
-    grads.put("down1.w", lambda o: L["down1"].wgrad(dy, Src.nhwc(S["a0"]), out=o))
+    grads.put("down1.w", lambda o: _down_wgrad(L["down1"], dy, S["y0"], s0, S["a0"], o))
     dy = _dgrad_in_act(L["down1"], dy, W["down1.w"], H, Wd, S["y0"], s0)
     grads.put("stem.w", lambda o: L["stem"].wgrad(dy, S["xs"], out=o))
     dx = None

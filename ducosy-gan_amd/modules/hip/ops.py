@@ -165,6 +165,10 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
     channel) prologue) for an NHWC tensor: the f16x3 kernels reduce them to the operand's power-of-two
     scale.  Cached on the tensor object per (version, prologue), so the forward, data-gradient and
     weight-gradient passes over one activation or gradient compute it once."""
+    if pro is not None:  # a record from the IN statistics (attach_act_range): no pass over t
+        ar = getattr(pro[0], "_dcs_act_rng", None)
+        if ar is not None and ar[0] == pro[2] and ar[1] is pro[1]:
+            return ar[2]
     cached = getattr(t, "_dcs_rng", None)
     if cached is not None and cached[0] == t._version and cached[1] is (pro[0] if pro else None) \
             and cached[2] == (pro[2] if pro else ACT_NONE) and _rng_valid(cached):
@@ -175,6 +179,16 @@ def range_rec(t: torch.Tensor, pro: Optional[Tuple[torch.Tensor, torch.Tensor, i
              _p(pro[1]) if pro else None, pro[2] if pro else ACT_NONE, _p(parts), _stream())
     t._dcs_rng = (t._version, pro[0] if pro else None, pro[2] if pro else ACT_NONE, parts)
     return parts
+
+
+def attach_act_range(st: "INStats", act: int) -> None:
+    """The range record of a = act(y * scale + shift) from the IN statistics (per (image, channel) max of
+    y, scale > 0): max |a| = max(0, xmax * scale + shift) for ReLU, attached to st.scale for range_rec,
+    so a consumer staging a as a prologue reads no extra pass over y."""
+    assert act == ACT_RELU and st.xmax is not None
+    rec = torch.zeros(lib.RANGE_PARTS, device=st.scale.device, dtype=torch.float32)
+    rec[:1] = torch.clamp(torch.addcmul(st.shift, st.xmax, st.scale), min=0).amax().reshape(1)
+    st.scale._dcs_act_rng = (act, st.shift, rec)
 
 
 def _out_rng(out: torch.Tensor):
