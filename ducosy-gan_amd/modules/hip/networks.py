@@ -66,7 +66,9 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
 # the InstanceNorm backward's partial sums of each residual block's first IN fused into the data
 # gradient that produces its input gradient (window path); "0" = separate partial-sum pass (A/B)
 _FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
-_PRO_DOWN = os.environ.get("DUCOSY_PRO_DOWN", "1") == "1"  # the down-convs' source activation as a prologue
+# the down-convs' source IN + ReLU staged as a prologue of their forward and weight gradient instead of
+# materialised by in_apply: "1" measured 1.5 ms per step slower (profiles/r04an, same box), so off
+_PRO_DOWN = os.environ.get("DUCOSY_PRO_DOWN", "0") == "1"
 
 # parameter gradients written in place into freshly zeroed .grad buffers; "0" = always through autograd (A/B)
 _GRAD_SINK = os.environ.get("DUCOSY_GRAD_SINK", "1") == "1"
