@@ -615,6 +615,72 @@ __global__ __launch_bounds__(256) void cb_bwd_apply4_kernel(const float* __restr
     range_note(rng, absmax4(o));  // every lane
 }
 
+// b5, multi-pixel float4 form (256 % (C / 4) == 0, the block's PX * 256 / (C / 4) pixels inside one image):
+// a thread keeps its 4 channels' tables (scale, shift, channel attention, argmax, coefficients) in
+// registers over PX pixels, so the per-image table loads and the range atomics drop by PX against
+// cb_bwd_apply4_kernel; the same arithmetic per element
+template <int PX>
+__global__ __launch_bounds__(256) void cb_bwd_apply4x_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                             const float* __restrict__ sc, const float* __restrict__ sh,
+                                                             const float* __restrict__ ca, const float* __restrict__ sa,
+                                                             const float* __restrict__ dsin, const int* __restrict__ sarg,
+                                                             const int* __restrict__ yarg, const Sum3* __restrict__ coef,
+                                                             int HW, int C, float* __restrict__ dy, float* __restrict__ rng) {
+    const int C4 = C >> 2;
+    const int ppb = 256 / C4;  // pixels per pass
+    const int c4 = threadIdx.x % C4, pl = threadIdx.x / C4;
+    const int pp0 = blockIdx.x * ppb * PX;
+    const int n = pp0 / HW;
+    const int nc = n * C + 4 * c4;
+    const float4 s = *reinterpret_cast<const float4*>(sc + nc);
+    const float4 b = *reinterpret_cast<const float4*>(sh + nc);
+    const float4 a = *reinterpret_cast<const float4*>(ca + nc);
+    const int4 ya = *reinterpret_cast<const int4*>(yarg + nc);
+    const float4 k0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc));
+    const float4 k1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc) + 4);
+    const float4 k2 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(coef + nc) + 8);
+    const float rC = 1.f / (float)C;
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        const int pp = pp0 + k * ppb + pl;
+        const int p = pp - n * HW;
+        const int i4 = pp * C4 + c4;
+        const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+        const float4 dv = reinterpret_cast<const float4*>(dout)[i4];
+        const float g = sa[pp];
+        const float2 ds = reinterpret_cast<const float2*>(dsin)[pp];
+        const int am = sarg[pp] - 4 * c4;
+        const float d0 = ds.x * rC;
+        float4 o;
+#define DCS_APPLY_LANE(X, K, KA, KB, KC)                      \
+    {                                                         \
+        const float z = fmaf(yv.X, s.X, b.X);                 \
+        float dzc = fmaf(dv.X, g, d0);                        \
+        if (am == K) dzc += ds.y;                             \
+        float dz = dzc * a.X;                                 \
+        if (ya.X == p) dz += KC;                              \
+        o.X = s.X * (dz - KA - z * KB);                       \
+    }
+        DCS_APPLY_LANE(x, 0, k0.x, k0.y, k0.z)
+        DCS_APPLY_LANE(y, 1, k0.w, k1.x, k1.y)
+        DCS_APPLY_LANE(z, 2, k1.z, k1.w, k2.x)
+        DCS_APPLY_LANE(w, 3, k2.y, k2.z, k2.w)
+#undef DCS_APPLY_LANE
+        reinterpret_cast<float4*>(dy)[i4] = o;
+        m = fmaxf(m, absmax4(o));
+    }
+    range_note(rng, m);
+}
+
+static inline bool cb_apply_px() {  // DCS_CB_APPLY_PX=0: the one-pixel apply (A/B)
+    static const bool on = [] {
+        const char* e = getenv("DCS_CB_APPLY_PX");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static inline int cb_chunks(int N, int HW) {
     int want = (int)cdiv(1024, N);
     int maxc = (int)cdiv(HW, 64);
@@ -744,7 +810,13 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     if ((e = check_launch("cb_bwd_dw_reduce"))) return e;
     if ((e = range_zero(rng, s))) return e;
     const long long total = P * C;
-    if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31)) {  // C % 4 == 0 checked above
+    const int C4 = C / 4;
+    constexpr int APX = 4;  // pixels per thread of the multi-pixel apply
+    if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31) && C4 <= 256 && 256 % C4 == 0 &&
+        HW % (APX * (256 / C4)) == 0 && cb_apply_px()) {
+        hipLaunchKernelGGL(cb_bwd_apply4x_kernel<APX>, dim3((unsigned)(P / (APX * (256 / C4)))), dim3(256), 0, s, dout,
+                           y, scale, shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, dy, rng);
+    } else if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31)) {  // C % 4 == 0 checked above
         const int total4 = (int)(total / 4);
         hipLaunchKernelGGL(cb_bwd_apply4_kernel, dim3((unsigned)cdiv(total4, 256)), dim3(256), 0, s, dout, y, scale,
                            shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, total4, dy, rng);
