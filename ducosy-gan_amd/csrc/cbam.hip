@@ -284,6 +284,42 @@ __global__ __launch_bounds__(256) void cb_bwd_dsa_kernel(const float* __restrict
     }
 }
 
+// b1 for C == 256 (one float4 per lane): a wave takes PX pixels of one image (HW % PX == 0) with its
+// lane's scale / shift / attention in registers and every pixel's loads issued together; per pixel
+// the same sums in the same order as cb_bwd_dsa_kernel
+template <int PX>
+__global__ __launch_bounds__(256) void cb_bwd_dsa64x_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ ca, const float* __restrict__ sa,
+                                                            int HW, long long P, float* __restrict__ dpre) {
+    const long long p0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * PX;
+    const int lane = threadIdx.x & 63;
+    if (p0 >= P) return;  // wave-uniform; P % PX == 0
+    const int n = (int)(p0 / HW);
+    const float4 s = reinterpret_cast<const float4*>(sc + (long long)n * 256)[lane];
+    const float4 b = reinterpret_cast<const float4*>(sh + (long long)n * 256)[lane];
+    const float4 a = reinterpret_cast<const float4*>(ca + (long long)n * 256)[lane];
+    float4 v[PX], d[PX];
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        v[k] = reinterpret_cast<const float4*>(y + (p0 + k) * 256)[lane];
+        d[k] = reinterpret_cast<const float4*>(dout + (p0 + k) * 256)[lane];
+    }
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        float acc = 0.f;
+        acc = fmaf(d[k].x, fmaf(v[k].x, s.x, b.x) * a.x, acc);
+        acc = fmaf(d[k].y, fmaf(v[k].y, s.y, b.y) * a.y, acc);
+        acc = fmaf(d[k].z, fmaf(v[k].z, s.z, b.z) * a.z, acc);
+        acc = fmaf(d[k].w, fmaf(v[k].w, s.w, b.w) * a.w, acc);
+        acc = wave_sum(acc);
+        if (lane == 0) {
+            const float g = sa[p0 + k];
+            dpre[p0 + k] = acc * g * (1.f - g);
+        }
+    }
+}
+
 // b2: dsin[q][ch] = sum_t wsa[ch][t] * dpre[q - (t - r)]  (adjoint of the zero-padded conv)
 __global__ void cb_bwd_dsin_kernel(const float* __restrict__ dpre, const float* __restrict__ wsa, int H, int W, int ksa,
                                    long long P, float* __restrict__ dsin) {
@@ -673,7 +709,7 @@ __global__ __launch_bounds__(256) void cb_bwd_apply4x_kernel(const float* __rest
     range_note(rng, m);
 }
 
-static inline bool cb_apply_px() {  // DCS_CB_APPLY_PX=0: the one-pixel apply (A/B)
+static inline bool cb_apply_px() {  // DCS_CB_APPLY_PX=0: the one-pixel apply and dsa passes (A/B)
     static const bool on = [] {
         const char* e = getenv("DCS_CB_APPLY_PX");
         return !(e && e[0] == '0');
@@ -780,8 +816,13 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     const int HW = H * W;
     // one wave per pixel: the 16-lane form (4 pixels per wave, 4 quads per wave) measured 104 vs
     // 96 us per 16-image launch here (a read-only pass wants more loads in flight per wave)
-    hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca, sa,
-                       HW, C, P, w.dpre);
+    constexpr int DPX = 4;  // pixels per wave of the C == 256 form
+    if (C == 256 && HW % DPX == 0 && cb_apply_px())
+        hipLaunchKernelGGL(cb_bwd_dsa64x_kernel<DPX>, dim3((unsigned)cdiv(P, 4 * DPX)), dim3(256), 0, s, dout, y, scale,
+                           shift, ca, sa, HW, P, w.dpre);
+    else
+        hipLaunchKernelGGL(cb_bwd_dsa_kernel, dim3((unsigned)cdiv(P, 4)), dim3(256), 0, s, dout, y, scale, shift, ca, sa,
+                           HW, C, P, w.dpre);
     int e = check_launch("cb_bwd_dsa");
     if (e) return e;
     hipLaunchKernelGGL(cb_bwd_dsin_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, w.dpre, wsa, H, W, ksa, P,
