@@ -148,6 +148,8 @@ def replicas_identical(flats) -> bool:
     c = replica_checksums(flats)
     if world() == 1:
         return True
+    if dist.get_backend(_GROUP) == "gloo":  # gloo gathers host tensors only
+        c = c.cpu()
     got = [torch.empty_like(c) for _ in range(world())]
     dist.all_gather(got, c, group=_GROUP)
     return all(torch.equal(g, got[0]) for g in got)
