@@ -709,14 +709,6 @@ __global__ __launch_bounds__(256) void cb_bwd_apply4x_kernel(const float* __rest
     range_note(rng, m);
 }
 
-static inline bool cb_apply_px() {  // DCS_CB_APPLY_PX=0: the one-pixel apply and dsa passes (A/B)
-    static const bool on = [] {
-        const char* e = getenv("DCS_CB_APPLY_PX");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 static inline int cb_chunks(int N, int HW) {
     int want = (int)cdiv(1024, N);
     int maxc = (int)cdiv(HW, 64);
@@ -817,7 +809,7 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     // one wave per pixel: the 16-lane form (4 pixels per wave, 4 quads per wave) measured 104 vs
     // 96 us per 16-image launch here (a read-only pass wants more loads in flight per wave)
     constexpr int DPX = 4;  // pixels per wave of the C == 256 form
-    if (C == 256 && HW % DPX == 0 && cb_apply_px())
+    if (C == 256 && HW % DPX == 0)
         hipLaunchKernelGGL(cb_bwd_dsa64x_kernel<DPX>, dim3((unsigned)cdiv(P, 4 * DPX)), dim3(256), 0, s, dout, y, scale,
                            shift, ca, sa, HW, P, w.dpre);
     else
@@ -854,7 +846,7 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     const int C4 = C / 4;
     constexpr int APX = 4;  // pixels per thread of the multi-pixel apply
     if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31) && C4 <= 256 && 256 % C4 == 0 &&
-        HW % (APX * (256 / C4)) == 0 && cb_apply_px()) {
+        HW % (APX * (256 / C4)) == 0) {
         hipLaunchKernelGGL(cb_bwd_apply4x_kernel<APX>, dim3((unsigned)(P / (APX * (256 / C4)))), dim3(256), 0, s, dout,
                            y, scale, shift, ca, sa, w.dsin, sarg, yargmax, w.coef, HW, C, dy, rng);
     } else if (total / 4 < (1LL << 31) && (long long)N * C < (1LL << 31)) {  // C % 4 == 0 checked above

@@ -64,17 +64,14 @@ def gen_param_names(nb: int, use_cbam: bool) -> Dict[str, str]:
 
 
 # the InstanceNorm backward's partial sums of each residual block's first IN fused into the data
-# gradient that produces its input gradient (window path); "0" = separate partial-sum pass (A/B)
-_FUSE_IBW = os.environ.get("DUCOSY_FUSE_IBW", "1") == "1"
-# the down-convs' source IN + ReLU staged as a prologue of their forward and weight gradient instead of
-# materialised by in_apply: "1" measured 1.5 ms per step slower (profiles/r04an, same box), so off
-_PRO_DOWN = os.environ.get("DUCOSY_PRO_DOWN", "0") == "1"
+# gradient that produces its input gradient (window path); False = separate partial-sum pass
+_FUSE_IBW = True
 
-# parameter gradients written in place into freshly zeroed .grad buffers; "0" = always through autograd (A/B)
-_GRAD_SINK = os.environ.get("DUCOSY_GRAD_SINK", "1") == "1"
+# parameter gradients written in place into freshly zeroed .grad buffers; False = always through autograd
+_GRAD_SINK = True
 # a second contribution to an existing .grad (the model called twice in one step) written to scratch
-# and added by one multi-tensor launch at the end of the backward; "0" = through autograd's adds
-_GRAD_ACC = os.environ.get("DUCOSY_GRAD_ACC", "1") == "1"
+# and added by one multi-tensor launch at the end of the backward; False = through autograd's adds
+_GRAD_ACC = True
 
 
 class _GradSink:
@@ -190,20 +187,15 @@ def _res_block_backward(L, W, b, blk, dout, use_cbam, grads):
 
 
 def _down_forward(g, y, st, wpack):
-    """Down-conv over a = relu(IN(y)): with the prologue staged by the window phase kernels (a is not
-    materialised: returns None for it), else over a = in_apply(y)."""
-    if g.s2win and _PRO_DOWN and st.xmax is not None:
-        ops.attach_act_range(st, ACT_RELU)
-        out, so = g.forward_in_stats(Src.nhwc(y), wpack, pro=(st.scale, st.shift, ACT_RELU), want_max=True)
-        return out, so, None
+    """Down-conv over a = relu(IN(y)), materialised by in_apply.  (Staging the IN + ReLU as a
+    prologue of the down-conv's forward and weight gradient instead was measured 1.5 ms per step
+    slower, profiles/r04an/, and removed.)"""
     a = ops.in_apply(y, st, ACT_RELU)
-    out, so = g.forward_in_stats(Src.nhwc(a), wpack, want_max=True)
+    out, so = g.forward_in_stats(Src.nhwc(a), wpack)
     return out, so, a
 
 
 def _down_wgrad(g, dy, y, st, a, o):
-    if a is None:
-        return g.wgrad(dy, Src.nhwc(y), pro=(st.scale, st.shift, ACT_RELU), out=o)
     return g.wgrad(dy, Src.nhwc(a), out=o)
 
 
@@ -226,9 +218,7 @@ def generator_forward(W: Dict[str, torch.Tensor], x: torch.Tensor, x2: Optional[
         pk[f"r{b}.c2.w"] = L["res"].pack_fwd(W[f"r{b}.c2.w"])
     N, H, Wd = stem_src.N, stem_src.H, stem_src.W
     # every conv followed by an InstanceNorm returns its statistics (fused into the conv epilogue)
-    y0, s0 = L["stem"].forward_in_stats(stem_src, pk["stem.w"], want_max=True)
-    # the down-convs take relu(IN(y)) of their source as a staged prologue where the window phase
-    # kernels run them: the activation is never written (its range record from the IN statistics)
+    y0, s0 = L["stem"].forward_in_stats(stem_src, pk["stem.w"])
     y1, s1, a0 = _down_forward(L["down1"], y0, s0, pk["down1.w"])
     y2, s2, a1 = _down_forward(L["down2"], y1, s1, pk["down2.w"])
     h = ops.in_apply(y2, s2, ACT_RELU)

@@ -28,26 +28,28 @@ _MMA_NAMES = {"f32": lib.MMA_F32, "bf16": lib.MMA_BF16, "bf16x3": lib.MMA_BF16X3
 # default f16x3: fp32-class (max error vs float64 <= the exact-f32 MFMA path's on every layer,
 # tests/test_gpu_mma.py::test_bf16x6_error_matches_exact_f32, also for bf16x6) at half of bf16x6's MFMAs
 _MMA = _MMA_NAMES[os.environ.get("DUCOSY_MMA", "f16x3")]
+# Path selectors below are module constants, not environment switches: the tests flip them (e.g.
+# ops._WIN = False) to hold a fused path to the one it replaced.
 # the Generator head's forward by tap projection on the MFMA pipe in the fp16 modes
-# (csrc/conv_head.hip); "0" = the exact-f32 VALU kernel (A/B)
-_HEAD_PROJ = os.environ.get("DUCOSY_HEAD_PROJ", "1") == "1"
-_BPRE = os.environ.get("DUCOSY_BPRE", "1") == "1"  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
-_STEM = os.environ.get("DUCOSY_STEM", "1") == "1"  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)
-_PREPACK = os.environ.get("DUCOSY_PREPACK", "1") == "1"  # the step's weight packs in two batched launches
-_SUBWIN = os.environ.get("DUCOSY_SUBWIN", "1") == "1"  # up-conv forwards on the sub-pixel window kernel
-_SUBWIN_D = os.environ.get("DUCOSY_SUBWIN_DGRAD", "1") == "1"  # (diagnostic: their data gradients too)
-_S2WIN = os.environ.get("DUCOSY_S2WIN", "1") == "1"  # the down-convs on the same window phase kernels
+# (csrc/conv_head.hip); False = the exact-f32 VALU kernel
+_HEAD_PROJ = True
+_BPRE = True  # pre-split fp16 weight planes for the f16x3 / f16 rows pass
+_STEM = True  # the Generator stem on its MFMA kernel (csrc/conv_stem.hip)
+_PREPACK = True  # the step's weight packs in two batched launches
+_SUBWIN = True  # up-conv forwards on the sub-pixel window kernel
+_SUBWIN_D = True  # (diagnostic: their data gradients too)
+_S2WIN = True  # the down-convs on the same window phase kernels
 
 
-# residual convs in the slice-major K order (DCS_KORDER_SLICE); 0 = tap-major (A/B switch)
-# IN statistics fused into the conv epilogue (ConvGeom.forward_in_stats); "0" = separate pass (A/B)
-_FUSE_STATS = os.environ.get("DUCOSY_FUSE_STATS", "1") == "1"
-_KSLICE = os.environ.get("DUCOSY_KSLICE", "1") == "1"
+# residual convs in the slice-major K order (DCS_KORDER_SLICE); False = tap-major
+# IN statistics fused into the conv epilogue (ConvGeom.forward_in_stats); False = separate pass
+_FUSE_STATS = True
+_KSLICE = True
 # reflection fold of the stride-1 pad-1 data gradient in the conv epilogue (dcs_conv_dgrad_reflect);
-# "0" = padded-grid rows pass + dcs_reflect_fold (A/B)
-_FUSE_FOLD = os.environ.get("DUCOSY_FUSE_FOLD", "1") == "1"
-# f16x3 residual convs on the window kernel (csrc/conv_win.hip); "0" = the rows pass (A/B)
-_WIN = os.environ.get("DUCOSY_WIN", "1") == "1"
+# False = padded-grid rows pass + dcs_reflect_fold
+_FUSE_FOLD = True
+# f16x3 residual convs on the window kernel (csrc/conv_win.hip); False = the rows pass
+_WIN = True
 
 
 def _h3() -> bool:

@@ -37,9 +37,9 @@ LAMBDA_CA, LAMBDA_CR, LAMBDA_CE = 2.0, 1.5, 1.0                 # trainer.py:500
 
 # The step as an explicit schedule of the fused forward / backward functions and the fused loss
 # kernel (no autograd graph: no slice / cat backward fills and copies, no per-term scalar
-# arithmetic, no gradient adds); "0" = the autograd step over the same kernels (A/B, reference
+# arithmetic, no gradient adds); False = the autograd step over the same kernels (the reference
 # structure)
-_EXPLICIT_STEP = os.environ.get("DUCOSY_EXPLICIT_STEP", "1") == "1"
+_EXPLICIT_STEP = True
 
 # loss_G's output slots of the fused loss recipe (and the train_step dict keys)
 _G_TERMS = ("loss_G", "loss_GAN", "loss_cycle", "loss_id", "loss_grad_cycle", "loss_grad_id", "loss_ssim",

@@ -3,7 +3,8 @@
 Every tensor the product code allocates through torch.empty / empty_like / zeros / zeros_like /
 ones on the device (kernel outputs, padded dgrad buffers, split-K partial slabs, the per-stream
 workspaces) is carved out of a larger buffer whose 4 KiB on either side is filled with a canary
-byte.  One step of the two CycleGANs of config 5 (serial schedule) runs with every allocation guarded,
+byte.  Two steps of the two CycleGANs of config 5 (serial schedule) run with every allocation guarded
+(the second replays the recorded weight packs as the batched pack launches),
 in the f16x3, f16 and bf16x6 operand modes;
 afterwards every guard band must still hold the canary: no kernel stores outside the extent its
 host code allocated for it (the two-stream audit).
@@ -105,6 +106,9 @@ def test_no_store_outside_allocations(mode):
         torch.cuda.synchronize()
         ops._WS.clear()  # workspaces are re-created (guarded) inside the step
         with _Guarded() as g:
+            # two steps: the first allocates the packs and workspaces (guarded) and records the pack
+            # plans; the second replays them as the batched pack launches (ops.prepack)
+            run.train_step(batches)
             run.train_step(batches)
             torch.cuda.synchronize()
         assert len(g.bufs) > 100, len(g.bufs)
