@@ -14,7 +14,9 @@
 // K loop: 16 slices x 3 kernel rows (ty) = 48 k-tiles of 48 k; a k-tile is three 16-k sub-tiles
 // (tx = 0, 1, 2) of 2 x 2 blocks x 3 products (lo*hi, hi*lo, hi*hi) per wave.  One inner fp32
 // accumulation chain per slice (144 k), added to the running sum (two-level, as conv.hip).
-// 8 waves = 4 (pixels) x 2 (channels) of 64 x 64; one workgroup per CU (115 KB of LDS).
+// 8 waves = 4 (pixels) x 2 (channels) of 64 x 64; one workgroup per CU (115 KB of LDS).  The k-tile
+// schedule (LDS-DMA for B, one window unit in flight, fragments read ahead, staggered wave pairs) is
+// described at conv3_win_h3_kernel.
 #include "common.hpp"
 #include "conv_common.hpp"
 #include <type_traits>
@@ -27,7 +29,9 @@ constexpr int WIN_PIX = 520;             // window pixels for W <= 128: (256 / W
 // halves per B plane-slot: 128 rows x 16 k + 48 (96 B: the three tx slots of a row, written by
 // neighbouring lanes, land on distinct banks)
 constexpr int WIN_SLOT = 128 * 16 + 48;
-constexpr int WIN_UNITS = (2 * WIN_PIX + WIN_NT - 1) / WIN_NT;  // window (pixel, 8-channel half) units per thread
+// window staging units (pixel, 8-channel half) per thread: the interior columns only, (256 / W + 2) x W
+// pixels x 2 halves <= 1024 for W <= 128
+constexpr int WIN_UNITS = 2;
 
 struct WinArgs {
     int N, H, W, C, Co;  // source NHWC [N][H][W][C]; output NHWC [N][H][W][Co]
@@ -54,6 +58,18 @@ __device__ __forceinline__ int win_pix(int wm, int i, int r, int kh) {
 // B: (buffer, plane, tx, output-channel row, half)
 __device__ __forceinline__ int wb_off(int buf, int pl, int tx, int row, int h) {
     return (buf * 6 + pl * 3 + tx) * WIN_SLOT + row * 16 + 8 * (h ^ ((row >> 3) & 1));
+}
+
+// one global_load_lds_dwordx4: lane L's 16 bytes land at LDS byte address lds + 16 L.  Inline asm: a
+// compiler-emitted LDS-DMA makes hipcc wait for it before every later LDS read it cannot tell apart
+// from the DMA's destination.  The kernel retires these itself (s_waitcnt vmcnt before the barrier
+// that publishes the buffer); the compiler's own vmcnt waits only grow more conservative beside them.
+__device__ __forceinline__ void win_glds(const void* base, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
 }
 
 // IN statistics of the tile (as conv.hip rows_in_stats, BM 256 x BN 128): per column the tile's
@@ -182,6 +198,19 @@ __device__ __forceinline__ void win_ibw(const floatx16 (&acc)[2][2], const float
 
 // NP: products per fragment pair (3: f16x3, hi*lo + lo*hi + hi*hi; 1: f16, hi*hi with the hi planes only);
 // IBW: the InstanceNorm-backward partial sums of the output (data gradients without addend)
+//
+// Schedule of a k-tile (one barrier each), built so that the fragment reads run ahead of the MFMAs
+// that consume them within the 256-register budget of two waves per SIMD (128 of them the two-level
+// accumulators):
+//   * B by LDS-DMA (win_glds): tile tt + 1 is issued into the other buffer at the top of tile tt and
+//     retired (vmcnt) before tile tt's barrier, so no register holds B in flight;
+//   * the window of the next slice one staging unit per k-tile (units 0, 1 in kernel rows 0, 1): only
+//     one unit's eight floats are live at a time.  Only the window's interior columns are loaded (two
+//     units per thread); the halo columns are written by the units of source columns 1 and W - 2
+//     (reflection) or zeroed once (zero padding);
+//   * B fragments one tap ahead (tap tx + 1's read before tap tx's MFMAs, pinned by sched_barrier);
+//   * waves 4-7 (the partners of waves 0-3 on their SIMDs) store their staging unit at the top of the
+//     next k-tile instead of after their MFMAs, so the two waves of a SIMD are not in the same phase.
 template <int NP, bool IBW>
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, const float* __restrict__ src,
                                                                  const _Float16* __restrict__ wh,
@@ -191,9 +220,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                                                                  const float* __restrict__ addend,
                                                                  float* __restrict__ out, Part* __restrict__ parts,
                                                                  IbwArgs ib) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT];
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT + 8];
     _Float16* const Wn = smem;                               // [2][2][WIN_PIX][16]
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;        // [2][6][WIN_SLOT]
+    _Float16* const Wspare = Bs + 2 * 6 * WIN_SLOT;          // 16 bytes nobody reads
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -204,7 +234,6 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int W = a.W, WP = a.W + 2, C = a.C;
     const int K = 9 * C;                       // packed K (slice-major: (c/16)*144 + tap*16 + c%16)
     const int nslice = C / 16;
-    const int npix = (a.R + 2) * WP;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
@@ -214,84 +243,90 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
     const float asc = __builtin_ldexpf(1.f, ea);
 
-    // window staging units of this thread: (pixel, 8-channel half); the byte offset of the unit's
-    // source channel 0 (OOB_OFF-style sentinel -1 for zero padding / past the window)
-    int uoff[WIN_UNITS];
+    // window staging units of this thread: (pixel, 8-channel half) of the window's interior columns
+    // ((R + 2) x W pixels: 2 units per thread at W <= 128).  uoff: byte offset of the unit's source
+    // channel 0 (-1: zero padding); uwd: its window pixel (bits 0-15) and the halo pixel it also writes
+    // (bits 16-31), each + 1 (0: none)
+    const int nint = (a.R + 2) * W;
+    int uoff[WIN_UNITS], uwd[WIN_UNITS];
 #pragma unroll
     for (int q = 0; q < WIN_UNITS; ++q) {
         const int u = tid + q * WIN_NT;
-        const int wpix = u >> 1, h = u & 1;
+        const int ip = u >> 1, h = u & 1;
         uoff[q] = -1;
-        if (wpix < npix) {
-            const int wr = wpix / WP, wc = wpix - (wpix / WP) * WP;
-            int sy = y0 - 1 + wr, sx = wc - 1;
+        uwd[q] = 0;
+        if (ip < nint) {
+            const int wr = ip / W, sx = ip - wr * W;
+            int dup = -1;
+            int sy = y0 - 1 + wr;
             bool ok = true;
             if (a.reflect) {
                 sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
-                sx = sx < 0 ? -sx : (sx >= W ? 2 * W - 2 - sx : sx);
+                if (sx == 1) dup = wr * WP;                   // column -1 reflects column 1
+                else if (sx == W - 2) dup = wr * WP + W + 1;  // column W reflects column W - 2
             } else {
-                ok = sy >= 0 && sy < a.H && sx >= 0 && sx < W;
+                ok = sy >= 0 && sy < a.H;
             }
+            uwd[q] = (wr * WP + sx + 2) | ((dup + 1) << 16);
             if (ok) uoff[q] = (((n * a.H + sy) * W + sx) * C + 8 * h) * 4;
         }
     }
-    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
-    float4 wr_[WIN_UNITS][2];
-    auto win_load = [&](int s) {
-#pragma unroll
-        for (int q = 0; q < WIN_UNITS; ++q) {
-            const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
-            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
-            __builtin_memcpy(&wr_[q][0], &v0, 16);
-            __builtin_memcpy(&wr_[q][1], &v1, 16);
+    if (!a.reflect) {  // zero halo columns of both buffers and planes
+        for (int i = tid; i < 2 * 2 * (a.R + 2) * 2 * 2; i += WIN_NT) {
+            const int h = i & 1, side = (i >> 1) & 1, rest = i >> 2;
+            const int wr = rest % (a.R + 2), bp = rest / (a.R + 2);
+            *reinterpret_cast<f16x8*>(Wn + win_off(bp >> 1, bp & 1, wr * WP + side * (W + 1), h)) = f16x8{};
         }
-    };
-    auto win_store = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < WIN_UNITS; ++q) {
-            const int u = tid + q * WIN_NT;
-            const int wpix = u >> 1, h = u & 1;
-            if (wpix < npix) {
-                f16x8 hi, lo;
-                split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
-                *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wpix, h)) = hi;
-                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wpix, h)) = lo;
-            }
-        }
-    };
-    // B k-tile (slice s, kernel row ty): 2 planes x 128 rows x 48 k = 1536 16-byte chunks, 3 per
-    // thread; chunk q -> (plane, row, tx, half) with (tx, half) fastest (96 contiguous bytes of a row)
-    // per-thread chunk geometry, fixed for the whole loop: global element offset (minus the k-tile's
-    // k base) and LDS offset (minus the buffer's)
-    int bg[3], bl[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int q = tid + i * WIN_NT;
-        const int pl = q / 768, rem = q - pl * 768;
-        const int row = rem / 6, c6 = rem - (rem / 6) * 6;
-        bg[i] = pl * 0x40000000 + (n0 + row) * K + c6 * 8;  // bit 30: the lo plane
-        bl[i] = wb_off(0, pl, c6 >> 1, row, c6 & 1);
     }
-    uint4 br0, br1, br2;  // named (an array here was promoted to LDS)
-    auto b_ld = [&](int i, int kb) {
-        const int g = bg[i] & 0x3fffffff;
-        const _Float16* w = (bg[i] >> 30) ? wl : wh;
-        return *reinterpret_cast<const uint4*>(w + g + kb);
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    float4 wq_[2];  // the unit in flight
+    auto win_load_u = [&](int q, int s) {  // unconditional (clamped offset): see the k loop
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+        __builtin_memcpy(&wq_[0], &v0, 16);
+        __builtin_memcpy(&wq_[1], &v1, 16);
     };
-    auto b_load = [&](int t) {
-        const int s = t / 3, ty = t - 3 * (t / 3);
-        const int kb = s * 144 + ty * 48;
-        br0 = b_ld(0, kb);
-        br1 = b_ld(1, kb);
-        br2 = b_ld(2, kb);
+    // unconditional store (a unit past the window writes the spare slot): a store under a branch lets
+    // the compiler sink the unit's load into the branch, next to its use
+    auto win_store_u = [&](int q, int buf) {
+        const int h = (tid + q * WIN_NT) & 1;
+        const int wp = (uwd[q] & 0xffff) - 1, wd = (uwd[q] >> 16) - 1;
+        f16x8 hi, lo;
+        split8h(wq_[0], wq_[1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + win_off(buf, 0, wp, h) : Wspare) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + win_off(buf, 1, wp, h) : Wspare) = lo;
+        if (wd >= 0) {
+            *reinterpret_cast<f16x8*>(Wn + win_off(buf, 0, wd, h)) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + win_off(buf, 1, wd, h)) = lo;
+        }
     };
-    auto b_store = [&](int buf) {
-        const int boff = buf * 6 * WIN_SLOT;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[0]) = br0;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[1]) = br1;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[2]) = br2;
+
+    // B k-tile (slice s, kernel row ty) by LDS-DMA: 2 planes x 3 tx slots x 128 rows = 24 blocks of
+    // 1 KB (plane, tx slot, 32-row block), three per wave; a block's LDS image is lane-linear (lane L ->
+    // row L / 2, half position L % 2), so the wb_off swizzle goes on the source side: lane L fetches
+    // half (L % 2) ^ bit 3 of its row.  The lane part of the source offset is the same for the three
+    // blocks (bit 3 of the row is bit 3 of L / 2); the block part and the plane are wave-uniform.
+    unsigned dsu[3], ddst[3];
+    const _Float16* dbase[3];
+    const unsigned dlane = 2u * (unsigned)((n0 + (lane >> 1)) * K + 8 * ((lane & 1) ^ ((lane >> 4) & 1)));
+    {
+        const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int c = __builtin_amdgcn_readfirstlane(wid) * 3 + i, pl = c / 12, rem = c - pl * 12;
+            const int tx = rem >> 2, rb = rem & 3;
+            dsu[i] = 2u * (unsigned)(rb * 32 * K + tx * 16);
+            dbase[i] = pl ? wl : wh;
+            ddst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)((pl * 3 + tx) * WIN_SLOT + rb * 32 * 16));
+        }
+    }
+    auto b_dma = [&](int t, int buf) {  // B tile t into buffer buf
+        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
+        const unsigned kb = 2u * (unsigned)(s_ * 144 + ty_ * 48);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) win_glds(dbase[i], dlane + (dsu[i] + kb), ddst[i] + 2u * (unsigned)(buf * 6 * WIN_SLOT));
     };
 
     // window pixel of this lane's block-0 output pixel 2m (tap (0, 0) = the window's top-left); its
@@ -310,74 +345,94 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    // prologue: window of slice 0, B tile 0; B tile 1 in flight
-    win_load(0);
-    win_store(0);
-    b_load(0);
-    b_store(0);
+    // prologue: window of slice 0, B tile 0
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        win_load_u(q, 0);
+        win_store_u(q, 0);
+    }
+    b_dma(0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
     __syncthreads();
-    b_load(1);
 
-    // every global load below is unconditional (indices clamped at the end): a load under a branch
-    // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer, which here
-    // would expose the window loads' HBM latency at every k-tile's B store
+    // every global load below is unconditional (offsets clamped at the end): a load under a branch
+    // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer
     const int last = 3 * nslice - 1;
-    for (int s = 0; s < nslice; ++s) {
-        const int wbuf = s & 1;
-        win_load(s + 1 < nslice ? s + 1 : s);
+    auto kloop = [&](auto role_tag) {
+        constexpr int ROLE = decltype(role_tag)::value;
+        for (int s = 0; s < nslice; ++s) {
+            const int wbuf = s & 1;
+            const int sn = s + 1 < nslice ? s + 1 : s;
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty) {
-            const int tt = 3 * s + ty, bbuf = tt & 1;
-            // A fragments of window pixels wbe + ty * WP + 0 .. 3: block i at tap tx takes fragment tx + i
-            f16x8 fh[4], fl[4];
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                const int wpix = wbe + ty * WP + f;
-                fh[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
-                if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
-            }
-#pragma unroll
-            for (int tx = 0; tx < 3; ++tx) {
-                f16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    ah[i] = fh[tx + i];
-                    if constexpr (NP == 3) al[i] = fl[tx + i];
+            for (int ty = 0; ty < 3; ++ty) {
+                const int tt = 3 * s + ty, bbuf = tt & 1;
+                // staging of the next slice's window (buffer wbuf ^ 1: last read before the previous
+                // slice's last barrier): unit ty loaded here, stored after this k-tile's MFMAs (ROLE 0)
+                // or at the top of the next k-tile (ROLE 1)
+                if constexpr (ROLE == 1) {
+                    if (ty >= 1) win_store_u(ty - 1, wbuf ^ 1);
                 }
+                if (ty < WIN_UNITS) win_load_u(ty, sn);
+                // B tile tt + 1 into the other buffer (last read before the previous barrier); past the
+                // end a repeat nobody reads
+                b_dma(tt + 1 < last ? tt + 1 : last, bbuf ^ 1);
+                __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-tile
+                // A fragments of window pixels wbe + ty * WP + 0 .. 3: block i at tap tx takes fragment tx + i
+                f16x8 fh[4], fl[4];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int row = wn * 64 + j * 32 + l32;
-                    bh[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 0, tx, row, kh));
-                    if constexpr (NP == 3) bl[j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 1, tx, row, kh));
+                for (int f = 0; f < 4; ++f) {
+                    const int wpix = wbe + ty * WP + f;
+                    fh[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 0, wpix, kh));
+                    if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(wbuf, 1, wpix, kh));
                 }
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
+                // B fragments one tap ahead: tap tx + 1's are read before tap tx's MFMAs
+                f16x8 pbh[2][2], pbl[2][2];
+                auto rd_b = [&](int tx, int slot) {
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        if constexpr (NP == 3) {
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
-                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], t[i][j], 0, 0, 0);
-                        }
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                        const int row = wn * 64 + j * 32 + l32;
+                        pbh[slot][j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 0, tx, row, kh));
+                        if constexpr (NP == 3) pbl[slot][j] = *reinterpret_cast<const f16x8*>(Bs + wb_off(bbuf, 1, tx, row, kh));
                     }
+                };
+                rd_b(0, 0);
+#pragma unroll
+                for (int tx = 0; tx < 3; ++tx) {
+                    if (tx < 2) rd_b(tx + 1, (tx + 1) & 1);
+                    __builtin_amdgcn_sched_barrier(0);  // the reads stay ahead of this tap's MFMAs
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const f16x8 bh = pbh[tx & 1][j];
+                            if constexpr (NP == 3) {
+                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[tx + i], bh, t[i][j], 0, 0, 0);
+                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], pbl[tx & 1][j], t[i][j], 0, 0, 0);
+                            }
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], bh, t[i][j], 0, 0, 0);
+                        }
+                }
+                if constexpr (ROLE == 0) {
+                    // (below the MFMAs: hoisted into them, the split would wait for the unit's load there)
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (ty < WIN_UNITS) win_store_u(ty, wbuf ^ 1);
+                }
+                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
+                __syncthreads();
             }
-            // stage B tile tt + 1 (its loads issued one k-tile ago), issue tile tt + 2 (past the end:
-            // a repeat into a buffer nobody reads again)
-            b_store(bbuf ^ 1);
-            b_load(tt + 2 < last ? tt + 2 : last);
-            if (ty == 2) win_store(wbuf ^ 1);
-            __syncthreads();
+            // close the slice's accumulation chain (144 k)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] += t[i][j];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                }
         }
-        // close the slice's accumulation chain (144 k)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                acc[i][j] += t[i][j];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
-            }
-    }
+    };
+    if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
+    else kloop(std::integral_constant<int, 0>{});
 
     // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
     const int eab = -(ea + eb);
