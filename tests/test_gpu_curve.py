@@ -1,4 +1,4 @@
-"""Loss-curve parity: 50 training steps of CycleGANSystem (HIP, default bf16x6 operands) at
+"""Loss-curve parity: 50 training steps of CycleGANSystem (HIP, default f16x3 operands) at
 BASELINE config 1 (128x128, bs 2, 1 residual block, cin 3) against the reference's own step loop
 (modules/trainer.py:447-525, tests/golden/make_golden.py --curve) run at 1, 2, 3, 4, 6 and 8 torch
 threads.

@@ -1,11 +1,13 @@
 """Parity at the north-star sizes (512 x 512, 9 residual blocks, cin 3), every comparison against
 the CPU oracle (oracle/ref_torch.py, pinned to the reference by the golden fixtures):
-  * BASELINE config 2: Generator_A2B forward + backward at bs 2: every stage's activation (stem,
-    down1, down2, the nine residual blocks, up1, up2, output) within 1e-3 relative (max |err| /
-    max |ref|), every conv weight gradient and the image gradient within relative L2 5e-3, the CBAM
-    attention weights (channel MLP, spatial 7x7: max-pool routed, 98-parameter sums that cancel)
-    within 1.5e-2 (the exact-f32 MFMA path itself is at 2.8e-3 there, f16x3 7.7e-3, bf16x6 4.1e-3:
-    scripts/diag/fullsize_grad_modes.py);
+  * BASELINE config 2: Generator_A2B forward + backward at bs 2 against the oracle run in float64:
+    every stage's activation (stem, down1, down2, the nine residual blocks, up1, up2, output) within
+    1e-3 relative (max |err| / max |ref|), every parameter gradient, the CBAM attention weights
+    included, and the image gradient within relative L2 5e-3.  (The CBAM weight gradients are sums
+    over 2 x 128^2 pixels that cancel: against float64 the fp32 oracle itself is at 3.5e-3 there, the
+    exact-f32 MFMA path at 3.6e-3 and f16x3 at 3.9e-3, every other gradient at <= 1.2e-3;
+    scripts/diag/oracle_f64_floor.py, profiles/r05g/.  Against the fp32 oracle the two fp32
+    roundings added up to 7.7e-3.);
   * BASELINE config 3's loss kernels at bs 8 on planes the HIP Generator produced: every loss term
     of trainer.py:469-512 and its d/dpred, including the batch-coupled ContrastRegion mean / std
     (trainer.py:126-128) and ContrastEdge mean / std / top-10 % at k = 209,715 (trainer.py:170-180);
@@ -63,10 +65,10 @@ def test_fullsize_generator_stages_and_grads_vs_oracle():
     x, _, m = _inputs(seed, 0, n)
     dout = torch.from_numpy(prng.normal(seed, "dout", (n, 1, HW, HW), 0, 1e-3))
     # oracle: stages, then the backward of <out, dout>
-    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
-    xr = x.clone().requires_grad_(True)
-    st = orc.generator_stages(pr, torch.cat([xr, m], 1), NB, True)
-    (st["out"] * dout).sum().backward()
+    pr = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    xr = x.double().requires_grad_(True)
+    st = orc.generator_stages(pr, torch.cat([xr, m.double()], 1), NB, True)
+    (st["out"] * dout.double()).sum().backward()
     # HIP: the same network through the module, stages from the fused forward's saved state
     G = Generator(input_channels=CIN, num_residual_blocks=NB, use_cbam=True)
     G.load_state_dict(p)
@@ -98,7 +100,7 @@ def test_fullsize_generator_stages_and_grads_vs_oracle():
         if v.dim() == 1 and k != f"model.{10 + NB + 9}.bias":
             continue  # pre-IN conv biases: exact zero gradient here, fp32 rounding noise on the CPU
         gerr[k] = _rel_l2(names[k].grad.cpu(), v.grad)
-    bad = {k: e for k, e in gerr.items() if e > (1.5e-2 if ".cbam." in k else 5e-3)}
+    bad = {k: e for k, e in gerr.items() if e > 5e-3}
     assert not bad, (bad, gerr)
     print("config 2 at 512x512 bs 2: worst stage", max(worst.values()), "worst grad", max(gerr.values()))
 
