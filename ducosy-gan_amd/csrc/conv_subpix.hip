@@ -117,13 +117,15 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     // zero).  MODE 1: the unit's window (row, column) packed as row * 4096 + column (-1: none); the dy
     // pixel depends on the iteration's phase
     int uoff[SP_UNITS];
+    const float rwp = 1.f / (float)WP;
 #pragma unroll
     for (int q = 0; q < SP_UNITS; ++q) {
         const int u = tid + q * SP_NT;
         const int wpix = u >> 1, h = u & 1;
         uoff[q] = -1;
         if (wpix < npix) {
-            const int wr = wpix / WP, wc = wpix - wr * WP;
+            // wpix / WP by a float reciprocal: exact, (wpix + 0.5) / WP stays >= 0.5 / WP from an integer
+            const int wr = (int)(((float)wpix + 0.5f) * rwp), wc = wpix - wr * WP;
             if constexpr (MODE == 0) {
                 const int sy = y0 - 1 + wr, sx = x0 - 1 + wc;
                 if (sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws) uoff[q] = (((n * a.Hs + sy) * a.Ws + sx) * C + 8 * h) * 4;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     int wbe;
     {
         const int q = wm * 64 + 2 * l32;
-        const int qy = q / TW;
+        const int qy = q >> __builtin_ctz(TW);
         wbe = MODE == 0 ? (qy + py) * WP + (q - qy * TW) + px : qy * WP + (q - qy * TW);
     }
 
@@ -299,27 +301,33 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         win_store(buf ^ 1);
         b_store(buf ^ 1);
         __syncthreads();
+        if ((s & 1) || s + 1 == nit) {  // close the accumulation chain every two iterations (128 k)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                acc[i][j] += t[i][j];
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] += t[i][j];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
-            }
+                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                }
+        }
     }
 
     // epilogue: undo the operand scales, NHWC store, IN statistics.  MODE 0: the phase's pixels of the
     // 2 Hs x 2 Ws output, channels co0 + j * 32 + lane; MODE 1: the Hs x Ws output, channels n0 + py * 64 + ...
     const int eab = -(ea + eb);
     const int Wo = MODE == 0 ? 2 * a.Ws : a.Ws;
-    auto opix = [&](int i, int r) {  // output pixel index within the image (increasing along r, then i)
+    // output pixel index within the image (increasing along r, then i); TW is a power of two and
+    // every product below fits 24 bits (index math off the slow 32-bit multiplier)
+    const int tws = __builtin_ctz(TW);
+    auto opix = [&](int i, int r) {
         const int q = wm * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
-        const int qy = q / TW;
-        if constexpr (MODE == 0) return (2 * (y0 + qy) + py) * Wo + 2 * (x0 + q - qy * TW) + px;
-        else return (y0 + qy) * Wo + x0 + q - qy * TW;
+        const int qy = q >> tws, qx = q & (TW - 1);
+        if constexpr (MODE == 0) return (int)__umul24(2 * (y0 + qy) + py, Wo) + 2 * (x0 + qx) + px;
+        else return (int)__umul24(y0 + qy, Wo) + x0 + qx;
     };
     const long long obase = (long long)n * (MODE == 0 ? 4LL : 1LL) * a.Hs * a.Ws * a.Co;
+    float* const outn = out + obase;  // the image's output (32-bit offsets below)
     const int co0 = MODE == 0 ? cb * 64 : n0 + py * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -328,7 +336,7 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
-                out[obase + (long long)opix(i, r) * a.Co + co0 + j * 32 + l32] = acc[i][j][r];
+                outn[(int)__umul24(opix(i, r), a.Co) + co0 + j * 32 + l32] = acc[i][j][r];
             }
     if constexpr (IBW) {  // per WG column: sums over the wave's 64 pixels, then the 4 pixel waves in order
         Sum2* ss = reinterpret_cast<Sum2*>(smem);  // [4][128]; the loop's last barrier freed the LDS
@@ -340,7 +348,7 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) yv[i][r] = ib.y[obase + (long long)opix(i, r) * a.Co + ch];
+                for (int r = 0; r < 16; ++r) yv[i][r] = ib.y[obase + (int)__umul24(opix(i, r), a.Co) + ch];
             float sa = 0.f, sb = 0.f;
 #pragma unroll
             for (int i = 0; i < 2; ++i)

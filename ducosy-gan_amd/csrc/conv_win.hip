@@ -173,7 +173,7 @@ __device__ __forceinline__ void win_ibw(const floatx16 (&acc)[2][2], const float
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int pix = p0 + win_pix(wm, i, r, kh);
-                const int py = pix / W, px = pix - py * W;
+                const int py = pix >> __builtin_ctz(W), px = pix & (W - 1);  // (W is a power of two)
                 if (py == 1 || py == H - 2 || px == 1 || px == W - 2) continue;  // the ring fold's pixels
                 const float xh = fmaf(yv[i][j][r], s, b);
                 const float g = acc[i][j][r] * act_grad(xh, ib.act);
