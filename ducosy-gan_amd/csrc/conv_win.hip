@@ -220,10 +220,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                                                                  const float* __restrict__ addend,
                                                                  float* __restrict__ out, Part* __restrict__ parts,
                                                                  IbwArgs ib) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 6 * WIN_SLOT + 8];
+    // f16x3: B k-tiles [2][6 = plane x tx][WIN_SLOT]; f16 (NP 1): B slices [2][9 taps][WIN_SLOT] (one
+    // barrier per slice, see below)
+    constexpr int BHALVES = NP == 3 ? 2 * 6 * WIN_SLOT : 2 * 9 * WIN_SLOT;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + BHALVES + 8];
     _Float16* const Wn = smem;                               // [2][2][WIN_PIX][16]
-    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;        // [2][6][WIN_SLOT]
-    _Float16* const Wspare = Bs + 2 * 6 * WIN_SLOT;          // 16 bytes nobody reads
+    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;
+    _Float16* const Wspare = Bs + BHALVES;                   // 16 bytes nobody reads
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -345,6 +348,99 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
+    if constexpr (NP == 1) {
+        // f16: one product per fragment pair, so a 48-k tile holds only 12 MFMAs per wave; instead the
+        // whole slice (9 taps, hi planes only) is staged per barrier: 36 MFMAs per wave between
+        // barriers.  B slice by LDS-DMA, 36 blocks of 1 KB (tap, 32-row block), blocks w, w + 8, ...
+        // of wave w.
+        unsigned sdst[5], ssu[5];
+        {
+            const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
+            const int w = __builtin_amdgcn_readfirstlane(wid);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const int c = w + 8 * i < 36 ? w + 8 * i : 35, tap = c >> 2, rb = c & 3;
+                ssu[i] = 2u * (unsigned)(rb * 32 * K + tap * 16);
+                sdst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)(tap * WIN_SLOT + rb * 32 * 16));
+            }
+        }
+        const bool fifth = wid + 32 < 36;  // wave-uniform: waves 0-3 issue a fifth block
+        auto s_dma = [&](int sl, int buf) {
+            const unsigned kb = 2u * (unsigned)(sl * 144);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) win_glds(wh, dlane + (ssu[i] + kb), sdst[i] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
+            if (fifth) win_glds(wh, dlane + (ssu[4] + kb), sdst[4] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
+        };
+#pragma unroll
+        for (int q = 0; q < WIN_UNITS; ++q) {
+            win_load_u(q, 0);
+            win_store_u(q, 0);
+        }
+        s_dma(0, 0);
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
+        __syncthreads();
+        auto sloop = [&](auto role_tag) {
+            constexpr int ROLE = decltype(role_tag)::value;
+            for (int s = 0; s < nslice; ++s) {
+                const int buf = s & 1;
+                const int sn = s + 1 < nslice ? s + 1 : s;
+                // the next slice into the other buffers (last read before this slice's top barrier):
+                // B by DMA now, the window's two units loaded now and stored after the kernel row that
+                // is this wave's staging point (ROLE 0: the last, ROLE 1: the first)
+                s_dma(sn, buf ^ 1);
+                win_load_u(1, sn);  // unit 1 into wq_, moved to wq1
+                const float4 wq1[2] = {wq_[0], wq_[1]};
+                win_load_u(0, sn);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int ty = 0; ty < 3; ++ty) {
+                    f16x8 fh[4];
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                        fh[f] = *reinterpret_cast<const f16x8*>(Wn + win_off(buf, 0, wbe + ty * WP + f, kh));
+                    f16x8 pb[2][2];
+                    auto rd_b = [&](int tx, int slot) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int row = wn * 64 + j * 32 + l32;
+                            pb[slot][j] = *reinterpret_cast<const f16x8*>(
+                                Bs + (buf * 9 + ty * 3 + tx) * WIN_SLOT + row * 16 + 8 * (kh ^ ((row >> 3) & 1)));
+                        }
+                    };
+                    rd_b(0, 0);
+#pragma unroll
+                    for (int tx = 0; tx < 3; ++tx) {
+                        if (tx < 2) rd_b(tx + 1, (tx + 1) & 1);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], pb[tx & 1][j], t[i][j], 0, 0, 0);
+                    }
+                    if (ty == (ROLE == 0 ? 2 : 0)) {  // staging point of this wave
+                        __builtin_amdgcn_sched_barrier(0);
+                        win_store_u(0, buf ^ 1);
+                        wq_[0] = wq1[0];
+                        wq_[1] = wq1[1];
+                        win_store_u(1, buf ^ 1);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs landed
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] += t[i][j];
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
+        };
+        if (wid >= 4) sloop(std::integral_constant<int, 1>{});
+        else sloop(std::integral_constant<int, 0>{});
+    } else {
     // prologue: window of slice 0, B tile 0
 #pragma unroll
     for (int q = 0; q < WIN_UNITS; ++q) {
@@ -433,6 +529,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     };
     if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
     else kloop(std::integral_constant<int, 0>{});
+    }
 
     // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
     const int eab = -(ea + eb);
