@@ -672,9 +672,17 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                                                                  const float* __restrict__ rnga,
                                                                  const float* __restrict__ rngb,
                                                                  float* __restrict__ ws) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
-    _Float16* const Xr = smem;                 // [4][2][66][64]
-    _Float16* const Dy = smem + 4 * WW_XROW;   // [2][2][64][64]
+    // f16x3: a ring of 4 source rows [2 planes][66][64] and 2 dy buffers [2][64][64], one image row per
+    // barrier.  f16 (NP 1, hi planes only): one product per fragment pair leaves 36 MFMAs per SIMD
+    // and row, so two rows run per barrier: a ring of 8 source rows and 4 dy buffers.
+    constexpr int RPB = NP == 3 ? 1 : 2;             // image rows per barrier
+    constexpr int NXS = NP == 3 ? 4 : 8;             // source-row ring slots
+    constexpr int NDB = NP == 3 ? 2 : 4;             // dy buffers
+    constexpr int XROW = NP == 3 ? WW_XROW : WW_WP * 64;
+    constexpr int DROW = NP == 3 ? WW_DROW : WW_SW * 64;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[NXS * XROW + NDB * DROW];
+    _Float16* const Xr = smem;                 // [NXS][planes][66][64]
+    _Float16* const Dy = smem + NXS * XROW;    // [NDB][planes][64][64]
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int ntile = a.gco * a.gci;
@@ -747,8 +755,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     auto st_dy = [&](int buf) {
         f16x8 hi, lo;
         split8h(dr[0], dr[1], asc, hi, lo);
-        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls) = hi;
-        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls) = lo;
+        *reinterpret_cast<f16x8*>(Dy + buf * DROW + dls) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * DROW + WW_SW * 64 + dls) = lo;
     };
     auto st_x = [&](int slot) {
 #pragma unroll
@@ -756,8 +764,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             if (xls[q] >= 0) {
                 f16x8 hi, lo;
                 split8h(xr[q][0], xr[q][1], bsc, hi, lo);
-                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
-                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
+                *reinterpret_cast<f16x8*>(Xr + slot * XROW + xls[q]) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * XROW + WW_WP * 64 + xls[q]) = lo;
             }
         }
     };
@@ -786,14 +794,17 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
 
-    // prologue: source rows y_beg-1 .. y_beg+1 into their ring slots, dy row y_beg into buffer 0
+    // prologue: source rows y_beg - 1 .. y_beg + RPB into their ring slots, dy rows y_beg .. y_beg + RPB - 1
 #pragma unroll 1
-    for (int r = y_beg - 1; r <= y_beg + 1; ++r) {
-        ld_x(r);
-        st_x(r & 3);
+    for (int r = y_beg - 1; r <= y_beg + RPB; ++r) {
+        ld_x(r <= H ? r : H);
+        st_x(r & (NXS - 1));
     }
-    ld_dy(y_beg);
-    st_dy(y_beg & 1);
+#pragma unroll 1
+    for (int r = y_beg; r < y_beg + RPB; ++r) {
+        ld_dy(r < y_end ? r : y_end - 1);
+        st_dy(r & (NDB - 1));
+    }
     __syncthreads();
 
     // one row of this wave's taps T0 .. T0 + NT_ - 1: 4 pixel sub-tiles x NT_ taps, the fragments of
@@ -802,10 +813,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         constexpr int T0 = decltype(tag)::value * WW_TPW;
         constexpr int NT_ = 9 - T0 < WW_TPW ? 9 - T0 : WW_TPW;
         constexpr int NJ = 4 * NT_;
-        const _Float16* const Db = Dy + (y & 1) * WW_DROW;
+        const _Float16* const Db = Dy + (y & (NDB - 1)) * DROW;
         const _Float16* Xs[3];
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + 3 + ty) & 3) * WW_XROW;  // row y - 1 + ty
+        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + NXS - 1 + ty) & (NXS - 1)) * XROW;  // row y - 1 + ty
         auto rdA = [&](int k, f16x8& h, f16x8& l) {
             h = ww_frag(Db + aoff + k * 16 * 64);
             if constexpr (NP == 3) l = ww_frag(Db + WW_SW * 64 + aoff + k * 16 * 64);
@@ -830,9 +841,9 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
             }
             tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tt, 0, 0, 0);
-            if (j == NJ / 2 - 1) {  // stage the rows loaded above into the buffers this row does not read
-                st_dy((y + 1) & 1);
-                st_x((y + 2) & 3);
+            if (j == NJ / 2 - 1) {  // stage the rows loaded above into the buffers no row of this barrier reads
+                st_dy((y + RPB) & (NDB - 1));
+                st_x((y + RPB + 1) & (NXS - 1));
             }
             bh = nbh;
             bl = nbl;
@@ -843,22 +854,46 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         }
     };
 
+    if constexpr (RPB == 1) {
 #pragma unroll 1
-    for (int y = y_beg; y < y_end; ++y) {
-        // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
-        ld_dy(y + 1 < y_end ? y + 1 : y);
-        ld_x(y + 2 <= H ? y + 2 : H);
-        if (half == 0) row(y, std::integral_constant<int, 0>{});
-        else row(y, std::integral_constant<int, 1>{});
-        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
+        for (int y = y_beg; y < y_end; ++y) {
+            // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
+            ld_dy(y + 1 < y_end ? y + 1 : y);
+            ld_x(y + 2 <= H ? y + 2 : H);
+            if (half == 0) row(y, std::integral_constant<int, 0>{});
+            else row(y, std::integral_constant<int, 1>{});
+            if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
 #pragma unroll
-            for (int i = 0; i < WW_TPW; ++i) {
+                for (int i = 0; i < WW_TPW; ++i) {
+                    acc[i] += t[i];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[i][r] = 0.f;
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+#pragma unroll 1
+        for (int y = y_beg; y < y_end; y += 2) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int yr = y + q;
+                if (yr < y_end) {  // (block-uniform)
+                    // next rows in flight, staged mid-row into the buffers no row of this barrier reads
+                    ld_dy(yr + 2 < y_end ? yr + 2 : y_end - 1);
+                    ld_x(yr + 3 <= H ? yr + 3 : H);
+                    if (half == 0) row(yr, std::integral_constant<int, 0>{});
+                    else row(yr, std::integral_constant<int, 1>{});
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < WW_TPW; ++i) {  // chains of two rows
                 acc[i] += t[i];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) t[i][r] = 0.f;
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
 
     // epilogue: undo the operand scales, slab [split][co][tap * C + ci]
