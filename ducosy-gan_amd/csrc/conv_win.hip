@@ -21,6 +21,7 @@
 #include "conv_common.hpp"
 #include <type_traits>
 
+
 namespace dcs {
 namespace {
 
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 const int sn = s + 1 < nslice ? s + 1 : s;
                 // the next slice into the other buffers (last read before this slice's top barrier):
                 // B by DMA now, the window's two units loaded now and stored after the kernel row that
-                // is this wave's staging point (ROLE 0: the last, ROLE 1: the first)
+                // is this wave's staging point (ROLE 0: the last, ROLE 1: the second)
                 s_dma(sn, buf ^ 1);
                 win_load_u(1, sn);  // unit 1 into wq_, moved to wq1
                 const float4 wq1[2] = {wq_[0], wq_[1]};
@@ -418,7 +419,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                             for (int j = 0; j < 2; ++j)
                                 t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], pb[tx & 1][j], t[i][j], 0, 0, 0);
                     }
-                    if (ty == (ROLE == 0 ? 2 : 0)) {  // staging point of this wave
+                    if (ty == (ROLE == 0 ? 2 : 1)) {  // staging point of this wave (kernel row 2 / 1)
                         __builtin_amdgcn_sched_barrier(0);
                         win_store_u(0, buf ^ 1);
                         wq_[0] = wq1[0];
@@ -841,7 +842,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
             }
             tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tt, 0, 0, 0);
-            if (j == NJ / 2 - 1) {  // stage the rows loaded above into the buffers no row of this barrier reads
+            // stage the rows loaded above into the buffers no row of this barrier reads: mid-row (f16x3),
+            // or at the row's end (f16: a row holds a third of the MFMAs, half a row hid too little of
+            // the loads' latency)
+            if (j == (NP == 1 ? NJ - 1 : NJ / 2 - 1)) {
                 st_dy((y + RPB) & (NDB - 1));
                 st_x((y + RPB + 1) & (NXS - 1));
             }

@@ -9,7 +9,7 @@ grep -E "FAILED|^E  " gpurun_out/${T}_tests.log | head -10; tail -1 gpurun_out/$
 [ $rc -le 1 ] || exit 1
 L=$R/ducosy-gan_amd/lib
 cd /tmp && export TMPDIR=/tmp
-for it in 1 2; do
+for it in ${ITS:-1 2}; do
 for v in base "$@"; do
   lib=$L/libducosy_hip_$v.so; [ "$v" = base ] && lib=$L/libducosy_hip.so
   DUCOSY_HIP_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/${T}_tr_${v}_$it -o tr -- python3 $R/bench.py --mma f16 --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/${T}_tr_${v}_$it.log 2>&1 || { echo "TRACE $v FAILED"; tail -3 $R/gpurun_out/${T}_tr_${v}_$it.log; exit 1; }
