@@ -188,36 +188,46 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             }
         }
     };
-    // B slice: 2 planes x 128 rows x 64 k = 2048 16-byte chunks, 4 per thread; chunk -> (plane, row,
-    // tap, half) with (tap, half) fastest (the 128 contiguous bytes of a row)
-    int bg[4], bl[4];
+    // B slice: 2 planes x 128 rows x 64 k = 2048 16-byte chunks, 4 per thread (chunks 0, 1 the hi
+    // plane, 2, 3 the lo plane: f16 loads only the first two); chunk -> (plane, row, tap, half) with
+    // (tap, half) fastest (the 128 contiguous bytes of a row).  S2: the chunks of (row, tap) pairs the
+    // MFMA loop skips load nothing (an out-of-range buffer offset reads zero without a fetch): 7 of the
+    // 16 (phase, tap) pairs of the forward, up to 5 of 8 of a data gradient launch
+    constexpr int NBC = NP == 3 ? 4 : 2;
+    const __amdgpu_buffer_rsrc_t bhr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(wh), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t blr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(NP == 3 ? wl : wh), (short)0, 0x7fffff00, 0x00020000);
+    int bg[NBC], bl[NBC], bt[NBC];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NBC; ++i) {
         const int q = tid + i * SP_NT;
         const int pl = q >> 10, rem = q & 1023;
         const int row = rem >> 3, c8 = rem & 7;
-        bg[i] = pl * 0x40000000 + (n0 + row) * K + c8 * 8;  // bit 30: the lo plane
+        bg[i] = ((n0 + row) * K + c8 * 8) * 2;  // byte offset in the plane
         bl[i] = sp_boff(0, pl, c8 >> 1, row, c8 & 1);
+        bt[i] = (c8 >> 1) | ((row >> 6) << 2);  // tap (u, t) and the row's 64-row half (MODE 0: py)
     }
-    uint4 br0, br1, br2, br3;
-    auto b_ld = [&](int i, int kb) {
-        const int g = bg[i] & 0x3fffffff;
-        const _Float16* w = (bg[i] >> 30) ? wl : wh;
-        return *reinterpret_cast<const uint4*>(w + g + kb);
-    };
+    u32x4 br[NBC];
     auto b_load = [&](int it) {
-        const int kb = it * 64;
-        br0 = b_ld(0, kb);
-        br1 = b_ld(1, kb);
-        br2 = b_ld(2, kb);
-        br3 = b_ld(3, kb);
+        const int kb = it * 128;  // bytes
+#pragma unroll
+        for (int i = 0; i < NBC; ++i) {
+            bool skip = false;
+            if constexpr (S2) {
+                const int u = (bt[i] >> 1) & 1, t = bt[i] & 1;
+                if constexpr (MODE == 0) {
+                    skip = ((bt[i] >> 2) == 0 && u == 0) || (PXC == 0 && t == 0);
+                } else {
+                    const int ph = it / nslice;
+                    skip = ((ph >> 1) == 0 && u == 1) || ((ph & 1) == 0 && t == 1);
+                }
+            }
+            br[i] = __builtin_amdgcn_raw_buffer_load_b128(i < 2 ? bhr : blr, skip ? 0x7fffffbf : bg[i] + kb, 0, 0);
+        }
     };
     auto b_store = [&](int buf) {
         const int boff = buf * 8 * SP_SLOT;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[0]) = br0;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[1]) = br1;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[2]) = br2;
-        *reinterpret_cast<uint4*>(Bs + boff + bl[3]) = br3;
+#pragma unroll
+        for (int i = 0; i < NBC; ++i) *reinterpret_cast<u32x4*>(Bs + boff + bl[i]) = br[i];
     };
 
     // row block i holds source pixels 2m + i of the wave's 64 (TW even: a pair shares a row), so block 0
@@ -673,7 +683,9 @@ __global__ __launch_bounds__(SW_NT, 1) void subpix_wgrad_kernel(SWArgs a, const 
                 }
                 tq[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, tq[tap], 0, 0, 0);
             }
-            if (k == 1) {  // stage the rows loaded above into the buffers this row does not read
+            // stage the rows loaded above into the buffers this row does not read: mid-row (f16x3), or
+            // after the row's MFMAs (f16: a third of the MFMAs hid too little of the loads' latency)
+            if (k == (NP == 1 ? 3 : 1)) {
                 st_dy((y + 1) & 1);
                 st_x((y + 2) & 3);
             }

@@ -633,8 +633,9 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
 // MFMA shape: M = co (32), N = ci (32), K = 16 pixels of the row; both operands pixel-major in LDS,
 // fragments by ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).  8 waves, two per
 // SIMD: waves w and w + 4 (same SIMD) own co block (w & 1) x ci block ((w >> 1) & 1), wave w taps
-// 0..4 and wave w + 4 taps 5..8, so each SIMD carries all nine taps of one 32 x 32 (co, ci) block and
-// each wave at most five accumulators (two-level: a chain of two rows = 128 pixels, then added to
+// 0..3 and wave w + 4 taps 5..8, tap 4 split between them by pixel sub-tile (ww_k / ww_tap), so each
+// SIMD carries all nine taps of one 32 x 32 (co, ci) block, 18 MFMA groups per wave, and each wave
+// five accumulators (two-level: a chain of two rows = 128 pixels, then added to
 // the running sum), leaving registers for fragment reads ahead and a second wave to cover LDS
 // latency.  Per row and SIMD: 4 pixel sub-tiles x 9 taps x 3 products = 108 MFMAs between barriers.
 // LDS (halves): ring [4 slots][2 planes][66 px][64 ch], dy [2 buffers][2 planes][64 px][64 ch];
@@ -666,6 +667,14 @@ __device__ __forceinline__ f16x8 ww_frag(const _Float16* p) {
     const wshortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wshortx4*)(p + 4 * 64));
     return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
+
+// (sub-tile k, tap) of a wave's j-th MFMA group in a row: the 36 pairs of a SIMD split 18 / 18
+// between its two waves, tap 4 shared (role 0: taps 0..4 on sub-tiles 0, 1 and taps 0..3 on 2, 3;
+// role 1: taps 5..8 on sub-tiles 0, 1 and taps 4..8 on 2, 3), so neither wave runs alone at the
+// row's end; the two partial sums of tap 4 meet in the epilogue
+__host__ __device__ constexpr int ww_k(int r, int j) { return r == 0 ? (j < 10 ? j / 5 : 2 + (j - 10) / 4) : (j < 8 ? j / 4 : 2 + (j - 8) / 5); }
+__host__ __device__ constexpr int ww_tap(int r, int j) { return r == 0 ? (j < 10 ? j % 5 : (j - 10) % 4) : (j < 8 ? 5 + j % 4 : 4 + (j - 8) % 5); }
+__host__ __device__ constexpr int ww_acc(int r, int tap) { return r == 0 ? tap : (tap == 4 ? 4 : tap - 5); }
 
 template <int NP>  // as conv3_win_h3_kernel
 __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const float* __restrict__ dy,
@@ -811,9 +820,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     // one row of this wave's taps T0 .. T0 + NT_ - 1: 4 pixel sub-tiles x NT_ taps, the fragments of
     // the next (sub-tile, tap) read before the MFMAs of the current one
     auto row = [&](int y, auto tag) {
-        constexpr int T0 = decltype(tag)::value * WW_TPW;
-        constexpr int NT_ = 9 - T0 < WW_TPW ? 9 - T0 : WW_TPW;
-        constexpr int NJ = 4 * NT_;
+        constexpr int R = decltype(tag)::value;
+        constexpr int NJ = 18;  // (sub-tile, tap) pairs of this wave
         const _Float16* const Db = Dy + (y & (NDB - 1)) * DROW;
         const _Float16* Xs[3];
 #pragma unroll
@@ -823,7 +831,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             if constexpr (NP == 3) l = ww_frag(Db + WW_SW * 64 + aoff + k * 16 * 64);
         };
         auto rdB = [&](int j, f16x8& h, f16x8& l) {
-            const int k = j / NT_, tap = T0 + j % NT_, ty = tap / 3, tx = tap % 3;
+            const int k = ww_k(R, j), tap = ww_tap(R, j), ty = tap / 3, tx = tap % 3;
             h = ww_frag(Xs[ty] + boff[tx] + k * 16 * 64);
             if constexpr (NP == 3) l = ww_frag(Xs[ty] + WW_WP * 64 + boff[tx] + k * 16 * 64);
         };
@@ -833,10 +841,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             if (j + 1 < NJ) {
-                if ((j + 1) % NT_ == 0) rdA((j + 1) / NT_, nah, nal);
+                if (ww_k(R, j + 1) != ww_k(R, j)) rdA(ww_k(R, j + 1), nah, nal);
                 rdB(j + 1, nbh, nbl);
             }
-            floatx16& tt = t[j % NT_];
+            floatx16& tt = t[ww_acc(R, ww_tap(R, j))];
             if constexpr (NP == 3) {
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tt, 0, 0, 0);
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
@@ -851,7 +859,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             }
             bh = nbh;
             bl = nbl;
-            if ((j + 1) % NT_ == 0) {
+            if (j + 1 < NJ && ww_k(R, j + 1) != ww_k(R, j)) {
                 ah = nah;
                 al = nal;
             }
@@ -900,13 +908,24 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
         }
     }
 
-    // epilogue: undo the operand scales, slab [split][co][tap * C + ci]
+    // epilogue: the two halves of tap 4 summed through LDS (free after the loop's last barrier), then
+    // undo the operand scales, slab [split][co][tap * C + ci]
+    float* const t4 = reinterpret_cast<float*>(smem) + (wid & 3) * 64 * 16 + lane;
+    if (half == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t4[r * 64] = acc[4][r];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[4][r] += t4[r * 64];
+    }
     const int eab = -(ea + eb);
     float* const slab = ws + (long long)split * Co * 9 * C;
     const int col = ci0 + 32 * cib + (lane & 31);
 #pragma unroll
     for (int i = 0; i < WW_TPW; ++i) {
-        const int tap = half * WW_TPW + i;
+        const int tap = half == 0 ? i : (i == 4 ? 9 : 5 + i);
         if (tap < 9) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {

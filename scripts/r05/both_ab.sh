@@ -16,4 +16,10 @@ for v in base "$@"; do
   DUCOSY_HIP_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/${T}_${mode}_${v} -o tr -- python3 $R/bench.py --mma $mode --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/${T}_${mode}_${v}.log 2>&1 || { echo "TRACE $v FAILED"; tail -3 $R/gpurun_out/${T}_${mode}_${v}.log; exit 1; }
 done
 done
+cd $R
+for mode in f16x3 f16; do
+  dirs=""; for v in base "$@"; do dirs="$dirs gpurun_out/${T}_${mode}_${v}"; done
+  python scripts/r05/trace_cmp.py 7 $dirs > gpurun_out/${T}_cmp_${mode}.txt || exit 1
+  rm -rf $dirs  # the databases exceed what gpurun copies back; the table is the record
+done
 echo traces ok
