@@ -1,6 +1,7 @@
 // Device helpers shared by the convolution kernels (conv.hip, conv_win.hip, conv_subpix.hip): MFMA operand vector
 // types, the f16x3 operand split and scale exponent, the XCD-aware workgroup order.
 #pragma once
+#include <type_traits>
 #include "common.hpp"
 
 namespace dcs {
@@ -27,13 +28,29 @@ __device__ __forceinline__ void split4h(const float4& a, float sc, f16x4& hi, f1
 }
 
 // f16x3 operand exponent: s with max|operand| * 2^s < 2^15, from the n (<= 1024) partial
-// maxima of the operand's range record (every wave reduces them itself; wave-uniform result)
+// maxima of the operand's range record (every wave reduces them itself; wave-uniform result).  All
+// sixteen loads of a lane in flight at once (buffer loads past n read 0, the identity of a max over
+// maxima >= 0): one memory round trip at a kernel's start instead of one per 128 partials; the wave
+// maximum by DPP within rows of 16 lanes, then the four row maxima
 __device__ __forceinline__ int f16x3_exp(const float* __restrict__ rng, int n) {
     const int lane = threadIdx.x & 63;
-    float m = 0.f;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, rng[i]);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rng), (short)0, n * 4, 0x00020000);
+    float v[16];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    for (int k = 0; k < 16; ++k) v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + 64 * k) * 4, 0, 0));
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m = fmaxf(m, v[k]);
+    auto dpp_max = [](float x, auto ctrl) {
+        const int y = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), decltype(ctrl)::value, 0xf, 0xf, true);
+        return fmaxf(x, __builtin_bit_cast(float, y));
+    };
+    m = dpp_max(m, std::integral_constant<int, 0xb1>{});   // quad_perm (1, 0, 3, 2)
+    m = dpp_max(m, std::integral_constant<int, 0x4e>{});   // quad_perm (2, 3, 0, 1)
+    m = dpp_max(m, std::integral_constant<int, 0x124>{});  // row_ror 4
+    m = dpp_max(m, std::integral_constant<int, 0x128>{});  // row_ror 8
+    const auto rl = [&](int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), l)); };
+    m = fmaxf(fmaxf(rl(0), rl(16)), fmaxf(rl(32), rl(48)));
     int e = 0;
     (void)frexpf(m, &e);  // m = f * 2^e, 0.5 <= f < 1 (e = 0 for m = 0)
     int sh = 15 - e;

@@ -102,16 +102,11 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     const int wm = wid & 3, py = wid >> 2;  // MODE 1: py is the wave's 64-channel half of the tile
     const int l32 = lane & 31, kh = lane >> 5;
 
-    const int ea = f16x3_exp(rng, a.rng_n);
+    // the source exponent (ea, asc) and the PRO table are read in the prologue, beside the first
+    // staging loads
+    int ea = 0;
+    float asc = 1.f;
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
-    const float asc = __builtin_ldexpf(1.f, ea);
-    if constexpr (PRO) {  // the image's prologue scale / shift (read before the first staging barrier)
-        for (int c = tid; c < C; c += SP_NT) {
-            pro_s[c] = psc[(long long)n * C + c];
-            pro_s[SP_PROC + c] = psh[(long long)n * C + c];
-        }
-        __syncthreads();
-    }
 
     // window staging units (pixel, 8-channel half).  MODE 0: byte offset of the unit's channel 0 (-1:
     // zero).  MODE 1: the unit's window (row, column) packed as row * 4096 + column (-1: none); the dy
@@ -249,9 +244,20 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
+    // prologue: every load of iteration 0 (and the exponent's, the PRO table's) in flight before the
+    // first store
     win_load(0);
-    win_store(0);
     b_load(0);
+    if constexpr (PRO) {  // the image's prologue scale / shift (published by the barrier below)
+        for (int c = tid; c < C; c += SP_NT) {
+            pro_s[c] = psc[(long long)n * C + c];
+            pro_s[SP_PROC + c] = psh[(long long)n * C + c];
+        }
+        __syncthreads();
+    }
+    ea = f16x3_exp(rng, a.rng_n);
+    asc = __builtin_ldexpf(1.f, ea);
+    win_store(0);
     b_store(0);
     __syncthreads();
 

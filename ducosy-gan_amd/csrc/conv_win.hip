@@ -25,6 +25,13 @@
 namespace dcs {
 namespace {
 
+#ifndef WIN_TIMING
+#define WIN_TIMING 0
+#endif
+#if WIN_TIMING  // probe build only: per-workgroup phase timestamps (scripts/r05/win_timing.py)
+__device__ unsigned long long g_win_t[16384 * 5];
+#endif
+
 constexpr int WIN_BN = 128, WIN_NT = 512;  // tiles: 256 pixels (whole rows) x WIN_BN channels
 constexpr int WIN_PIX = 520;             // window pixels for W <= 128: (256 / W + 2) * (W + 2) <= 520
 // halves per B plane-slot: 128 rows x 16 k + 48 (96 B: the three tx slots of a row, written by
@@ -229,6 +236,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;
     _Float16* const Wspare = Bs + BHALVES;                   // 16 bytes nobody reads
 
+#if WIN_TIMING
+    const unsigned long long tm0 = wall_clock64();
+    unsigned long long tm1 = 0, tm2 = 0;
+#endif
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
     const int ntile = L % a.gy, mt = L / a.gy;
@@ -243,9 +254,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int wm = wid >> 1, wn = wid & 1;
     const int l32 = lane & 31, kh = lane >> 5;
 
-    const int ea = f16x3_exp(rng, a.rng_n);
+    // the source exponent (ea, asc) is read in the prologue, its loads beside the first staging loads
+    int ea = 0;
+    float asc = 1.f;
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
-    const float asc = __builtin_ldexpf(1.f, ea);
 
     // window staging units of this thread: (pixel, 8-channel half) of the window's interior columns
     // ((R + 2) x W pixels: 2 units per thread at W <= 128).  uoff: byte offset of the unit's source
@@ -260,7 +272,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         uoff[q] = -1;
         uwd[q] = 0;
         if (ip < nint) {
-            const int wr = ip / W, sx = ip - wr * W;
+            const int wr = ip >> __builtin_ctz(W), sx = ip & (W - 1);  // (W is a power of two)
             int dup = -1;
             int sy = y0 - 1 + wr;
             bool ok = true;
@@ -338,7 +350,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     int wbe;
     {
         const int q = wm * 64 + 2 * l32;
-        wbe = (q / W) * WP + (q - (q / W) * W);
+        wbe = (q >> __builtin_ctz(W)) * WP + (q & (W - 1));
     }
 
     floatx16 acc[2][2], t[2][2];
@@ -372,12 +384,17 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
             for (int i = 0; i < 4; ++i) win_glds(wh, dlane + (ssu[i] + kb), sdst[i] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
             if (fifth) win_glds(wh, dlane + (ssu[4] + kb), sdst[4] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
         };
-#pragma unroll
-        for (int q = 0; q < WIN_UNITS; ++q) {
-            win_load_u(q, 0);
-            win_store_u(q, 0);
-        }
+        // prologue: every load of slice 0 (and the exponent's) in flight before the first store
         s_dma(0, 0);
+        win_load_u(1, 0);
+        const float4 wp1[2] = {wq_[0], wq_[1]};
+        win_load_u(0, 0);
+        ea = f16x3_exp(rng, a.rng_n);
+        asc = __builtin_ldexpf(1.f, ea);
+        win_store_u(0, 0);
+        wq_[0] = wp1[0];
+        wq_[1] = wp1[1];
+        win_store_u(1, 0);
         __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
         __syncthreads();
         auto sloop = [&](auto role_tag) {
@@ -442,15 +459,23 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         if (wid >= 4) sloop(std::integral_constant<int, 1>{});
         else sloop(std::integral_constant<int, 0>{});
     } else {
-    // prologue: window of slice 0, B tile 0
-#pragma unroll
-    for (int q = 0; q < WIN_UNITS; ++q) {
-        win_load_u(q, 0);
-        win_store_u(q, 0);
-    }
+    // prologue: window of slice 0, B tile 0, every load (and the exponent's) in flight before the first
+    // store
     b_dma(0, 0);
+    win_load_u(1, 0);
+    const float4 wp1[2] = {wq_[0], wq_[1]};
+    win_load_u(0, 0);
+    ea = f16x3_exp(rng, a.rng_n);
+    asc = __builtin_ldexpf(1.f, ea);
+    win_store_u(0, 0);
+    wq_[0] = wp1[0];
+    wq_[1] = wp1[1];
+    win_store_u(1, 0);
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
     __syncthreads();
+#if WIN_TIMING
+    tm1 = wall_clock64();
+#endif
 
     // every global load below is unconditional (offsets clamped at the end): a load under a branch
     // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer
@@ -530,6 +555,9 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     };
     if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
     else kloop(std::integral_constant<int, 0>{});
+#if WIN_TIMING
+    tm2 = wall_clock64();
+#endif
     }
 
     // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
@@ -576,6 +604,14 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm, wn, lane);
         win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(smem));
     }
+#if WIN_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0 && L < 16384) {
+        unsigned long long* g = g_win_t + 5 * L;
+        g[0] = tm0; g[1] = tm1; g[2] = tm2; g[3] = wall_clock64(); g[4] = __smid();
+    }
+#endif
 }
 
 // pre-split weight pack (dcs_pack_weights_h3): the range of the raw weights first, then every block
@@ -708,8 +744,9 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int cob = wid & 1, cib = (wid >> 1) & 1, half = wid >> 2;
 
-    const int ea = f16x3_exp(rnga, a.rng_a_n), eb = f16x3_exp(rngb, a.rng_b_n);
-    const float asc = __builtin_ldexpf(1.f, ea), bsc = __builtin_ldexpf(1.f, eb);
+    // the operand exponents are read in the prologue, beside the first rows' loads
+    int ea = 0, eb = 0;
+    float asc = 1.f, bsc = 1.f;
 
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
@@ -804,16 +841,40 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) { acc[i][r] = 0.f; t[i][r] = 0.f; }
 
-    // prologue: source rows y_beg - 1 .. y_beg + RPB into their ring slots, dy rows y_beg .. y_beg + RPB - 1
-#pragma unroll 1
-    for (int r = y_beg - 1; r <= y_beg + RPB; ++r) {
-        ld_x(r <= H ? r : H);
-        st_x(r & (NXS - 1));
-    }
-#pragma unroll 1
-    for (int r = y_beg; r < y_beg + RPB; ++r) {
-        ld_dy(r < y_end ? r : y_end - 1);
-        st_dy(r & (NDB - 1));
+    // prologue: source rows y_beg - 1 .. y_beg + RPB into their ring slots, dy rows y_beg .. y_beg + RPB - 1;
+    // every row's loads (and the exponents') in flight before the first store
+    {
+        float4 px_[RPB + 2][WW_XU][2], pd_[RPB][2];
+#pragma unroll
+        for (int i = 0; i < RPB + 2; ++i) {
+            const int r = y_beg - 1 + i;
+            ld_x(r <= H ? r : H);
+#pragma unroll
+            for (int q = 0; q < WW_XU; ++q) { px_[i][q][0] = xr[q][0]; px_[i][q][1] = xr[q][1]; }
+        }
+#pragma unroll
+        for (int i = 0; i < RPB; ++i) {
+            const int r = y_beg + i;
+            ld_dy(r < y_end ? r : y_end - 1);
+            pd_[i][0] = dr[0];
+            pd_[i][1] = dr[1];
+        }
+        ea = f16x3_exp(rnga, a.rng_a_n);
+        eb = f16x3_exp(rngb, a.rng_b_n);
+        asc = __builtin_ldexpf(1.f, ea);
+        bsc = __builtin_ldexpf(1.f, eb);
+#pragma unroll
+        for (int i = 0; i < RPB + 2; ++i) {
+#pragma unroll
+            for (int q = 0; q < WW_XU; ++q) { xr[q][0] = px_[i][q][0]; xr[q][1] = px_[i][q][1]; }
+            st_x((y_beg - 1 + i) & (NXS - 1));
+        }
+#pragma unroll
+        for (int i = 0; i < RPB; ++i) {
+            dr[0] = pd_[i][0];
+            dr[1] = pd_[i][1];
+            st_dy((y_beg + i) & (NDB - 1));
+        }
     }
     __syncthreads();
 
@@ -1060,6 +1121,12 @@ extern "C" int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, 
                        wexp);
     return check_launch("pack_weights_h3");
 }
+
+#if WIN_TIMING
+extern "C" int dcs_probe_win_times(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcs::g_win_t), (size_t)n * 5 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int dcs_conv3_win_ok(const dcs_conv_desc* dp, int dgrad) { return dp ? win_check(*dp, !dgrad) : 0; }
 

@@ -20,6 +20,7 @@ cd $R
 for mode in f16x3 f16; do
   dirs=""; for v in base "$@"; do dirs="$dirs gpurun_out/${T}_${mode}_${v}"; done
   python scripts/r05/trace_cmp.py 7 $dirs > gpurun_out/${T}_cmp_${mode}.txt || exit 1
+  for k in ${INST:-}; do python scripts/r05/trace_inst.py 7 $k $dirs > gpurun_out/${T}_inst_${k}_${mode}.txt || exit 1; done
   rm -rf $dirs  # the databases exceed what gpurun copies back; the table is the record
 done
 echo traces ok
