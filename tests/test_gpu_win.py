@@ -199,3 +199,43 @@ def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
     a = torch.relu((yd - m) / torch.sqrt(v + 1e-5))
     (a * da_s.double().cpu()).sum().backward()
     assert _relmax(dy_f, yd.grad) <= 1e-4
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
+def test_win_persistent_jobs_bit_identical(ops, mode):
+    """More jobs than CUs: N = 3 at 128 x 128 x 256 is 384 (tile, column tile) jobs on a grid of one
+    workgroup per CU, so workgroups run two jobs, the last slice of the first staging the second's first
+    slice and B tile (conv3_win_h3_kernel, launch_win).  Against the same convs one image at a time (128
+    jobs, one per workgroup): bit-identical outputs and IN statistics (forward), and data gradients with
+    the residual addend bit-identical inside the two-pixel border (the border's reflection-ring pass
+    splits K by the batch size, so there the sums differ in order: 1e-6 of the largest value)."""
+    ops.set_mma(mode)
+    g = _geom(ops)
+    N, H, W = 3, 128, 128
+    xd = rnd((N, 256, H, W), 71, "x").float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    w = torch.from_numpy(prng.normal(72, "w", (256, 256, 3, 3), 0, 0.05)).float().to(DEV)
+    wp = g.pack_fwd(w)
+    y, st = g.forward_in_stats(ops.Src.nhwc(xd), wp, want_max=True)
+    Rd = rnd((N, 256, H, W), 73, "R").float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Ad = rnd((N, 256, H, W), 74, "A").float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    wd = g.pack_dgrad(w)
+    dx = g.dgrad(Rd, wd, H, W, addend=Ad)
+    for i in range(N):
+        yi, sti = g.forward_in_stats(ops.Src.nhwc(xd[i:i + 1].contiguous()), wp, want_max=True)
+        assert torch.equal(y[i:i + 1], yi), (mode, i)
+        for a, b in ((st.scale, sti.scale), (st.shift, sti.shift), (st.xmax, sti.xmax), (st.xargmax, sti.xargmax)):
+            assert torch.equal(a[i:i + 1], b), (mode, i)
+        dxi = g.dgrad(Rd[i:i + 1].contiguous(), wd, H, W, addend=Ad[i:i + 1].contiguous())
+        assert torch.equal(dx[i:i + 1, 2:H - 2, 2:W - 2], dxi[:, 2:H - 2, 2:W - 2]), (mode, i)
+        assert float((dx[i:i + 1] - dxi).abs().max()) <= 1e-6 * float(dxi.abs().max()), (mode, i)
+    # the data gradient with the InstanceNorm-backward partial sums in its epilogue (the training step's
+    # form; zero padding, whose window halo must survive the epilogue's LDS use): the same da as
+    # without them, and the IN backward from the fused sums within 1e-5 of the separate pass
+    from modules.hip.lib import ACT_RELU
+    st_y = ops.in_stats(y)
+    da_f, parts, nch = g.dgrad(Rd, wd, H, W, inbwd=(y, st_y, ACT_RELU))
+    da_s = g.dgrad(Rd, wd, H, W)
+    assert parts is not None and torch.equal(da_f, da_s), mode
+    dy_f = ops.in_act_backward_parts(da_f, y, st_y, ACT_RELU, parts, nch)
+    dy_s = ops.in_act_backward(da_s, y, st_y, ACT_RELU)
+    assert _relmax(dy_f, dy_s.double().cpu()) <= 1e-5, mode
