@@ -16,12 +16,7 @@
 // accumulation chain per slice (144 k), added to the running sum (two-level, as conv.hip).
 // 8 waves = 4 (pixels) x 2 (channels) of 64 x 64; one workgroup per CU (115 KB of LDS).  The k-tile
 // schedule (LDS-DMA for B, one window unit in flight, fragments read ahead, staggered wave pairs) is
-// described at conv3_win_h3_kernel.  Persistent grid: one workgroup per CU walks the (tile, column
-// tile) jobs, each job's last slice staging the next job's first.  Besides hiding the per-job
-// prologue, this changed the whole step's power: with 8-24 rounds of short-lived workgroups per launch
-// the package ran at ~1320 W under power-limit throttling (PPT active 37 % of the time, engine clock
-// ~2.0 GHz for every kernel of the step); with the persistent grid ~1040 W at 2.39 GHz, 38 -> 43 img/s
-// (profiles/r05x/).
+// described at conv3_win_h3_kernel.
 #include "common.hpp"
 #include "conv_common.hpp"
 #include <type_traits>
@@ -41,9 +36,6 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #endif
 #if CLK_PROBE  // probe build only: core-clock and wall-clock counters per weight-gradient workgroup
 __device__ unsigned long long g_clk[4096 * 4];
-#endif
-#ifndef WIN_PERSIST
-#define WIN_PERSIST 1
 #endif
 
 constexpr int WIN_BN = 128, WIN_NT = 512;  // tiles: 256 pixels (whole rows) x WIN_BN channels
@@ -254,20 +246,12 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const unsigned long long tm0 = wall_clock64();
     unsigned long long tm1 = 0, tm2 = 0;
 #endif
-    // persistent workgroups (launch_win: gridDim.x <= jobs): job j = blockIdx.x + k gridDim.x, in the
-    // XCD-aware tile order; the last slice of a job stages the next job's first slice and B tile, so a
-    // job's prologue overlaps the previous job's last k-tiles (odd slice counts: one job per workgroup)
-    const int total = a.N * a.tiles * a.gy;
-    auto job_params = [&](int j, int& n_, int& tile_, int& n0_, int& y0_) {
-        const int L = xcd_remap(j, total);
-        const int ntile = L % a.gy, mt = L / a.gy;
-        n_ = mt / a.tiles;
-        tile_ = mt - n_ * a.tiles;
-        n0_ = ntile * WIN_BN;
-        y0_ = tile_ * a.R;  // first image row of the tile
-    };
-    int job = blockIdx.x, n, tile, n0, y0;
-    job_params(job, n, tile, n0, y0);
+    const int T = gridDim.x;
+    const int L = xcd_remap(blockIdx.x, T);
+    const int ntile = L % a.gy, mt = L / a.gy;
+    const int n = mt / a.tiles, tile = mt - n * a.tiles;
+    const int n0 = ntile * WIN_BN;
+    const int y0 = tile * a.R;                 // first image row of the tile
     const int W = a.W, WP = a.W + 2, C = a.C;
     const int K = 9 * C;                       // packed K (slice-major: (c/16)*144 + tap*16 + c%16)
     const int nslice = C / 16;
@@ -275,9 +259,6 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     const int l32 = lane & 31, kh = lane >> 5;
-    // window pixel of this lane's block-0 output pixel 2m (tap (0, 0) = the window's top-left); its
-    // block-1 pixel 2m + 1 is the next one (W is even: the pair shares a row)
-    const int wbe = ((wm * 64 + 2 * l32) >> __builtin_ctz(a.W)) * (a.W + 2) + ((wm * 64 + 2 * l32) & (a.W - 1));
 
     // the source exponent (ea, asc) is read in the prologue, its loads beside the first staging loads
     int ea = 0;
@@ -285,20 +266,33 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
 
     // window staging units of this thread: (pixel, 8-channel half) of the window's interior columns
-    // ((R + 2) x W pixels: 2 units per thread at W <= 128), their source offsets and window pixels
-    // recomputed at each use (held in registers through the job loop, they were spilled)
+    // ((R + 2) x W pixels: 2 units per thread at W <= 128).  uoff: byte offset of the unit's source
+    // channel 0 (-1: zero padding); uwd: its window pixel (bits 0-15) and the halo pixel it also writes
+    // (bits 16-31), each + 1 (0: none)
     const int nint = (a.R + 2) * W;
-    // byte offset of unit q's source channel 0 for the tile of (image n_, first row y0_) (-1: zero padding)
-    auto unit_src = [&](int q, int n_, int y0_) {
+    int uoff[WIN_UNITS], uwd[WIN_UNITS];
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
         const int u = tid + q * WIN_NT;
         const int ip = u >> 1, h = u & 1;
-        const int wr = ip >> __builtin_ctz(W), sx = ip & (W - 1);  // (W is a power of two)
-        int sy = y0_ - 1 + wr;
-        bool ok = ip < nint;
-        if (a.reflect) sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
-        else ok = ok && sy >= 0 && sy < a.H;
-        return ok ? (((n_ * a.H + sy) * W + sx) * C + 8 * h) * 4 : -1;
-    };
+        uoff[q] = -1;
+        uwd[q] = 0;
+        if (ip < nint) {
+            const int wr = ip >> __builtin_ctz(W), sx = ip & (W - 1);  // (W is a power of two)
+            int dup = -1;
+            int sy = y0 - 1 + wr;
+            bool ok = true;
+            if (a.reflect) {
+                sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
+                if (sx == 1) dup = wr * WP;                   // column -1 reflects column 1
+                else if (sx == W - 2) dup = wr * WP + W + 1;  // column W reflects column W - 2
+            } else {
+                ok = sy >= 0 && sy < a.H;
+            }
+            uwd[q] = (wr * WP + sx + 2) | ((dup + 1) << 16);
+            if (ok) uoff[q] = (((n * a.H + sy) * W + sx) * C + 8 * h) * 4;
+        }
+    }
     if (!a.reflect) {  // zero halo columns of both buffers and planes
         for (int i = tid; i < 2 * 2 * (a.R + 2) * 2 * 2; i += WIN_NT) {
             const int h = i & 1, side = (i >> 1) & 1, rest = i >> 2;
@@ -308,10 +302,8 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     float4 wq_[2];  // the unit in flight
-    // unit q of slice s of the tile (n_, y0_); unconditional (clamped offset): see the k loop
-    auto win_load_u = [&](int q, int s, int n_, int y0_) {
-        const int uo = unit_src(q, n_, y0_);
-        const int off = uo >= 0 ? uo + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
+    auto win_load_u = [&](int q, int s) {  // unconditional (clamped offset): see the k loop
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;  // 16 channels = 64 B per slice
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
         u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
@@ -321,13 +313,8 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     // unconditional store (a unit past the window writes the spare slot): a store under a branch lets
     // the compiler sink the unit's load into the branch, next to its use
     auto win_store_u = [&](int q, int buf) {
-        const int u = tid + q * WIN_NT;
-        const int ip = u >> 1, h = u & 1;
-        const int wr = ip >> __builtin_ctz(W), sx = ip & (W - 1);
-        // window pixel (-1: past the window) and the halo pixel the unit also writes (reflection: column
-        // -1 reflects column 1, column W reflects column W - 2)
-        const int wp = ip < nint ? wr * WP + sx + 1 : -1;
-        const int wd = ip < nint && a.reflect ? (sx == 1 ? wr * WP : (sx == W - 2 ? wr * WP + W + 1 : -1)) : -1;
+        const int h = (tid + q * WIN_NT) & 1;
+        const int wp = (uwd[q] & 0xffff) - 1, wd = (uwd[q] >> 16) - 1;
         f16x8 hi, lo;
         split8h(wq_[0], wq_[1], asc, hi, lo);
         *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + win_off(buf, 0, wp, h) : Wspare) = hi;
@@ -343,31 +330,34 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     // row L / 2, half position L % 2), so the wb_off swizzle goes on the source side: lane L fetches
     // half (L % 2) ^ bit 3 of its row.  The lane part of the source offset is the same for the three
     // blocks (bit 3 of the row is bit 3 of L / 2); the block part and the plane are wave-uniform.
-    // (blocks 3 w .. 3 w + 2 of wave w: waves 0-3 the hi plane, 4-7 the lo plane)
-    const _Float16* const dbase = __builtin_amdgcn_readfirstlane(wid) >= 4 ? wl : wh;
-    // lane part of the B source offset for column tile n0_
-    auto dlane = [&](int n0_) { return 2u * (unsigned)((n0_ + (lane >> 1)) * K + 8 * ((lane & 1) ^ ((lane >> 4) & 1))); };
-    // block i of this wave: source offset (without the lane and k parts) and LDS destination, computed
-    // at each use from the wave index (scalar arithmetic; held, they cost six SGPRs through the loop)
-    auto dblk = [&](int i, unsigned& su, unsigned& dst) {
+    unsigned dsu[3], ddst[3];
+    const _Float16* dbase[3];
+    const unsigned dlane = 2u * (unsigned)((n0 + (lane >> 1)) * K + 8 * ((lane & 1) ^ ((lane >> 4) & 1)));
+    {
         const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
-        const int c = __builtin_amdgcn_readfirstlane(wid) * 3 + i, pl = c / 12, rem = c - pl * 12;
-        const int tx = rem >> 2, rb = rem & 3;
-        su = 2u * (unsigned)(rb * 32 * K + tx * 16);
-        dst = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)((pl * 3 + tx) * WIN_SLOT + rb * 32 * 16));
-    };
-    auto b_dma = [&](int t, int buf, int n0_) {  // B tile t of column tile n0_ into buffer buf
-        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
-        const unsigned kb = 2u * (unsigned)(s_ * 144 + ty_ * 48);
-        const unsigned dl = dlane(n0_);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            unsigned su, dst;
-            dblk(i, su, dst);
-            win_glds(dbase, dl + (su + kb), dst + 2u * (unsigned)(buf * 6 * WIN_SLOT));
+            const int c = __builtin_amdgcn_readfirstlane(wid) * 3 + i, pl = c / 12, rem = c - pl * 12;
+            const int tx = rem >> 2, rb = rem & 3;
+            dsu[i] = 2u * (unsigned)(rb * 32 * K + tx * 16);
+            dbase[i] = pl ? wl : wh;
+            ddst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)((pl * 3 + tx) * WIN_SLOT + rb * 32 * 16));
         }
+    }
+    auto b_dma = [&](int t, int buf) {  // B tile t into buffer buf
+        const int s_ = t / 3, ty_ = t - 3 * (t / 3);
+        const unsigned kb = 2u * (unsigned)(s_ * 144 + ty_ * 48);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) win_glds(dbase[i], dlane + (dsu[i] + kb), ddst[i] + 2u * (unsigned)(buf * 6 * WIN_SLOT));
     };
 
+    // window pixel of this lane's block-0 output pixel 2m (tap (0, 0) = the window's top-left); its
+    // block-1 pixel 2m + 1 is the next one (W is even: the pair shares a row)
+    int wbe;
+    {
+        const int q = wm * 64 + 2 * l32;
+        wbe = (q >> __builtin_ctz(W)) * WP + (q & (W - 1));
+    }
 
     floatx16 acc[2][2], t[2][2];
 #pragma unroll
@@ -377,104 +367,34 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; t[i][j][r] = 0.f; }
 
-    // epilogue of the current job: undo the operand scales, + addend, NHWC store, IN statistics.  Its
-    // LDS scratch is B buffer 1 (read by the last k-tile, free after the last barrier; buffer 0 holds
-    // the next job's first B tile).  Not a window buffer: with zero padding their halo columns are
-    // zeroed once per workgroup and must stay zero
-    float* const elds = reinterpret_cast<float*>(Bs + (NP == 3 ? 6 : 9) * WIN_SLOT);
-    auto epilogue = [&]() {
-        // lane-dependent index math from opaque copies of the thread index: derived from loop
-        // invariants, the compiler hoisted it out of the job loop, holding registers through the k loop
-        int tid_e = tid;
-        asm volatile("" : "+v"(tid_e));
-        const int lane_e = tid_e & 63, wid_e = tid_e >> 6;
-        const int wm_e = wid_e >> 1, wn_e = wid_e & 1, l32_e = lane_e & 31, kh_e = lane_e >> 5;
-        const int eab = -(ea + eb);
-        const int p0 = y0 * W;  // the tile's first pixel within the image
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
-        const long long obase = (long long)n * a.H * W * a.Co;
-        auto ooff = [&](int i, int j, int r) {
-            const int pix = p0 + win_pix(wm_e, i, r, kh_e);
-            return obase + (long long)pix * a.Co + n0 + wn_e * 64 + j * 32 + l32_e;
-        };
-        if (addend) {  // wave-uniform: all 64 addend loads issued before the first use
-            floatx16 ad[2][2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) ad[i][j][r] = addend[ooff(i, j, r)];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r] + ad[i][j][r];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r];
-        }
-        if (parts) win_stats(acc, p0, n0, a.Co, wm_e, wn_e, lane_e, tid_e, elds, parts, (long long)n * a.tiles + tile);
-        if constexpr (IBW) {  // (y loaded here, after the stores: issuing them earlier spills ~70 VGPRs)
-            float yv[2][2][16];
-            win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm_e, wn_e, lane_e);
-            win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm_e, wn_e, lane_e, tid_e, tile, elds);
-        }
-    };
-    // after a job's epilogue: the next job (its first slice and B tile were staged by the last slice)
-    auto next_job = [&](int nj) {
-        __syncthreads();  // the epilogue's LDS reads are done before the next job stages into buffer 1
-        job = nj;
-        job_params(job, n, tile, n0, y0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    };
-
     if constexpr (NP == 1) {
         // f16: one product per fragment pair, so a 48-k tile holds only 12 MFMAs per wave; instead the
         // whole slice (9 taps, hi planes only) is staged per barrier: 36 MFMAs per wave between
         // barriers.  B slice by LDS-DMA, 36 blocks of 1 KB (tap, 32-row block), blocks w, w + 8, ...
         // of wave w.
-        // block i of this wave: source offset (without the lane and slice parts) and LDS destination,
-        // computed at each use from the wave index (held, they cost ten SGPRs through the loop)
-        auto sblk = [&](int i, unsigned& su, unsigned& dst) {
+        unsigned sdst[5], ssu[5];
+        {
             const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
             const int w = __builtin_amdgcn_readfirstlane(wid);
-            const int c = w + 8 * i < 36 ? w + 8 * i : 35, tap = c >> 2, rb = c & 3;
-            su = 2u * (unsigned)(rb * 32 * K + tap * 16);
-            dst = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)(tap * WIN_SLOT + rb * 32 * 16));
-        };
-        const bool fifth = __builtin_amdgcn_readfirstlane(wid) + 32 < 36;  // waves 0-3 issue a fifth block
-        auto s_dma = [&](int sl, int buf, int n0_) {
-            const unsigned kb = 2u * (unsigned)(sl * 144);
-            const unsigned dl = dlane(n0_);
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
-                if (i == 4 && !fifth) break;
-                unsigned su, dst;
-                sblk(i, su, dst);
-                win_glds(wh, dl + (su + kb), dst + 2u * (unsigned)(buf * 9 * WIN_SLOT));
+                const int c = w + 8 * i < 36 ? w + 8 * i : 35, tap = c >> 2, rb = c & 3;
+                ssu[i] = 2u * (unsigned)(rb * 32 * K + tap * 16);
+                sdst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)(tap * WIN_SLOT + rb * 32 * 16));
             }
+        }
+        const bool fifth = wid + 32 < 36;  // wave-uniform: waves 0-3 issue a fifth block
+        auto s_dma = [&](int sl, int buf) {
+            const unsigned kb = 2u * (unsigned)(sl * 144);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) win_glds(wh, dlane + (ssu[i] + kb), sdst[i] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
+            if (fifth) win_glds(wh, dlane + (ssu[4] + kb), sdst[4] + 2u * (unsigned)(buf * 9 * WIN_SLOT));
         };
         // prologue: every load of slice 0 (and the exponent's) in flight before the first store
-        s_dma(0, 0, n0);
-        win_load_u(1, 0, n, y0);
+        s_dma(0, 0);
+        win_load_u(1, 0);
         const float4 wp1[2] = {wq_[0], wq_[1]};
-        win_load_u(0, 0, n, y0);
+        win_load_u(0, 0);
         ea = f16x3_exp(rng, a.rng_n);
         asc = __builtin_ldexpf(1.f, ea);
         win_store_u(0, 0);
@@ -483,22 +403,18 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
         win_store_u(1, 0);
         __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
         __syncthreads();
-        auto sloop = [&](auto role_tag, bool more, int xn, int xy0, int xn0) {
+        auto sloop = [&](auto role_tag) {
             constexpr int ROLE = decltype(role_tag)::value;
             for (int s = 0; s < nslice; ++s) {
                 const int buf = s & 1;
-                // the last slice stages the next job's slice 0 (xn, xy0, xn0: its image, first row,
-                // column tile)
-                const bool lst = s == nslice - 1;
-                const int sn = lst ? (more ? 0 : s) : s + 1;
-                const int ln = lst && more ? xn : n, ly0 = lst && more ? xy0 : y0, ln0 = lst && more ? xn0 : n0;
+                const int sn = s + 1 < nslice ? s + 1 : s;
                 // the next slice into the other buffers (last read before this slice's top barrier):
                 // B by DMA now, the window's two units loaded now and stored after the kernel row that
                 // is this wave's staging point (ROLE 0: the last, ROLE 1: the second)
-                s_dma(sn, buf ^ 1, ln0);
-                win_load_u(1, sn, ln, ly0);  // unit 1 into wq_, moved to wq1
+                s_dma(sn, buf ^ 1);
+                win_load_u(1, sn);  // unit 1 into wq_, moved to wq1
                 const float4 wq1[2] = {wq_[0], wq_[1]};
-                win_load_u(0, sn, ln, ly0);
+                win_load_u(0, sn);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int ty = 0; ty < 3; ++ty) {
@@ -546,24 +462,15 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                     }
             }
         };
-        for (;;) {
-            const int nj = job + (int)gridDim.x;
-            const bool more = nj < total;  // (block-uniform)
-            int xn = n, xt, xn0 = n0, xy0 = y0;
-            if (more) job_params(nj, xn, xt, xn0, xy0);
-            if (wid >= 4) sloop(std::integral_constant<int, 1>{}, more, xn, xy0, xn0);
-            else sloop(std::integral_constant<int, 0>{}, more, xn, xy0, xn0);
-            epilogue();
-            if (!more) break;
-            next_job(nj);
-        }
+        if (wid >= 4) sloop(std::integral_constant<int, 1>{});
+        else sloop(std::integral_constant<int, 0>{});
     } else {
     // prologue: window of slice 0, B tile 0, every load (and the exponent's) in flight before the first
     // store
-    b_dma(0, 0, n0);
-    win_load_u(1, 0, n, y0);
+    b_dma(0, 0);
+    win_load_u(1, 0);
     const float4 wp1[2] = {wq_[0], wq_[1]};
-    win_load_u(0, 0, n, y0);
+    win_load_u(0, 0);
     ea = f16x3_exp(rng, a.rng_n);
     asc = __builtin_ldexpf(1.f, ea);
     win_store_u(0, 0);
@@ -579,15 +486,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     // every global load below is unconditional (offsets clamped at the end): a load under a branch
     // makes the compiler wait for all outstanding loads (vmcnt(0)) at the next consumer
     const int last = 3 * nslice - 1;
-    auto kloop = [&](auto role_tag, bool more, int xn, int xy0, int xn0) {
+    auto kloop = [&](auto role_tag) {
         constexpr int ROLE = decltype(role_tag)::value;
         for (int s = 0; s < nslice; ++s) {
             const int wbuf = s & 1;
-            // the last slice stages the next job's slice 0 (its B tile 0 by the last k-tile; xn, xy0, xn0:
-            // its image, first row, column tile)
-            const bool lst = s == nslice - 1;
-            const int sn = lst ? (more ? 0 : s) : s + 1;
-            const int ln = lst && more ? xn : n, ly0 = lst && more ? xy0 : y0;
+            const int sn = s + 1 < nslice ? s + 1 : s;
 #pragma unroll
             for (int ty = 0; ty < 3; ++ty) {
                 const int tt = 3 * s + ty, bbuf = tt & 1;
@@ -597,11 +500,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 if constexpr (ROLE == 1) {
                     if (ty >= 1) win_store_u(ty - 1, wbuf ^ 1);
                 }
-                if (ty < WIN_UNITS) win_load_u(ty, sn, ln, ly0);
-                // B tile tt + 1 into the other buffer (last read before the previous barrier); after the
-                // last tile the next job's tile 0, or a repeat nobody reads
-                if (tt < last) b_dma(tt + 1, bbuf ^ 1, n0);
-                else b_dma(more ? 0 : last, bbuf ^ 1, more ? xn0 : n0);
+                if (ty < WIN_UNITS) win_load_u(ty, sn);
+                // B tile tt + 1 into the other buffer (last read before the previous barrier); past the
+                // end a repeat nobody reads
+                b_dma(tt + 1 < last ? tt + 1 : last, bbuf ^ 1);
                 __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-tile
                 // A fragments of window pixels wbe + ty * WP + 0 .. 3: block i at tap tx takes fragment tx + i
                 f16x8 fh[4], fl[4];
@@ -657,26 +559,62 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 }
         }
     };
-    for (;;) {
-        const int nj = job + (int)gridDim.x;
-        const bool more = nj < total;  // (block-uniform)
-        int xn = n, xt, xn0 = n0, xy0 = y0;
-        if (more) job_params(nj, xn, xt, xn0, xy0);
-        if (wid >= 4) kloop(std::integral_constant<int, 1>{}, more, xn, xy0, xn0);  // (wave-uniform branch)
-        else kloop(std::integral_constant<int, 0>{}, more, xn, xy0, xn0);
+    if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
+    else kloop(std::integral_constant<int, 0>{});
 #if WIN_TIMING
-        tm2 = wall_clock64();
+    tm2 = wall_clock64();
 #endif
-        epilogue();
-        if (!more) break;
-        next_job(nj);
     }
+
+    // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
+    const int eab = -(ea + eb);
+    const int p0 = y0 * W;  // the tile's first pixel within the image
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+    const long long obase = (long long)n * a.H * W * a.Co;
+    auto ooff = [&](int i, int j, int r) {
+        const int pix = p0 + win_pix(wm, i, r, kh);
+        return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 32 + l32;
+    };
+
+    if (addend) {  // wave-uniform: all 64 addend loads issued before the first use
+        floatx16 ad[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ad[i][j][r] = addend[ooff(i, j, r)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r] + ad[i][j][r];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) out[ooff(i, j, r)] = acc[i][j][r];
+    }
+    if (parts) win_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(smem), parts,
+                         (long long)n * a.tiles + tile);
+    if constexpr (IBW) {  // (y loaded here, after the stores: issuing them earlier spills ~70 VGPRs)
+        float yv[2][2][16];
+        win_ibw_load(yv, ib, obase, p0, a.Co, n0, wm, wn, lane);
+        win_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(smem));
     }
 #if WIN_TIMING
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (tid == 0 && blockIdx.x < 16384) {
-        unsigned long long* g = g_win_t + 5 * blockIdx.x;
+    if (tid == 0 && L < 16384) {
+        unsigned long long* g = g_win_t + 5 * L;
         g[0] = tm0; g[1] = tm1; g[2] = tm2; g[3] = wall_clock64(); g[4] = __smid();
     }
 #endif
@@ -1142,30 +1080,13 @@ int win_check(const dcs_conv_desc& d, bool fwd) {
     return d.Ho == d.Hs + 2 && d.Wo == d.Ws + 2 && d.pt == 2 && d.pl == 2 && d.pad_mode == DCS_PAD_ZERO;
 }
 
-// compute units of the current device (cached per device)
-int device_cus() {
-    static int cache[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        cache[dev] = v;
-    }
-    return cache[dev];
-}
-
 int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* src, const void* wh, const void* wl,
                const int* wexp, const float* addend, float* out, Part* parts, hipStream_t s,
                const IbwArgs* ibw = nullptr) {
     WinArgs a;
     a.N = d.N; a.H = H; a.W = W; a.C = d.Cs; a.Co = d.Co; a.reflect = reflect;
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
-    // persistent workgroups, one per CU, when the slice count is even (a job's last slice stages the next
-    // job's first slice into buffer 0); otherwise one job per workgroup
-    const int jobs = a.N * a.tiles * a.gy;
-    const int cus = device_cus();
-    const unsigned blocks = (unsigned)(WIN_PERSIST && (d.Cs / 16) % 2 == 0 && jobs > cus ? cus : jobs);
+    const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
     const IbwArgs ib = ibw ? *ibw : IbwArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
 #define DCS_WIN_LAUNCH(NP_, IBW_)                                                                                   \
     hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                     \

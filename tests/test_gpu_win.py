@@ -202,13 +202,13 @@ def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
 
 
 @pytest.mark.parametrize("mode", ["f16x3", "f16"])
-def test_win_persistent_jobs_bit_identical(ops, mode):
-    """More jobs than CUs: N = 3 at 128 x 128 x 256 is 384 (tile, column tile) jobs on a grid of one
-    workgroup per CU, so workgroups run two jobs, the last slice of the first staging the second's first
-    slice and B tile (conv3_win_h3_kernel, launch_win).  Against the same convs one image at a time (128
-    jobs, one per workgroup): bit-identical outputs and IN statistics (forward), and data gradients with
+def test_win_batch_vs_per_image_bit_identical(ops, mode):
+    """A full-size batch (N = 3 at 128 x 128 x 256: 384 jobs, more than the GPU has CUs) against the same
+    convs one image at a time: bit-identical outputs and IN statistics (forward), data gradients with
     the residual addend bit-identical inside the two-pixel border (the border's reflection-ring pass
-    splits K by the batch size, so there the sums differ in order: 1e-6 of the largest value)."""
+    splits K by the batch size, so there the sums differ in order: 1e-6 of the largest value), and the
+    data gradient with the InstanceNorm-backward partial sums in its epilogue (the training step's form)
+    equal to the one without them."""
     ops.set_mma(mode)
     g = _geom(ops)
     N, H, W = 3, 128, 128
