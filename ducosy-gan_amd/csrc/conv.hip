@@ -1244,18 +1244,20 @@ __global__ __launch_bounds__(2 * BM, (MMA == MMA_BF16X6 || MMA == MMA_F16X3 || M
                     const int ol = oh == OOB_OFF ? OOB_OFF : oh + 2 * d.ldb;
                     if constexpr (BQ == 2) {
                         dst[BQ * sub] = buf_load4(b3rsrc, oh);
-                        if constexpr (!F1) dst[BQ * sub + 1] = buf_load4(b3rsrc, ol);
+                        // (f16: the lo slot zero, not left unwritten -- a partly written array was kept in
+                        // scratch memory)
+                        dst[BQ * sub + 1] = F1 ? make_float4(0.f, 0.f, 0.f, 0.f) : buf_load4(b3rsrc, ol);
                     } else {
                         const float2 h = buf_load2(b3rsrc, oh);
                         float2 l = make_float2(0.f, 0.f);
                         if constexpr (!F1) l = buf_load2(b3rsrc, ol);
                         dst[BQ * sub] = make_float4(h.x, h.y, l.x, l.y);
                     }
-                    continue;
-                }
-                const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
+                } else {
+                    const int off = (ok && col < d.ldb) ? (int)(((long long)(n0 + brow) * d.ldb + col) * 4) : OOB_OFF;
 #pragma unroll
-                for (int q = 0; q < BQ; ++q) dst[BQ * sub + q] = buf_load4(brsrc, off + 16 * q);
+                    for (int q = 0; q < BQ; ++q) dst[BQ * sub + q] = buf_load4(brsrc, off + 16 * q);
+                }
             }
             return;
         }
