@@ -370,7 +370,8 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
     if constexpr (NP == 1) {
         // f16: one product per fragment pair, so a 48-k tile holds only 12 MFMAs per wave; instead the
         // whole slice (9 taps, hi planes only) is staged per barrier: 36 MFMAs per wave between
-        // barriers.  B slice by LDS-DMA, 36 blocks of 1 KB (tap, 32-row block), blocks w, w + 8, ...
+        // barriers.  One accumulation level: the fp32 chain over all 9 C products (K <= 4608) rounds far
+        // below the fp16 operands' 2^-11, so the two-level sum of the f16x3 path buys nothing here.  B slice by LDS-DMA, 36 blocks of 1 KB (tap, 32-row block), blocks w, w + 8, ...
         // of wave w.
         unsigned sdst[5], ssu[5];
         {
@@ -440,7 +441,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                         for (int i = 0; i < 2; ++i)
 #pragma unroll
                             for (int j = 0; j < 2; ++j)
-                                t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], pb[tx & 1][j], t[i][j], 0, 0, 0);
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[tx + i], pb[tx & 1][j], acc[i][j], 0, 0, 0);
                     }
                     if (ty == (ROLE == 0 ? 2 : 1)) {  // staging point of this wave (kernel row 2 / 1)
                         __builtin_amdgcn_sched_barrier(0);
@@ -452,14 +453,6 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
                 }
                 __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs landed
                 __syncthreads();
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        acc[i][j] += t[i][j];
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
-                    }
             }
         };
         if (wid >= 4) sloop(std::integral_constant<int, 1>{});
