@@ -109,15 +109,17 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
 
     // window staging units (pixel, 8-channel half).  MODE 0: byte offset of the unit's channel 0 (-1:
-    // zero).  MODE 1: the unit's window (row, column) packed as row * 4096 + column (-1: none); the dy
-    // pixel depends on the iteration's phase
-    int uoff[SP_UNITS];
+    // zero).  MODE 1: the byte offset of the unit's dy pixel (2 (y0 + row), 2 (x0 + column)) at phase
+    // (0, 0), and in uvm the phases (qy, qx) whose pixel (2 (y0 + row) - qy, 2 (x0 + column) - qx) is in
+    // the image (bit 2 qy + qx); a phase moves the pixel by a block-uniform (qy 2 Ws + qx) C * 4 bytes
+    int uoff[SP_UNITS], uvm[SP_UNITS];
     const float rwp = 1.f / (float)WP;
 #pragma unroll
     for (int q = 0; q < SP_UNITS; ++q) {
         const int u = tid + q * SP_NT;
         const int wpix = u >> 1, h = u & 1;
         uoff[q] = -1;
+        uvm[q] = 0;
         if (wpix < npix) {
             // wpix / WP by a float reciprocal: exact, (wpix + 0.5) / WP stays >= 0.5 / WP from an integer
             const int wr = (int)(((float)wpix + 0.5f) * rwp), wc = wpix - wr * WP;
@@ -125,7 +127,12 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                 const int sy = y0 - 1 + wr, sx = x0 - 1 + wc;
                 if (sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws) uoff[q] = (((n * a.Hs + sy) * a.Ws + sx) * C + 8 * h) * 4;
             } else {
-                uoff[q] = wr * 4096 + wc;
+                uoff[q] = (((n * 2 * a.Hs + 2 * (y0 + wr)) * 2 * a.Ws + 2 * (x0 + wc)) * C + 8 * h) * 4;
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph) {
+                    const int cy = y0 - (ph >> 1) + wr, cx = x0 - (ph & 1) + wc;
+                    if (cy >= 0 && cy < a.Hs && cx >= 0 && cx < a.Ws) uvm[q] |= 1 << ph;
+                }
             }
         }
     }
@@ -137,12 +144,9 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         if constexpr (MODE == 0) {
             return uoff[q] >= 0 ? uoff[q] + it * 64 : 0x7fffffbf;
         } else {
-            const int ph = it / nslice, s = it - ph * nslice;
-            const int qy = ph >> 1, qx = ph & 1;  // the phase
-            const int cy = y0 - qy + (uoff[q] >> 12), cx = x0 - qx + (uoff[q] & 4095);  // phase sub-grid pixel
-            const bool ok = uoff[q] >= 0 && cy >= 0 && cy < a.Hs && cx >= 0 && cx < a.Ws;
-            const int h = (tid + q * SP_NT) & 1;
-            return ok ? ((((n * 2 * a.Hs + 2 * cy + qy) * 2 * a.Ws + 2 * cx + qx) * C + 8 * h) * 4 + s * 64) : 0x7fffffbf;
+            const int ph = it / nslice, s = it - ph * nslice;  // (block-uniform)
+            const int pshift = (s * 16 - ((ph >> 1) * 2 * a.Ws + (ph & 1)) * C) * 4;
+            return (uvm[q] >> ph) & 1 ? uoff[q] + pshift : 0x7fffffbf;
         }
     };
     auto win_load = [&](int it) {
