@@ -107,6 +107,14 @@ def cpu_baseline(img, blocks, cin, threads):
                       f"({c1 * 1e3:.0f} ms/step) = config1_img_s"}
 
 
+def all_finite(tensors) -> bool:
+    """One device-side verdict over every tensor: True when none holds a NaN or an infinity.  A step
+    whose numbers went bad must not be reported (round 5: a kernel that wrote NaN ran faster, since NaN
+    operands draw less power)."""
+    flags = [torch.isfinite(t.detach()).all().reshape(1) for t in tensors if t.numel()]
+    return bool(torch.cat(flags).all().item()) if flags else True
+
+
 def _pmc_record(mode):
     """HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction) and MFMA-busy of the
     dominant kernel from the committed rocprofv3 PMC passes (profiles/pmc_resconv_MODE.json, written
@@ -145,6 +153,8 @@ def main():
                     help="--dual: both models one after the other on each GPU (serial; trainer.py "
                          "ConcurrentCycleGANs), or split GPU groups (groups: soft tissue on the first half of the "
                          "ranks, lung on the second, each with its own all-reduce)")
+    ap.add_argument("--inject-nan", action="store_true",
+                    help="test hook: put a NaN into the synthetic inputs (the run must then exit non-zero)")
     ap.add_argument("--workload", default="step", choices=["step", "g_a2b"],
                     help="step: the full training step (BASELINE config 3/4); g_a2b: Generator_A2B forward + "
                          "backward only (BASELINE config 2, conv + CBAM kernels)")
@@ -184,6 +194,7 @@ def main():
         def step(b):
             out = G(b[0], b[1])
             out.backward(b[2])
+            return [out]
     elif args.dual:
         from modules.trainer import ConcurrentCycleGANs
         cins = (3, 2)
@@ -196,6 +207,10 @@ def main():
         batches = [_synthetic(args.batch, args.img, args.cin - 1, device, 100 * rank + i) for i in range(2)]
         step = lambda b: system.train_step(*b)
     models = 2 if args.dual and not groups else 1
+    if args.inject_nan:
+        for b in batches:
+            for t in (b if args.dual and not groups else [b]):
+                t[0].view(-1)[0] = float("nan")
 
     for i in range(args.warmup):
         step(batches[i % 2])
@@ -209,8 +224,9 @@ def main():
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     marks[0].record()
+    last = None
     for i in range(args.steps):
-        step(batches[i % 2])
+        last = step(batches[i % 2])
         marks[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
@@ -225,6 +241,20 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, med_ms = float(t[0]), float(t[1])
     n_launch, ms_launch, flop_launch = ops.PROBE.summary()
+    # outside the timing: the last timed step's loss terms (or Generator output) and every parameter
+    # must be finite, on every rank
+    outs = last if isinstance(last, (list, tuple)) else [last]
+    checked = [v for o in outs for v in (o.values() if isinstance(o, dict) else [o])]
+    if args.workload == "g_a2b":
+        checked += [p_ for p_ in G.parameters()] + [p_.grad for p_ in G.parameters()]
+    else:
+        sysms_all = runner.systems if (args.dual and not groups) else [system]
+        checked += [opt.flat_p for sm in sysms_all for opt in sm.optimizers]
+    finite = all_finite(checked)
+    if world > 1:
+        fl = torch.tensor([1 if finite else 0], device=device)
+        torch.distributed.all_reduce(fl, op=torch.distributed.ReduceOp.MIN)
+        finite = bool(fl.item())
     replicas_ok = None
     if world > 1:  # every replica of a model must still hold the same parameters
         from modules import parallel as par
@@ -270,6 +300,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "replicas_identical": replicas_ok,
+            "finite": finite,
             "dtype": MODE_DTYPE[args.mma],
             "data": "synthetic (U(-1,1) slices, Bernoulli(0.3) masks, resident in HBM; N(0,0.02) init)",
             "config": {
@@ -300,13 +331,17 @@ def main():
                 "gflop_per_launch": round(flop_launch / 1e9, 3),
             },
         }
-        if world == 1 and not args.no_cpu_baseline and not args.dual and args.workload == "step":
+        if world == 1 and finite and not args.no_cpu_baseline and not args.dual and args.workload == "step":
             threads = min(16, os.cpu_count() or 1)
             rec["cpu_baseline"] = cpu_baseline(args.img, args.blocks, args.cin, threads)
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    if not finite:
+        print("bench.py: the timed step produced non-finite losses or parameters; the record is invalid",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -32,6 +32,7 @@ __device__ __forceinline__ void split4h(const float4& a, float sc, f16x4& hi, f1
 // sixteen loads of a lane in flight at once (buffer loads past n read 0, the identity of a max over
 // maxima >= 0): one memory round trip at a kernel's start instead of one per 128 partials; the wave
 // maximum by DPP within rows of 16 lanes, then the four row maxima
+static_assert(DCS_RANGE_PARTS <= 1024, "f16x3_exp reduces at most 16 x 64 partial maxima");
 __device__ __forceinline__ int f16x3_exp(const float* __restrict__ rng, int n) {
     const int lane = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rng), (short)0, n * 4, 0x00020000);

@@ -792,8 +792,10 @@ extern "C" size_t dcs_head_dgrad_in_workspace_size(int N, int H, int W) {
 extern "C" int dcs_head_dgrad_in(const float* dy_out, const float* dy_rng, int dy_rng_n, const float* wk, int N, int H,
                                  int W, const float* y, const float* scale, const float* shift, int act, int mma,
                                  float* dy, void* ws, size_t ws_bytes, float* rng, void* stream) {
-    if (!dy_out || !dy_rng || dy_rng_n <= 0 || !wk || !y || !scale || !shift || !dy || !ws)
+    if (!dy_out || !dy_rng || !wk || !y || !scale || !shift || !dy || !ws)
         return fail(DCS_E_INVALID, "head_dgrad_in: null pointer");
+    if (dy_rng_n <= 0 || dy_rng_n > 1024)
+        return fail(DCS_E_INVALID, "head_dgrad_in: dy_rng_n must be in 1..1024 (range-record partials)");
     if (N <= 0 || H < 2 * HP_R + 2 || W < 2 * HP_R + 2 || act != DCS_ACT_RELU || (mma != DCS_MMA_F16X3 && mma != DCS_MMA_F16))
         return fail(DCS_E_INVALID, "head_dgrad_in: H, W >= 8, ReLU, f16x3 / f16 operands expected");
     if (ws_bytes < dcs_head_dgrad_in_workspace_size(N, H, W)) return fail(DCS_E_WORKSPACE, "head_dgrad_in: workspace too small");

@@ -414,7 +414,8 @@ bool stem_geom(const dcs_conv_desc* dp) {
            d.pt == 3 && d.pl == 3 && d.pad_mode == DCS_PAD_REFLECT && d.Ho == d.Hs && d.Wo == d.Ws && d.Hs >= 4 &&
            d.Ws >= 4 && d.s_c == 1 && d.s_w == 4 && d.s_h == (long long)d.Ws * 4 && d.s_n == (long long)d.Hs * d.Ws * 4 &&
            d.csplit == d.Cs && d.pro_act == DCS_ACT_NONE && d.epi_act == DCS_ACT_NONE &&
-           (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_b && d.rng_a_n > 0 && d.rng_b_n > 0;
+           (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a && d.rng_b && d.rng_a_n > 0 &&
+           d.rng_a_n <= 1024 && d.rng_b_n > 0 && d.rng_b_n <= 1024;  // f16x3_exp reads at most 1024 partials
 }
 }  // namespace
 

@@ -987,6 +987,12 @@ SWPlan sw_plan(const dcs_conv_desc& d) {
     return p;
 }
 
+// the epilogues index an image's output with 24-bit pixel products and 32-bit element offsets
+// (__umul24(opix, Co)): every output pixel index and element offset of one image must fit
+bool out_geom(const dcs_conv_desc& d) {
+    return (long long)d.Ho * d.Wo < (1LL << 24) && (long long)d.Ho * d.Wo * d.Co < 0x7fffff00LL;
+}
+
 bool tile_geom(int N, int Hs, int Ws, SubArgs* a) {
     const int TW = Ws < 128 ? Ws : 128;
     if (N <= 0 || Hs <= 0 || TW < 16 || 256 % TW || Ws % TW || Hs % (256 / TW)) return false;  // (TW even)
@@ -1006,7 +1012,7 @@ bool subpix_geom(const dcs_conv_desc& d, SubArgs* a) {
                     d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
                     d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
                     16LL * d.Co * d.Cs < (1LL << 30);
-    if (!ok || !tile_geom(d.N, d.Hs, d.Ws, a)) return false;
+    if (!ok || !out_geom(d) || !tile_geom(d.N, d.Hs, d.Ws, a)) return false;
     if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 32; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
     return true;
 }
@@ -1022,7 +1028,7 @@ bool subpix_dgrad_geom(const dcs_conv_desc& d, SubArgs* a) {
                     d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
                     d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
                     16LL * d.Co * d.Cs < (1LL << 30);
-    if (!ok || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
+    if (!ok || !out_geom(d) || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
     if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; }
     return true;
 }
@@ -1042,7 +1048,7 @@ bool s2_geom(const dcs_conv_desc& d, SubArgs* a) {
                         d.epi_act == DCS_ACT_NONE && (d.mma == DCS_MMA_F16X3 || d.mma == DCS_MMA_F16) && d.rng_a &&
                         d.rng_a_n > 0 && d.rng_a_n <= 1024 && (long long)d.N * d.Hs * d.Ws * d.Cs * 4 < 0x7fffff00LL - 64 &&
                         d.Co > 0 && 16LL * d.Co * d.Cs < (1LL << 30);
-    if (!common) return false;
+    if (!common || !out_geom(d)) return false;
     if (d.parity == 0) {  // forward
         if (d.Hs != 2 * d.Ho || d.Ws != 2 * d.Wo || d.Co % 128 || !tile_geom(d.N, d.Ho, d.Wo, a)) return false;
         if (a) { a->C = d.Cs; a->Co = d.Co; a->gy = d.Co / 128; a->cblk = d.Co / 64; a->rng_n = d.rng_a_n; a->pro_act = d.pro_act; }

@@ -34,6 +34,9 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef CLK_PROBE
 #define CLK_PROBE 0
 #endif
+#ifndef DCS_WIN16  // f16x3 residual convs on the 16x16x32 window kernel (0: the 32x32x16 one; A/B builds)
+#define DCS_WIN16 1
+#endif
 #if CLK_PROBE  // probe build only: core-clock and wall-clock counters per weight-gradient workgroup
 __device__ unsigned long long g_clk[4096 * 4];
 #endif
@@ -613,6 +616,413 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win_h3_kernel(WinArgs a, cons
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// The f16x3 window conv on v_mfma_f32_16x16x32_f16 (conv3_win16_kernel: same tile, operands, window
+// and B staging as conv3_win_h3_kernel above).  Both MFMA shapes do the same MACs per fragment byte,
+// but under the package power limit the 16x16x32 form sustains ~12 % more FLOP/s: 1758 against 1562
+// TFLOP/s of f16x3 products in a bare LDS-read + MFMA loop with every CU busy on random operands
+// (scripts/probes/mfma_shape_power.hip, profiles/r06b/; MI355X_MICROARCH.md, DVFS item 7).
+//
+// K = 32 per MFMA = two (slice, tap) units of 16 channels: the fragments' k groups 0, 1 (lanes 0-31)
+// take unit 2j, k groups 2, 3 (lanes 32-63) unit 2j + 1 -- the packed B's k = 16 unit + channel, so a
+// k-step is 32 consecutive packed k.  A slice has nine taps: the k-steps walk the 18 units of a PAIR
+// of slices, 9 k-steps, k-step 4 taking tap 8 of the even slice and tap 0 of the odd one.  The even
+// slice of a pair sits in window buffer 0, the odd one in buffer 1; the next odd slice is staged
+// during k-steps 0-3 (buffer 1 is free after the previous pair's k-step 8), the next even slice
+// during k-steps 5-8 (buffer 0 is free after k-step 4), one unit in flight per thread as above.
+// One barrier per k-step: B (128 output-channel rows x 32 k x 2 planes, 16 KB) by LDS-DMA into the
+// other of two buffers.  Per k-step and wave: 4 x 4 blocks of 16 x 16 x 3 products = 48 MFMAs.
+// Row block i of wave wm holds the 16 consecutive tile pixels wm * 64 + 16 i + (lane & 15) (W >= 16:
+// a block never crosses an image row), so the window needs no swizzle: the 16 lanes of a
+// ds_read_b128 lane group read 16 distinct 16-byte bank groups (pixel stride 32 B, the two channel
+// halves on odd / even groups).  A B row (output channel co) holds its four 8-k groups rotated by
+// 2 * ((co >> 2) & 3), which makes the B reads conflict-free too.  Two-level accumulation: chains of
+// 5 and 4 k-steps (160 / 128 k), added to the running sum.
+constexpr int W16_BSLOT = 128 * 32;  // halves per B plane and k-step
+
+__device__ __forceinline__ int w16_off(int buf, int pl, int wpix, int h) {
+    return ((buf * 2 + pl) * WIN_PIX + wpix) * 16 + 8 * h;
+}
+
+// IN statistics of the tile from the 16x16 accumulator layout (lane: column lane & 15 of each block,
+// rows 4 (lane >> 4) + r): per column over the lane's 16 pixels, merged with lanes ^ 16 and ^ 32, then
+// over the four pixel waves in a fixed order (as win_stats)
+__device__ __forceinline__ void win16_stats(const f32x4v (&acc)[4][4], int p0, int n0, int Co, int wm, int wn,
+                                            int lane, int tid, float* lds, Part* __restrict__ parts, long long chunk) {
+    Part* sp = reinterpret_cast<Part*>(lds);  // [4][128]
+    const int g = lane >> 4, m16 = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float s = 0.f, mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // increasing pixel order (first maximum)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = acc[i][j][r];
+                s += v;
+                if (v > mx) { mx = v; am = p0 + wm * 64 + 16 * i + 4 * g + r; }
+            }
+        float mean = s * (1.f / 16.f), m2 = 0.f, cnt = 16.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dv = acc[i][j][r] - mean;
+                m2 = fmaf(dv, dv, m2);
+            }
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {  // equal counts on both sides
+            const float mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64), mxb = __shfl_xor(mx, o, 64);
+            const int amb = __shfl_xor(am, o, 64);
+            const float dl = mb - mean;
+            m2 = m2 + m2b + dl * dl * (0.5f * cnt);
+            mean = mean + 0.5f * dl;
+            cnt *= 2.f;
+            if (mxb > mx || (mxb == mx && amb < am)) { mx = mxb; am = amb; }
+        }
+        if (g == 0) {
+            Part p;
+            p.cnt = cnt;
+            p.mean = mean;
+            p.m2 = m2;
+            p.mx = mx;
+            p.amax = am;
+            p.pad[0] = p.pad[1] = p.pad[2] = 0;
+            sp[wm * WIN_BN + wn * 64 + j * 16 + m16] = p;
+        }
+    }
+    __syncthreads();
+    if (tid < WIN_BN && n0 + tid < Co) {
+        Part a = sp[tid];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            const Part b = sp[w * WIN_BN + tid];
+            const float tot = a.cnt + b.cnt, dl = b.mean - a.mean;
+            a.mean += dl * (b.cnt / tot);
+            a.m2 += b.m2 + dl * dl * (a.cnt * b.cnt / tot);
+            a.cnt = tot;
+            if (b.mx > a.mx || (b.mx == a.mx && b.amax < a.amax)) { a.mx = b.mx; a.amax = b.amax; }
+        }
+        parts[chunk * Co + n0 + tid] = a;
+    }
+}
+
+// win_ibw for the 16x16 accumulator layout
+__device__ __forceinline__ void win16_ibw(const f32x4v (&acc)[4][4], const float (&yv)[4][4][4], const IbwArgs& ib,
+                                          int n, int p0, int H, int W, int Co, int n0, int wm, int wn, int lane,
+                                          int tid, int tile, float* lds) {
+    const int g = lane >> 4, m16 = lane & 15;
+    Sum2* sp = reinterpret_cast<Sum2*>(lds);  // [4][128]; the k-loop's last barrier freed the LDS
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + m16;
+        const float s = ib.sc[(long long)n * Co + col], b = ib.sh[(long long)n * Co + col];
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int pix = p0 + wm * 64 + 16 * i + 4 * g + r;
+                const int py = pix >> __builtin_ctz(W), px = pix & (W - 1);  // (W is a power of two)
+                if (py == 1 || py == H - 2 || px == 1 || px == W - 2) continue;  // the ring fold's pixels
+                const float xh = fmaf(yv[i][j][r], s, b);
+                const float gg = acc[i][j][r] * act_grad(xh, ib.act);
+                sa += gg;
+                sb = fmaf(gg, xh, sb);
+            }
+        sa += __shfl_xor(sa, 16, 64);  // the same operand pair on both lanes: order-free
+        sb += __shfl_xor(sb, 16, 64);
+        sa += __shfl_xor(sa, 32, 64);
+        sb += __shfl_xor(sb, 32, 64);
+        if (g == 0) sp[wm * 128 + wn * 64 + j * 16 + m16] = Sum2{sa, sb};
+    }
+    __syncthreads();
+    if (tid < 128 && n0 + tid < Co) {
+        Sum2 t = sp[tid];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            t.a += sp[w * 128 + tid].a;
+            t.b += sp[w * 128 + tid].b;
+        }
+        ib.parts[((long long)n * ib.nchunk + tile) * Co + n0 + tid] = t;
+    }
+}
+
+template <bool IBW, bool WIDE>  // WIDE: W >= 64
+__global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const float* __restrict__ src,
+                                                                const _Float16* __restrict__ wh,
+                                                                const _Float16* __restrict__ wl,
+                                                                const float* __restrict__ rng,
+                                                                const int* __restrict__ wexp,
+                                                                const float* __restrict__ addend,
+                                                                float* __restrict__ out, Part* __restrict__ parts,
+                                                                IbwArgs ib) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 2 * W16_BSLOT + 8];
+    _Float16* const Wn = smem;                        // [2 buffers][2 planes][WIN_PIX][16]
+    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;  // [2 buffers][2 planes][128 rows][32 k]
+    _Float16* const Wspare = Bs + 2 * 2 * W16_BSLOT;  // 16 bytes nobody reads
+
+    const int T = gridDim.x;
+    const int L = xcd_remap(blockIdx.x, T);
+    const int ntile = L % a.gy, mt = L / a.gy;
+    const int n = mt / a.tiles, tile = mt - n * a.tiles;
+    const int n0 = ntile * WIN_BN;
+    const int y0 = tile * a.R;
+    const int W = a.W, WP = a.W + 2, C = a.C;
+    const int K = 9 * C;
+    const int npair = C / 32;
+    const int lw = __builtin_ctz(W);
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int m16 = lane & 15, g = lane >> 4;
+
+    int ea = 0;
+    float asc = 1.f;
+    const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
+
+    // window staging units (as conv3_win_h3_kernel)
+    const int nint = (a.R + 2) * W;
+    int uoff[WIN_UNITS], uwd[WIN_UNITS];
+#pragma unroll
+    for (int q = 0; q < WIN_UNITS; ++q) {
+        const int u = tid + q * WIN_NT;
+        const int ip = u >> 1, h = u & 1;
+        uoff[q] = -1;
+        uwd[q] = 0;
+        if (ip < nint) {
+            const int wr = ip >> lw, sx = ip & (W - 1);
+            int dup = -1;
+            int sy = y0 - 1 + wr;
+            bool ok = true;
+            if (a.reflect) {
+                sy = sy < 0 ? -sy : (sy >= a.H ? 2 * a.H - 2 - sy : sy);
+                if (sx == 1) dup = wr * WP;
+                else if (sx == W - 2) dup = wr * WP + W + 1;
+            } else {
+                ok = sy >= 0 && sy < a.H;
+            }
+            uwd[q] = (wr * WP + sx + 2) | ((dup + 1) << 16);
+            if (ok) uoff[q] = (((n * a.H + sy) * W + sx) * C + 8 * h) * 4;
+        }
+    }
+    if (!a.reflect) {  // zero halo columns of both buffers and planes
+        for (int i = tid; i < 2 * 2 * (a.R + 2) * 2 * 2; i += WIN_NT) {
+            const int h = i & 1, side = (i >> 1) & 1, rest = i >> 2;
+            const int wr = rest % (a.R + 2), bp = rest / (a.R + 2);
+            *reinterpret_cast<f16x8*>(Wn + w16_off(bp >> 1, bp & 1, wr * WP + side * (W + 1), h)) = f16x8{};
+        }
+    }
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    float4 wq_[2];
+    auto win_load_u = [&](int q, int s) {
+        const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+        __builtin_memcpy(&wq_[0], &v0, 16);
+        __builtin_memcpy(&wq_[1], &v1, 16);
+    };
+    auto win_store_u = [&](int q, int buf) {
+        const int h = (tid + q * WIN_NT) & 1;
+        const int wp = (uwd[q] & 0xffff) - 1, wd = (uwd[q] >> 16) - 1;
+        f16x8 hi, lo;
+        split8h(wq_[0], wq_[1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 0, wp, h) : Wspare) = hi;
+        *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 1, wp, h) : Wspare) = lo;
+        if (wd >= 0) {
+            *reinterpret_cast<f16x8*>(Wn + w16_off(buf, 0, wd, h)) = hi;
+            *reinterpret_cast<f16x8*>(Wn + w16_off(buf, 1, wd, h)) = lo;
+        }
+    };
+
+    // B k-step by LDS-DMA: 16 blocks of 1 KB (plane, 16-row block), blocks 2w and 2w + 1 of wave w.  Lane
+    // L of a block lands at row L / 4, 16-byte slot L % 4, which holds the row's k group
+    // (L % 4 - 2 ((row >> 2) & 3)) & 3 (the rotation above; (row >> 2) & 3 = (L >> 4) & 3)
+    unsigned dsu[2], ddst[2];
+    const _Float16* dbase[2];
+    const unsigned dlane = 2u * (unsigned)((n0 + (lane >> 2)) * K + 8 * (((lane & 3) - 2 * ((lane >> 4) & 3)) & 3));
+    {
+        const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int b = __builtin_amdgcn_readfirstlane(wid) * 2 + i, pl = b >> 3, rb = b & 7;
+            dsu[i] = 2u * (unsigned)(rb * 16 * K);
+            dbase[i] = pl ? wl : wh;
+            ddst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)(pl * W16_BSLOT + rb * 16 * 32));
+        }
+    }
+    auto b_dma = [&](int j, int buf) {  // k-step j (packed k 32 j .. 32 j + 31) into B buffer buf
+        const unsigned kb = 2u * (unsigned)(j * 32);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) win_glds(dbase[i], dlane + (dsu[i] + kb), ddst[i] + 2u * (unsigned)(buf * 2 * W16_BSLOT));
+    };
+
+    // fragment offsets (halves).  A: window pixel of row block i at tap (0, 0) = ublk[i] + m16 (wave-
+    // uniform block part); k group g reads channel half g & 1 of the unit of its lane half.  B: row
+    // wn * 64 + 16 j + m16, k group g in slot (g + 2 ((m16 >> 2) & 3)) & 3.
+    // (W >= 64: the wave's four blocks are consecutive pixels of one row, block offsets 256 i halves
+    // fold into the reads' immediate offsets; narrower images add a uniform offset per block)
+    int ublk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = wm * 64 + 16 * i;
+        ublk[i] = __builtin_amdgcn_readfirstlane(((q >> lw) * WP + (q & (W - 1))) * 16);
+    }
+    const int alane = ublk[0] + m16 * 16 + 8 * (g & 1);
+    const int blane = (wn * 64 + m16) * 32 + 8 * ((g + 2 * ((m16 >> 2) & 3)) & 3);
+    const bool hiu = g >= 2;  // this lane's k groups take the k-step's second unit
+
+    f32x4v acc[4][4], t[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; t[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; }
+
+    // prologue: window of slice 0 (buffer 0) and B k-step 0, every load (and the exponent's) in flight
+    // before the first store
+    b_dma(0, 0);
+    win_load_u(1, 0);
+    const float4 wp1[2] = {wq_[0], wq_[1]};
+    win_load_u(0, 0);
+    ea = f16x3_exp(rng, a.rng_n);
+    asc = __builtin_ldexpf(1.f, ea);
+    win_store_u(0, 0);
+    wq_[0] = wp1[0];
+    wq_[1] = wp1[1];
+    win_store_u(1, 0);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
+    __syncthreads();
+
+    const int nstep = 9 * npair;
+    auto kloop = [&](auto role_tag) {
+        constexpr int ROLE = decltype(role_tag)::value;
+        for (int p = 0; p < npair; ++p) {
+            const int s_odd = 2 * p + 1;                                // staged in k-steps 0-3 (buffer 1)
+            const int s_even = 2 * p + 2 < 2 * npair ? 2 * p + 2 : 2 * p;  // k-steps 5-8 (buffer 0; past the end a repeat)
+#pragma unroll
+            for (int js = 0; js < 9; ++js) {
+                const int j = 9 * p + js, bbuf = j & 1;
+                const int ph = js < 4 ? js : js - 5;  // position in the staging window (js 4: none)
+                const int sbuf = js < 4 ? 1 : 0, ssl = js < 4 ? s_odd : s_even;
+                if constexpr (ROLE == 1) {
+                    if (js != 4 && (ph == 1 || ph == 3)) win_store_u(ph >> 1, sbuf);
+                }
+                if (js != 4 && (ph == 0 || ph == 2)) win_load_u(ph >> 1, ssl);
+                b_dma(j + 1 < nstep ? j + 1 : nstep - 1, bbuf ^ 1);
+                __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-step
+                // units 2 js, 2 js + 1 of the pair: window buffer (slice of the pair) and tap offset
+                const int u0 = 2 * js, u1 = 2 * js + 1;
+                const int t0 = u0 % 9, t1 = u1 % 9;
+                const int o0 = (u0 / 9) * 2 * WIN_PIX * 16 + ((t0 / 3) * WP + t0 % 3) * 16;
+                const int o1 = (u1 / 9) * 2 * WIN_PIX * 16 + ((t1 / 3) * WP + t1 % 3) * 16;
+                // (the lane bases pass through an empty asm each k-step: hoisted out of the loop, the
+                // nine k-steps' addresses were kept live and spilled)
+                int al_ = alane, bl_ = blane;
+                asm volatile("" : "+v"(al_), "+v"(bl_));
+                const _Float16* const Ak = Wn + al_ + (hiu ? o1 : o0);
+                f16x8 fh[4], fl[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
+                    fh[i] = *reinterpret_cast<const f16x8*>(Ak + bo);
+                    fl[i] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
+                }
+                const _Float16* const Bk = Bs + bbuf * 2 * W16_BSLOT + bl_;
+                f16x8 pbh[2], pbl[2];
+                pbh[0] = *reinterpret_cast<const f16x8*>(Bk);
+                pbl[0] = *reinterpret_cast<const f16x8*>(Bk + W16_BSLOT);
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb) {
+                    if (jb < 3) {  // the next column block's fragments ahead of this one's MFMAs
+                        pbh[(jb + 1) & 1] = *reinterpret_cast<const f16x8*>(Bk + (jb + 1) * 16 * 32);
+                        pbl[(jb + 1) & 1] = *reinterpret_cast<const f16x8*>(Bk + (jb + 1) * 16 * 32 + W16_BSLOT);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    const f16x8 bh = pbh[jb & 1], bl = pbl[jb & 1];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[i], bh, t[i][jb], 0, 0, 0);
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bl, t[i][jb], 0, 0, 0);
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bh, t[i][jb], 0, 0, 0);
+                    }
+                }
+                if constexpr (ROLE == 0) {
+                    if (js != 4 && (ph == 0 || ph == 2)) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        win_store_u(ph >> 1, sbuf);
+                    }
+                }
+                if (js == 4 || js == 8) {  // close the accumulation chain (160 / 128 k)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            acc[i][jj] += t[i][jj];
+                            // (pinned here: sunk to the next closure, the sum kept both chains live and spilled)
+                            asm volatile("" : "+v"(acc[i][jj]));
+                            t[i][jj] = f32x4v{0.f, 0.f, 0.f, 0.f};
+                        }
+                }
+                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
+                __syncthreads();
+            }
+        }
+    };
+    if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
+    else kloop(std::integral_constant<int, 0>{});
+
+    // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
+    const int eab = -(ea + eb);
+    const int p0 = y0 * W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], eab);
+    const long long obase = (long long)n * a.H * W * a.Co;
+    auto ooff = [&](int i, int j, int r) {
+        const int pix = p0 + wm * 64 + 16 * i + 4 * g + r;
+        return obase + (long long)pix * a.Co + n0 + wn * 64 + j * 16 + m16;
+    };
+    if (addend) {  // wave-uniform: all 64 addend loads issued before the first use
+        float ad[4][4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ad[i][j][r] = addend[ooff(i, j, r)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) out[ooff(i, j, r)] = acc[i][j][r] + ad[i][j][r];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) out[ooff(i, j, r)] = acc[i][j][r];
+    }
+    if (parts) win16_stats(acc, p0, n0, a.Co, wm, wn, lane, tid, reinterpret_cast<float*>(smem), parts,
+                           (long long)n * a.tiles + tile);
+    if constexpr (IBW) {
+        float yv[4][4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) yv[i][j][r] = ib.y[ooff(i, j, r)];
+        win16_ibw(acc, yv, ib, n, p0, a.H, W, a.Co, n0, wm, wn, lane, tid, tile, reinterpret_cast<float*>(smem));
+    }
+}
+
 // pre-split weight pack (dcs_pack_weights_h3): the range of the raw weights first, then every block
 // derives the same exponent and writes hi / lo fp16 planes of the slice-major B
 __global__ __launch_bounds__(256) void wrange_kernel(const float* __restrict__ w, long long n, float* __restrict__ parts) {
@@ -1081,7 +1491,21 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
     const IbwArgs ib = ibw ? *ibw : IbwArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-#define DCS_WIN_LAUNCH(NP_, IBW_)                                                                                   \
+    if (DCS_WIN16 && d.mma == DCS_MMA_F16X3 && W >= 16 && d.Cs % 32 == 0) {  // the 16x16x32 kernel
+        const _Float16* h = reinterpret_cast<const _Float16*>(wh);
+        const _Float16* l = reinterpret_cast<const _Float16*>(wl);
+#define DCS_WIN16_LAUNCH(IBW_, WIDE_)                                                                              \
+    hipLaunchKernelGGL((conv3_win16_kernel<IBW_, WIDE_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src, h, l, d.rng_a, wexp, \
+                       addend, out, parts, ib);
+        if (W >= 64) {
+            if (ibw) { DCS_WIN16_LAUNCH(true, true) } else { DCS_WIN16_LAUNCH(false, true) }
+        } else {
+            if (ibw) { DCS_WIN16_LAUNCH(true, false) } else { DCS_WIN16_LAUNCH(false, false) }
+        }
+#undef DCS_WIN16_LAUNCH
+        return check_launch("conv3_win16");
+    }
+#define DCS_WIN_LAUNCH(NP_, IBW_)                                                                                 \
     hipLaunchKernelGGL((conv3_win_h3_kernel<NP_, IBW_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src,                     \
                        reinterpret_cast<const _Float16*>(wh), reinterpret_cast<const _Float16*>(wl), d.rng_a, wexp, addend, \
                        out, parts, ib);

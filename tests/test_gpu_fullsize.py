@@ -223,3 +223,45 @@ def test_fullsize_default_mode_deterministic_and_close_to_f32():
     for k, v in out["f32"].items():
         assert _rel(out["d"][k], v) <= 1e-4, (prev, k, out["d"][k], v)
         assert _rel(out["x6"][k], v) <= 1e-4, ("bf16x6", k, out["x6"][k], v)
+
+
+def test_fullsize_f16_pair_finite_deterministic_and_close_to_f16x3():
+    """BASELINE config 5 at its image size on one GPU: the soft-tissue (cin 3) + lung (cin 2) pair
+    (ConcurrentCycleGANs, serial schedule; the reference trains them one after the other,
+    /root/reference/train.py:27-38) in the fp16 MFMA mode, 512 x 512, bs 2 per model, 9 blocks, two
+    steps.  Every loss term is finite, two runs are bit-identical, and each term is within 5e-3 of
+    the fp32-class f16x3 run at step 0 (pure forward) and 1e-2 of its scale after one Adam update
+    (the bars of the steps_64 fixture test, tests/test_gpu_concurrent.py)."""
+    import math
+
+    from modules.hip import ops
+    from modules.trainer import ConcurrentCycleGANs
+    cfg = [(3, 904), (2, 905)]
+    prev = ops.get_mma()
+    out = {}
+    try:
+        for tag, mode in (("f16", "f16"), ("f16_again", "f16"), ("f16x3", "f16x3")):
+            ops.set_mma(mode)
+            run = ConcurrentCycleGANs([_system(c, NB, prng.step_model_seeds(s)) for c, s in cfg], DEV)
+            steps = []
+            for i in range(2):
+                batches = [tuple(x.to(DEV) for x in _inputs(s, i, 2, c)) for c, s in cfg]
+                steps.append([{k: float(v) for k, v in o.items()} for o in run.train_step(batches)])
+            out[tag] = steps
+            del run
+            torch.cuda.empty_cache()
+    finally:
+        ops.set_mma(prev)
+    assert out["f16"] == out["f16_again"], "f16 step not bit-reproducible"
+    worst = {}
+    for i in range(2):
+        for j, model in enumerate(("soft", "lung")):
+            for k, v in out["f16"][i][j].items():
+                ref = out["f16x3"][i][j][k]
+                assert math.isfinite(v), (model, i, k, v)
+                scale = abs(ref) if i == 0 else max(abs(ref), abs(out["f16x3"][0][j][k]))
+                e = abs(v - ref) / max(scale, 1e-2)
+                worst[(i, model, k)] = e
+                assert e <= (5e-3 if i == 0 else 1e-2), (model, i, k, v, ref, e)
+    print("f16 pair vs f16x3 at 512x512, worst relative difference per step:",
+          {i: max((v, k) for (j, _, k), v in worst.items() if j == i) for i in range(2)})
