@@ -921,32 +921,42 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                 // nine k-steps' addresses were kept live and spilled)
                 int al_ = alane, bl_ = blane;
                 asm volatile("" : "+v"(al_), "+v"(bl_));
+                // issue order: the first MFMA's operands (B block 0, A block 0) first, so after the
+                // barrier every wave waits for 4 of its reads, not 10 (eight waves' reads queue at the LDS)
                 const _Float16* const Ak = Wn + al_ + (hiu ? o1 : o0);
-                f16x8 fh[4], fl[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
-                    fh[i] = *reinterpret_cast<const f16x8*>(Ak + bo);
-                    fl[i] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
-                }
                 const _Float16* const Bk = Bs + bbuf * 2 * W16_BSLOT + bl_;
-                f16x8 pbh[2], pbl[2];
-                pbh[0] = *reinterpret_cast<const f16x8*>(Bk);
-                pbl[0] = *reinterpret_cast<const f16x8*>(Bk + W16_BSLOT);
-#pragma unroll
-                for (int jb = 0; jb < 4; ++jb) {
-                    if (jb < 3) {  // the next column block's fragments ahead of this one's MFMAs
-                        pbh[(jb + 1) & 1] = *reinterpret_cast<const f16x8*>(Bk + (jb + 1) * 16 * 32);
-                        pbl[(jb + 1) & 1] = *reinterpret_cast<const f16x8*>(Bk + (jb + 1) * 16 * 32 + W16_BSLOT);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
+                f16x8 pbh[2], pbl[2], fh[4], fl[4];
+                auto rd_a = [&](int i) {
+                    const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
+                    fl[i] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
+                    fh[i] = *reinterpret_cast<const f16x8*>(Ak + bo);
+                };
+                auto rd_b = [&](int jb) {
+                    pbh[jb & 1] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32);
+                    pbl[jb & 1] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32 + W16_BSLOT);
+                };
+                auto mma = [&](int i, int jb) {
                     const f16x8 bh = pbh[jb & 1], bl = pbl[jb & 1];
+                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[i], bh, t[i][jb], 0, 0, 0);
+                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bl, t[i][jb], 0, 0, 0);
+                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bh, t[i][jb], 0, 0, 0);
+                };
+                rd_b(0);
+                rd_a(0);
+                __builtin_amdgcn_sched_barrier(0);  // the first block's operands issue first
+                rd_a(1);
+                rd_a(2);
+                rd_a(3);
+                rd_b(1);
+                __builtin_amdgcn_sched_barrier(0);  // every read in flight before the first wait
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[i], bh, t[i][jb], 0, 0, 0);
-                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bl, t[i][jb], 0, 0, 0);
-                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bh, t[i][jb], 0, 0, 0);
-                    }
+                for (int i = 0; i < 4; ++i) mma(i, 0);
+#pragma unroll
+                for (int jb = 1; jb < 4; ++jb) {
+                    if (jb < 3) rd_b(jb + 1);  // the next column block's fragments ahead of this one's MFMAs
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) mma(i, jb);
                 }
                 if constexpr (ROLE == 0) {
                     if (js != 4 && (ph == 0 || ph == 2)) {

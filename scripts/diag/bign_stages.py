@@ -17,6 +17,7 @@ HW, NB, CIN, seed = 512, 9, 3, 921
 
 
 REC = []
+HEAD_WK = []
 
 
 def _hook():
@@ -30,8 +31,18 @@ def _hook():
                 REC.append((name, t.detach().clone()))
             return r
         return g
-    for name in ("in_act_backward", "in_act_backward_parts", "head_dgrad_in", "cbam_backward", "act_backward"):
+    for name in ("in_act_backward", "in_act_backward_parts", "cbam_backward", "act_backward"):
         setattr(ops, name, wrap(name, getattr(ops, name)))
+    f_head = ops.head_dgrad_in
+
+    def head(dy_out, wk, y, st, act):  # its inputs too
+        HEAD_WK.append(wk.detach().clone())
+        for k, t in (("dy_out", dy_out), ("y", y), ("scale", st.scale), ("shift", st.shift)):
+            REC.append((f"head_in.{k}", t.detach().clone()))
+        r = f_head(dy_out, wk, y, st, act)
+        REC.append(("head_dgrad_in", r.detach().clone()))
+        return r
+    ops.head_dgrad_in = head
     ops.ConvGeom.dgrad = wrap("dgrad", ops.ConvGeom.dgrad)
 
 
@@ -76,6 +87,35 @@ def main():
         a = run(G, x[:h], m[:h], dout[:h])
         b = run(G, x[h:], m[h:], dout[h:])
         full = run(G, x, m, dout)
+        # replay the head's fused data gradient on the recorded inputs of the N-image call, whole and in
+        # halves, against the unfused path
+        from modules.hip.lib import ACT_RELU, DCS_PAD_REFLECT
+        from modules.hip.ops import ConvGeom, INStats
+        hk = {k.split(".", 1)[1]: v for k, v in full.items() if ".head_in." in k}
+        hk = {k.split(".")[-1]: v for k, v in hk.items()}
+        wk = HEAD_WK[-1]
+        rep = ops.head_dgrad_in(hk["dy_out"], wk, hk["y"], INStats(hk["scale"], hk["shift"]), ACT_RELU)
+        halves = [ops.head_dgrad_in(hk["dy_out"][a:b].contiguous(), wk, hk["y"][a:b].contiguous(),
+                                    INStats(hk["scale"][a:b].contiguous(), hk["shift"][a:b].contiguous()), ACT_RELU)
+                  for a, b in ((0, h), (h, n))]
+        g7 = ConvGeom(64, 1, 7, 1, (3, 3, 3, 3), DCS_PAD_REFLECT)
+        unf = ops.in_act_backward(g7.dgrad(hk["dy_out"].contiguous().view(n, HW, HW, 1), wk, HW, HW), hk["y"],
+                                  INStats(hk["scale"], hk["shift"]), ACT_RELU)
+        ref_full = [v for k, v in full.items() if k.endswith(".head_dgrad_in")][0]
+        # each half replayed on its own recorded inputs and weight pack
+        for nm, rr, wkr in (("half a", a, HEAD_WK[0]), ("half b", b, HEAD_WK[1])):
+            hi = {k.split(".")[-1]: v for k, v in rr.items() if ".head_in." in k}
+            got = [v for k, v in rr.items() if k.endswith(".head_dgrad_in")][0]
+            rp = ops.head_dgrad_in(hi["dy_out"], wkr, hi["y"], INStats(hi["scale"], hi["shift"]), ACT_RELU)
+            un = ops.in_act_backward(g7.dgrad(hi["dy_out"].contiguous().view(h, HW, HW, 1), wkr, HW, HW), hi["y"],
+                                     INStats(hi["scale"], hi["shift"]), ACT_RELU)
+            m2 = float(un.abs().max())
+            print(f"{nm}: in-step vs unfused {float((got - un).abs().max()) / m2:.3e}, replay vs unfused "
+                  f"{float((rp - un).abs().max()) / m2:.3e}, wk vs full wk {float((wkr - wk).abs().max()):.3e}", flush=True)
+        mx = float(unf.abs().max())
+        print("replay: whole vs unfused", float((rep - unf).abs().max()) / mx, "halves vs unfused",
+              float((torch.cat(halves) - unf).abs().max()) / mx, "in-step whole vs unfused",
+              float((ref_full - unf).abs().max()) / mx, flush=True)
         for k, v in full.items():
             if v.shape[0] != n:
                 continue

@@ -12,7 +12,7 @@ two steps):
     ContrastEdge are computed over the whole batch on every rank);
   * step-0 gradients: each optimizer's flat gradient after the all-reduce, as Adam receives it
     (FusedAdam.flat_g at step()), equals the whole-batch run's within relative L2 1e-5 for G, D_A
-    and D_B.  This is the check Adam's parameters cannot give: its first update is lr * sign(g),
+    and D_B (at 512 x 512 in f16x3: 5e-4, see the config-4 test).  This is the check Adam's parameters cannot give: its first update is lr * sign(g),
     invariant to the gradient's scale, so an all-reduce that divided by w^2, or a wrong
     grad_scale on the batch-coupled terms, would pass a parameter comparison;
   * the parameters after each step: the replicas follow the whole-batch run up to Adam's sign
@@ -166,11 +166,11 @@ def _rel_l2(got, ref):
     return float((got.double() - ref.double()).norm() / ref.double().norm().clamp_min(1e-30))
 
 
-def _param_delta(got, want, bound, where):
+def _param_delta(got, want, bound, where, med_tol=1e-6):
     for k, (g, w) in enumerate(zip(got, want)):
         d = (g - w).abs()
         med, mx = float(d.median()), float(d.max())
-        assert med <= 1e-6 and mx <= bound, (where, ("G", "D_A", "D_B")[k], med, mx)
+        assert med <= med_tol and mx <= bound, (where, ("G", "D_A", "D_B")[k], med, mx)
 
 
 def _param_slices(system):
@@ -188,7 +188,7 @@ def _param_slices(system):
     return out
 
 
-def _check_grads(got, want, where, slices=None):
+def _check_grads(got, want, where, slices=None, tol=GRAD_TOL):
     """Step-0 applied gradients of the three optimizers: relative L2 against the reference gradients
     (on failure, the parameters that carry most of the difference)."""
     errs = []
@@ -196,15 +196,15 @@ def _check_grads(got, want, where, slices=None):
         assert g is not None and w is not None and float(w.norm()) > 0, (where, k)
         e = _rel_l2(g, w)
         errs.append(e)
-        if e > GRAD_TOL and slices is not None:
+        if e > tol and slices is not None:
             d2 = sorted(((float((g[a:b].double() - w[a:b].double()).norm()), _rel_l2(g[a:b], w[a:b]), nm)
                          for nm, a, b in slices[k]), reverse=True)[:8]
             print(f"{where}: {('G', 'D_A', 'D_B')[k]} rel L2 {e:.3e}; largest contributions (|diff|, rel, name):", d2)
-        assert e <= GRAD_TOL, (where, ("G", "D_A", "D_B")[k], e)
+        assert e <= tol, (where, ("G", "D_A", "D_B")[k], e)
     return errs
 
 
-def _dp_vs_whole_batch(res, full, cfg, slices=None):
+def _dp_vs_whole_batch(res, full, cfg, slices=None, grad_tol=GRAD_TOL, med_tol=1e-6):
     n = cfg["n"]
     for r, rec in enumerate(res):
         assert rec["world"] == 2 and rec["shard"] == (r * n // 2, (r + 1) * n // 2)
@@ -219,7 +219,7 @@ def _dp_vs_whole_batch(res, full, cfg, slices=None):
     for rec in res:
         for g0, g1 in zip(rec["grads"][0], res[0]["grads"][0]):
             assert torch.equal(g0, g1), "the ranks applied different gradients"
-    errs = _check_grads(res[0]["grads"][0], full["grads"][0], "step 0", slices)
+    errs = _check_grads(res[0]["grads"][0], full["grads"][0], "step 0", slices, grad_tol)
     print(f"dp {cfg}: step-0 applied-gradient rel L2 (G, D_A, D_B) = {errs}")
     # later steps follow from parameters that agree to Adam's sign-flip bound
     for k, v in full["losses"][1].items():
@@ -227,7 +227,7 @@ def _dp_vs_whole_batch(res, full, cfg, slices=None):
         assert abs(m - v) <= 1e-3 * max(abs(v), abs(full["losses"][0][k]), 1e-2), (k, m, v)
     for i in range(STEPS):
         for rec in res:
-            _param_delta(rec["params"][i], full["params"][i], 2 * LR * (i + 1) + 1e-7, f"step {i}")
+            _param_delta(rec["params"][i], full["params"][i], 2 * LR * (i + 1) + 1e-7, f"step {i}", med_tol)
 
 
 def test_dp_two_ranks_equal_whole_batch(tmp_path):
@@ -236,15 +236,32 @@ def test_dp_two_ranks_equal_whole_batch(tmp_path):
     _dp_vs_whole_batch(res, full, SMALL, _param_slices(s))
 
 
-def test_dp_two_ranks_equal_whole_batch_config4_size(tmp_path):
+@pytest.mark.parametrize("mma", ["f32", "f16x3"])
+def test_dp_two_ranks_equal_whole_batch_config4_size(tmp_path, mma):
     """BASELINE config 4's per-rank work: two ranks at bs 8, 512 x 512, 9 blocks, cin 3, against one
-    process at bs 16 (the whole data-parallel batch)."""
-    res = _launch("dp", tmp_path, FULL, timeout=600)
-    s, full = _run(3, 0, FULL["n"], STEPS, FULL)
+    process at bs 16 (the whole data-parallel batch).
+
+    Exact f32 MFMA: the step-0 gradients within relative L2 1e-5, as at 64 x 64.  f16x3: the operands'
+    power-of-two scales come from the max |value| of each call's whole tensor, so a rank's 24-image
+    Generator call and the whole batch's 48-image call can round differently (at ~1e-7), and a
+    rounding that moves a pre-activation across a ReLU kink changes that pixel's gradient by O(1)
+    (scripts/diag/bign_stages.py: each call's fused head gradient equals the unfused path on its own
+    inputs within 4e-7).  The bar there is 5e-4 (measured 1.0e-4 for G, 1.6e-4 for D_A): a mis-scaled
+    all-reduce or grad_scale is still off by percent or more.  The parameters after the second Adam step
+    then differ by a median 2.5e-6 (bar 1e-5; f32: 1e-6), each flipped first-step sign moving an entry
+    by up to 2 lr."""
+    from modules.hip import ops
+    res = _launch("dp", tmp_path, FULL, mma=mma, timeout=600)
+    prev = ops.get_mma()
+    ops.set_mma(mma)
+    try:
+        s, full = _run(3, 0, FULL["n"], STEPS, FULL)
+    finally:
+        ops.set_mma(prev)
     slices = _param_slices(s)
     del s
     torch.cuda.empty_cache()
-    _dp_vs_whole_batch(res, full, FULL, slices)
+    _dp_vs_whole_batch(res, full, FULL, slices, *((1e-5, 1e-6) if mma == "f32" else (5e-4, 1e-5)))
 
 
 def test_dp_per_rank_loss_stats_equal_shard_runs(tmp_path):
