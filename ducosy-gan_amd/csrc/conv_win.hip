@@ -34,6 +34,9 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef CLK_PROBE
 #define CLK_PROBE 0
 #endif
+#ifndef WIN16_KO
+#define WIN16_KO 0
+#endif
 #ifndef DCS_WIN16  // f16x3 residual convs on the 16x16x32 window kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WIN16 1
 #endif
@@ -758,10 +761,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                                                                 const float* __restrict__ addend,
                                                                 float* __restrict__ out, Part* __restrict__ parts,
                                                                 IbwArgs ib) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 2 * 2 * W16_BSLOT + 8];
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 3 * 2 * W16_BSLOT + 8];
     _Float16* const Wn = smem;                        // [2 buffers][2 planes][WIN_PIX][16]
-    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;  // [2 buffers][2 planes][128 rows][32 k]
-    _Float16* const Wspare = Bs + 2 * 2 * W16_BSLOT;  // 16 bytes nobody reads
+    _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;  // [3 buffers][2 planes][128 rows][32 k]
+    _Float16* const Wspare = Bs + 3 * 2 * W16_BSLOT;  // 16 bytes nobody reads
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -817,7 +820,11 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     float4 wq_[2];
     auto win_load_u = [&](int q, int s) {
+#if WIN16_KO == 1  // probe build only (results wrong by design): every window load an L2 hit
+        const int off = uoff[q] >= 0 ? ((uoff[q] + s * 64) & 0xffff) : 0x7fffffbf;
+#else
         const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
+#endif
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
         u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
@@ -880,9 +887,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
 #pragma unroll
         for (int j = 0; j < 4; ++j) { acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; t[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; }
 
-    // prologue: window of slice 0 (buffer 0) and B k-step 0, every load (and the exponent's) in flight
-    // before the first store
+    // prologue: window of slice 0 (buffer 0) and B k-steps 0 and 1, every load (and the exponent's) in
+    // flight before the first store
     b_dma(0, 0);
+    b_dma(1, 1);
     win_load_u(1, 0);
     const float4 wp1[2] = {wq_[0], wq_[1]};
     win_load_u(0, 0);
@@ -896,73 +904,86 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     __syncthreads();
 
     const int nstep = 9 * npair;
+    // fragments carried across k-steps: the k-step's B (four column blocks) and the A row block in use
+    // plus the next one.  Row block i's MFMAs run with block i + 1's A (or, at i = 3, the next k-step's
+    // block 0) in flight, and during i = 3 each column block's B is replaced by the next k-step's right
+    // after its last MFMA: the reads a k-step needs are issued during the previous one, so no wave
+    // starts a k-step with its LDS reads queued behind eight waves' bursts.  That needs B k-step j + 1
+    // readable during k-step j: three B buffers (k-step j in buffer j % 3 = js % 3, the DMA for j + 2
+    // issued at the top of j), and each window slice published one k-step before its first fragment
+    // read (see the staging windows below).
+    f16x8 bh[4], bl[4], ah[2], al[2];
+    auto a_base = [&](int js_) {  // this lane's A base of k-step js_ of a pair (units 2 js_, 2 js_ + 1)
+        const int u0 = 2 * js_, u1 = 2 * js_ + 1;
+        const int t0 = u0 % 9, t1 = u1 % 9;
+        const int o0 = (u0 / 9) * 2 * WIN_PIX * 16 + ((t0 / 3) * WP + t0 % 3) * 16;
+        const int o1 = (u1 / 9) * 2 * WIN_PIX * 16 + ((t1 / 3) * WP + t1 % 3) * 16;
+        // (through an empty asm: hoisted out of the loop, the nine k-steps' bases stayed live and spilled)
+        int al_ = alane;
+        asm volatile("" : "+v"(al_));
+        return Wn + al_ + (hiu ? o1 : o0);
+    };
+    auto b_base = [&](int buf) {
+        int bl_ = blane;
+        asm volatile("" : "+v"(bl_));
+        return Bs + buf * 2 * W16_BSLOT + bl_;
+    };
+    auto rd_a = [&](const _Float16* Ak, int i, int slot) {
+        const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
+        al[slot] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
+        ah[slot] = *reinterpret_cast<const f16x8*>(Ak + bo);
+    };
+    auto rd_b = [&](const _Float16* Bk, int jb) {
+        bh[jb] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32);
+        bl[jb] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32 + W16_BSLOT);
+    };
+    {  // k-step 0's fragments (published by the prologue's barrier)
+        rd_a(a_base(0), 0, 0);
+        const _Float16* const B0 = b_base(0);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) rd_b(B0, jb);
+    }
     auto kloop = [&](auto role_tag) {
         constexpr int ROLE = decltype(role_tag)::value;
         for (int p = 0; p < npair; ++p) {
-            const int s_odd = 2 * p + 1;                                // staged in k-steps 0-3 (buffer 1)
-            const int s_even = 2 * p + 2 < 2 * npair ? 2 * p + 2 : 2 * p;  // k-steps 5-8 (buffer 0; past the end a repeat)
+            // staging windows (one unit in flight per thread): the odd slice 2p + 1 into window buffer 1 in
+            // k-steps 0-2 (buffer 1's previous slice had its last fragment read in the previous pair's
+            // k-step 8; its first read is k-step 4's block 0, issued in k-step 3), the next even slice into
+            // buffer 0 in k-steps 5-7 (last read of slice 2p in k-step 4; first read of slice 2p + 2 in
+            // k-step 8 for the next pair's k-step 0)
+            const int s_odd = 2 * p + 1;
+            const int s_even = 2 * p + 2 < 2 * npair ? 2 * p + 2 : 2 * p;  // past the end a repeat nobody reads
 #pragma unroll
             for (int js = 0; js < 9; ++js) {
-                const int j = 9 * p + js, bbuf = j & 1;
-                const int ph = js < 4 ? js : js - 5;  // position in the staging window (js 4: none)
-                const int sbuf = js < 4 ? 1 : 0, ssl = js < 4 ? s_odd : s_even;
-                if constexpr (ROLE == 1) {
-                    if (js != 4 && (ph == 1 || ph == 3)) win_store_u(ph >> 1, sbuf);
+                const int j = 9 * p + js;
+                const int ph = js < 3 ? js : (js >= 5 && js < 8 ? js - 5 : -1);  // position in a staging window
+                const int sbuf = js < 3 ? 1 : 0, ssl = js < 3 ? s_odd : s_even;
+                if constexpr (ROLE == 1) {  // unit ph - 1 stored at the top of the next k-step
+                    if (ph == 1 || ph == 2) win_store_u(ph - 1, sbuf);
                 }
-                if (js != 4 && (ph == 0 || ph == 2)) win_load_u(ph >> 1, ssl);
-                b_dma(j + 1 < nstep ? j + 1 : nstep - 1, bbuf ^ 1);
+                if (WIN16_KO != 3 && (ph == 0 || ph == 1)) win_load_u(ph, ssl);  // (probe build 3: no window loads)
+                b_dma(j + 2 < nstep ? j + 2 : nstep - 1, (js + 2) % 3);
                 __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-step
-                // units 2 js, 2 js + 1 of the pair: window buffer (slice of the pair) and tap offset
-                const int u0 = 2 * js, u1 = 2 * js + 1;
-                const int t0 = u0 % 9, t1 = u1 % 9;
-                const int o0 = (u0 / 9) * 2 * WIN_PIX * 16 + ((t0 / 3) * WP + t0 % 3) * 16;
-                const int o1 = (u1 / 9) * 2 * WIN_PIX * 16 + ((t1 / 3) * WP + t1 % 3) * 16;
-                // (the lane bases pass through an empty asm each k-step: hoisted out of the loop, the
-                // nine k-steps' addresses were kept live and spilled)
-                int al_ = alane, bl_ = blane;
-                asm volatile("" : "+v"(al_), "+v"(bl_));
-                // issue order: the first MFMA's operands (B block 0, A block 0) first, so after the
-                // barrier every wave waits for 4 of its reads, not 10 (eight waves' reads queue at the LDS)
-                const _Float16* const Ak = Wn + al_ + (hiu ? o1 : o0);
-                const _Float16* const Bk = Bs + bbuf * 2 * W16_BSLOT + bl_;
-                f16x8 pbh[2], pbl[2], fh[4], fl[4];
-                auto rd_a = [&](int i) {
-                    const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
-                    fl[i] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
-                    fh[i] = *reinterpret_cast<const f16x8*>(Ak + bo);
-                };
-                auto rd_b = [&](int jb) {
-                    pbh[jb & 1] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32);
-                    pbl[jb & 1] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32 + W16_BSLOT);
-                };
-                auto mma = [&](int i, int jb) {
-                    const f16x8 bh = pbh[jb & 1], bl = pbl[jb & 1];
-                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[i], bh, t[i][jb], 0, 0, 0);
-                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bl, t[i][jb], 0, 0, 0);
-                    t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[i], bh, t[i][jb], 0, 0, 0);
-                };
-                rd_b(0);
-                rd_a(0);
-                __builtin_amdgcn_sched_barrier(0);  // the first block's operands issue first
-                rd_a(1);
-                rd_a(2);
-                rd_a(3);
-                rd_b(1);
-                __builtin_amdgcn_sched_barrier(0);  // every read in flight before the first wait
+                const _Float16* const Ak = a_base(js);
+                const _Float16* const An = a_base((js + 1) % 9);
+                const _Float16* const Bn = b_base((js + 1) % 3);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) mma(i, 0);
-#pragma unroll
-                for (int jb = 1; jb < 4; ++jb) {
-                    if (jb < 3) rd_b(jb + 1);  // the next column block's fragments ahead of this one's MFMAs
+                for (int i = 0; i < 4; ++i) {
+                    if (i < 3) rd_a(Ak, i + 1, (i + 1) & 1);
+                    else rd_a(An, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) mma(i, jb);
+                    for (int jb = 0; jb < 4; ++jb) {
+                        const int sl = i & 1;
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[sl], bh[jb], t[i][jb], 0, 0, 0);
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], bl[jb], t[i][jb], 0, 0, 0);
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], bh[jb], t[i][jb], 0, 0, 0);
+                        if (i == 3) rd_b(Bn, jb);  // the next k-step's column block jb
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                 }
                 if constexpr (ROLE == 0) {
-                    if (js != 4 && (ph == 0 || ph == 2)) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        win_store_u(ph >> 1, sbuf);
-                    }
+                    if (ph == 0 || ph == 1) win_store_u(ph, sbuf);
                 }
                 if (js == 4 || js == 8) {  // close the accumulation chain (160 / 128 k)
 #pragma unroll
@@ -976,7 +997,9 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                         }
                 }
                 __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
+#if WIN16_KO != 2  // (probe build 2: no barrier)
                 __syncthreads();
+#endif
             }
         }
     };

@@ -8,7 +8,7 @@ for the G pair, 11.05 MB per D at cin 3) is averaged over the replicas by ONE st
 all-reduce after the backward, stream-ordered on the compute stream.  The exchange is not
 overlapped with the backward: RCCL's kernels on a queue of their own beside the backward's would
 share compute-unit pairs with it, the condition of the two-queue hazard (Config 5),
-for at most ~1 ms of a 250 ms step.  Initial weights
+for at most ~1 ms of a ~200 ms step.  Initial weights
 are broadcast from the group's first rank once; ``replicas_identical`` checks after a run that
 every replica still holds the same parameters (bench.py reports it).
 
