@@ -34,8 +34,8 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef CLK_PROBE
 #define CLK_PROBE 0
 #endif
-#ifndef WIN16_KO
-#define WIN16_KO 0
+#ifndef DCS_WGRAD16  // f16x3 residual weight gradient on the 16x16x32 kernel (0: the 32x32x16 one; A/B builds)
+#define DCS_WGRAD16 1
 #endif
 #ifndef DCS_WIN16  // f16x3 residual convs on the 16x16x32 window kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WIN16 1
@@ -820,11 +820,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     float4 wq_[2];
     auto win_load_u = [&](int q, int s) {
-#if WIN16_KO == 1  // probe build only (results wrong by design): every window load an L2 hit
-        const int off = uoff[q] >= 0 ? ((uoff[q] + s * 64) & 0xffff) : 0x7fffffbf;
-#else
         const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
-#endif
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
         u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
@@ -961,7 +957,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                 if constexpr (ROLE == 1) {  // unit ph - 1 stored at the top of the next k-step
                     if (ph == 1 || ph == 2) win_store_u(ph - 1, sbuf);
                 }
-                if (WIN16_KO != 3 && (ph == 0 || ph == 1)) win_load_u(ph, ssl);  // (probe build 3: no window loads)
+                if (ph == 0 || ph == 1) win_load_u(ph, ssl);
                 b_dma(j + 2 < nstep ? j + 2 : nstep - 1, (js + 2) % 3);
                 __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-step
                 const _Float16* const Ak = a_base(js);
@@ -997,9 +993,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                         }
                 }
                 __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
-#if WIN16_KO != 2  // (probe build 2: no barrier)
                 __syncthreads();
-#endif
             }
         }
     };
@@ -1448,6 +1442,259 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// The residual weight gradient on v_mfma_f32_16x16x32_f16 (f16x3; same workgroup, rolling window,
+// staging and slabs as wgrad3_win_h3_kernel above, the MFMA shape the window conv moved to for the
+// power-limited clock, conv3_win16_kernel).  M = 16 output channels, N = 16 input channels, K = 32
+// pixels of the row: two k-steps per 64-pixel row.  A SIMD's waves w and w + 4 still share one
+// 32 x 32 (co, ci) block = 2 x 2 sub-blocks of 16 x 16; wave w takes taps 0-3 on all four
+// sub-blocks and tap 4 on the co sub-block 0, wave w + 4 taps 5-8 and tap 4 on co sub-block 1: 18
+// accumulators each, no shared accumulator to merge.  Fragments by ds_read_b64_tr_b16 (lane group
+// g = lane >> 4 takes pixels 8 g .. 8 g + 7 of the k-step, lane 4 q + p of the group addresses pixel
+// row q (+ 4 for the second read), channels 4 p .. 4 p + 3).  The 16-byte channel units of a pixel
+// row are XOR-swizzled by bits 1 and 3 of the pixel (ww16_swz), which spreads the eight pixel rows
+// of a 32-lane read group (rows r .. r + 3 and r + 8 .. r + 11) over all 64 banks at any tap offset;
+// the unit index's bit 1 is the 16-channel sub-block, so the second sub-block's fragment is the first
+// one's offset XOR 16 halves.
+__device__ __forceinline__ int ww16_swz(int pix) { return (((pix >> 1) & 1) << 2) | (((pix >> 3) & 1) << 1); }
+
+__device__ __forceinline__ f16x8 ww16_frag(const _Float16* p1, const _Float16* p2) {
+    const wshortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wshortx4*)(p1));
+    const wshortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wshortx4*)(p2));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const float* __restrict__ dy,
+                                                                const float* __restrict__ src,
+                                                                const float* __restrict__ rnga,
+                                                                const float* __restrict__ rngb,
+                                                                float* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
+    _Float16* const Xr = smem;                 // [4 slots][2 planes][66][64]
+    _Float16* const Dy = smem + 4 * WW_XROW;   // [2 buffers][2 planes][64][64]
+
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = a.gco * a.gci;
+    const int tile = L % ntile, split = L / ntile;
+    const int co0 = (tile % a.gco) * 64, ci0 = (tile / a.gco) * 64;
+    const int rc = split % a.rchunks, rest = split / a.rchunks;
+    const int strip = rest % a.strips, n = rest / a.strips;
+    const int x0 = strip * WW_SW;
+    const int H = a.H, W = a.W, C = a.C, Co = a.Co;
+    const int y_beg = rc * a.rows_per;
+    const int y_end = y_beg + a.rows_per < H ? y_beg + a.rows_per : H;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int cob = wid & 1, cib = (wid >> 1) & 1, half = wid >> 2;
+
+    int ea = 0, eb = 0;
+    float asc = 1.f, bsc = 1.f;
+
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int OOB = 0x7fffffbf;
+
+    int doff, dls;
+    {
+        const int pix = tid >> 3, cu = tid & 7;
+        doff = ((x0 + pix) * Co + co0 + 8 * cu) * 4;
+        dls = pix * 64 + 8 * (cu ^ ww16_swz(pix));
+    }
+    int xoff[WW_XU], xls[WW_XU];
+#pragma unroll
+    for (int q = 0; q < WW_XU; ++q) {
+        const int u = tid + q * WW_NT, wc = u >> 3, cu = u & 7;
+        xoff[q] = -1;
+        xls[q] = -1;
+        if (wc < WW_WP) {
+            int sx = x0 - 1 + wc;
+            bool ok = true;
+            if (a.reflect) sx = sx < 0 ? -sx : (sx >= W ? 2 * W - 2 - sx : sx);
+            else ok = sx >= 0 && sx < W;
+            if (ok) xoff[q] = (sx * C + ci0 + 8 * cu) * 4;
+            xls[q] = wc * 64 + 8 * (cu ^ ww16_swz(wc));
+        }
+    }
+    float4 dr[2], xr[WW_XU][2];
+    auto ld_dy = [&](int y) {
+        const int rb = ((n * H + y) * W) * Co * 4;
+        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff, 0, 0);
+        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff + 16, 0, 0);
+        __builtin_memcpy(&dr[0], &v0, 16);
+        __builtin_memcpy(&dr[1], &v1, 16);
+    };
+    auto ld_x = [&](int r) {  // logical source row r in [-1, H]
+        int sy = r;
+        bool ok = true;
+        if (a.reflect) sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
+        else ok = sy >= 0 && sy < H;
+        const int rb = ((n * H + sy) * W) * C * 4;
+#pragma unroll
+        for (int q = 0; q < WW_XU; ++q) {
+            const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
+            __builtin_memcpy(&xr[q][0], &v0, 16);
+            __builtin_memcpy(&xr[q][1], &v1, 16);
+        }
+    };
+    auto st_dy = [&](int buf) {
+        f16x8 hi, lo;
+        split8h(dr[0], dr[1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls) = hi;
+        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls) = lo;
+    };
+    auto st_x = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < WW_XU; ++q) {
+            if (xls[q] >= 0) {
+                f16x8 hi, lo;
+                split8h(xr[q][0], xr[q][1], bsc, hi, lo);
+                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
+                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
+            }
+        }
+    };
+
+    // transposed-read lane offsets (halves) of k-step 0 and the first sub-block: A (dy) at pixel row
+    // 8 g + q (+ 4: the second read, same swizzle), channel 32 cob + 4 p; B (source) at pixel row
+    // 8 g + q + tx, whose second read can carry into bit 3 (its own offset)
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    int aoff, boff1[3], boff2[3];
+    {
+        const int r = 8 * g + q, c = 32 * cob + 4 * pp;
+        aoff = r * 64 + 8 * ((c >> 3) ^ ww16_swz(r)) + (c & 7);
+        const int cb = 32 * cib + 4 * pp;
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+            const int p1 = r + tx, p2 = r + 4 + tx;
+            boff1[tx] = p1 * 64 + 8 * ((cb >> 3) ^ ww16_swz(p1)) + (cb & 7);
+            boff2[tx] = p2 * 64 + 8 * ((cb >> 3) ^ ww16_swz(p2)) + (cb & 7);
+        }
+    }
+
+    f32x4v acc[18], t[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) { acc[i] = f32x4v{0.f, 0.f, 0.f, 0.f}; t[i] = f32x4v{0.f, 0.f, 0.f, 0.f}; }
+
+    // prologue: source rows y_beg - 1 .. y_beg + 1 into their ring slots, dy row y_beg; every row's loads
+    // (and the exponents') in flight before the first store
+    {
+        float4 px_[3][WW_XU][2], pd_[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int r = y_beg - 1 + i;
+            ld_x(r <= H ? r : H);
+#pragma unroll
+            for (int u = 0; u < WW_XU; ++u) { px_[i][u][0] = xr[u][0]; px_[i][u][1] = xr[u][1]; }
+        }
+        ld_dy(y_beg);
+        pd_[0] = dr[0];
+        pd_[1] = dr[1];
+        ea = f16x3_exp(rnga, a.rng_a_n);
+        eb = f16x3_exp(rngb, a.rng_b_n);
+        asc = __builtin_ldexpf(1.f, ea);
+        bsc = __builtin_ldexpf(1.f, eb);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int u = 0; u < WW_XU; ++u) { xr[u][0] = px_[i][u][0]; xr[u][1] = px_[i][u][1]; }
+            st_x((y_beg - 1 + i) & 3);
+        }
+        dr[0] = pd_[0];
+        dr[1] = pd_[1];
+        st_dy(y_beg & 1);
+    }
+    __syncthreads();
+
+    // one row: two k-steps of 32 pixels; per k-step the A fragments of both co sub-blocks, then the
+    // wave's five taps with the next tap's B fragments read ahead of the current one's MFMAs
+    auto row = [&](int y, auto tag) {
+        constexpr int R = decltype(tag)::value;
+        const _Float16* const Db = Dy + (y & 1) * WW_DROW;
+        const _Float16* Xs[3];
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + 3 + ty) & 3) * WW_XROW;  // row y - 1 + ty
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            f16x8 ah[2], al[2];
+#pragma unroll
+            for (int cs = 0; cs < 2; ++cs) {
+                const int o = (aoff ^ (16 * cs)) + kk * 32 * 64;
+                ah[cs] = ww16_frag(Db + o, Db + o + 4 * 64);
+                al[cs] = ww16_frag(Db + WW_SW * 64 + o, Db + WW_SW * 64 + o + 4 * 64);
+            }
+            // (tap, ci sub-block) pairs of the wave: the next pair's B fragments read ahead of this one's MFMAs
+            f16x8 bh[2], bl[2];
+            auto rd_b = [&](int jp, int slot) {
+                const int tt = jp >> 1, ns = jp & 1;
+                const int tap = R == 0 ? tt : (tt < 4 ? 5 + tt : 4);
+                const int ty = tap / 3, tx = tap % 3;
+                const int o1 = (boff1[tx] ^ (16 * ns)) + kk * 32 * 64, o2 = (boff2[tx] ^ (16 * ns)) + kk * 32 * 64;
+                bh[slot] = ww16_frag(Xs[ty] + o1, Xs[ty] + o2);
+                bl[slot] = ww16_frag(Xs[ty] + WW_WP * 64 + o1, Xs[ty] + WW_WP * 64 + o2);
+            };
+            rd_b(0, 0);
+#pragma unroll
+            for (int jp = 0; jp < 10; ++jp) {
+                if (jp < 9) rd_b(jp + 1, (jp + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+                const int tt = jp >> 1, ns = jp & 1;
+                const int tap = R == 0 ? tt : (tt < 4 ? 5 + tt : 4);
+                const int sl = jp & 1;
+#pragma unroll
+                for (int cs = 0; cs < 2; ++cs) {
+                    if (tap == 4 && cs != R) continue;  // tap 4: co sub-block R only
+                    const int idx = tap == 4 ? 16 + ns : (R == 0 ? tap : tap - 5) * 4 + cs * 2 + ns;
+                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cs], bh[sl], t[idx], 0, 0, 0);
+                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bl[sl], t[idx], 0, 0, 0);
+                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bh[sl], t[idx], 0, 0, 0);
+                }
+            }
+            if (kk == 0) {  // stage the rows loaded for the next barrier (buffers no row of this one reads)
+                __builtin_amdgcn_sched_barrier(0);
+                st_dy((y + 1) & 1);
+                st_x((y + 2) & 3);
+            }
+        }
+    };
+
+#pragma unroll 1
+    for (int y = y_beg; y < y_end; ++y) {
+        ld_dy(y + 1 < y_end ? y + 1 : y);
+        ld_x(y + 2 <= H ? y + 2 : H);
+        if (half == 0) row(y, std::integral_constant<int, 0>{});
+        else row(y, std::integral_constant<int, 1>{});
+        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {  // chains of two rows (128 pixels)
+#pragma unroll
+            for (int i = 0; i < 18; ++i) {
+                acc[i] += t[i];
+                asm volatile("" : "+v"(acc[i]));  // (pinned: see conv3_win16_kernel)
+                t[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        __syncthreads();
+    }
+
+    // epilogue: undo the operand scales, slab [split][co][tap * C + ci]; lane holds rows 4 g + r (co)
+    // and column lane & 15 (ci) of each 16 x 16 sub-block
+    const int eab = -(ea + eb);
+    float* const slab = ws + (long long)split * Co * 9 * C;
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+        int tap, cs, ns;
+        if (i >= 16) { tap = 4; cs = half; ns = i - 16; }
+        else { tap = (half == 0 ? 0 : 5) + i / 4; cs = (i >> 1) & 1; ns = i & 1; }
+        const int col = ci0 + 32 * cib + 16 * ns + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rowc = co0 + 32 * cob + 16 * cs + 4 * g + r;
+            slab[(long long)rowc * 9 * C + tap * C + col] = __builtin_ldexpf(acc[i][r], eab);
+        }
+    }
+}
+
 struct WWPlan {
     int strips, rchunks, rows_per, nsplit;
 };
@@ -1495,6 +1742,8 @@ int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, fl
     const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
     if (d.mma == DCS_MMA_F16)
         hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    else if (DCS_WGRAD16)
+        hipLaunchKernelGGL(wgrad3_win16_kernel, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
     else
         hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
     const int e = check_launch("wgrad3_win");

@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_win.py > gpurun_out/r06p_win.log 2>&1 || { echo TESTFAIL; exit 1; }
+timeout -k 10 120 python scripts/kbench.py --only res --mma f16x3 --batch 16 --reps 30 > gpurun_out/r06p_kb16.log 2>&1 || exit 1
+DUCOSY_HIP_LIB=$PWD/ducosy-gan_amd/lib/libducosy_hip_w32.so timeout -k 10 120 python scripts/kbench.py --only res --mma f16x3 --batch 16 --reps 30 > gpurun_out/r06p_kb32.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/r06p_bench16.log 2>&1 || exit 1
+DUCOSY_HIP_LIB=$PWD/ducosy-gan_amd/lib/libducosy_hip_w32.so timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/r06p_bench32.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_fullsize.py tests/test_gpu_train.py > gpurun_out/r06p_full.log 2>&1 || { echo FULLFAIL; exit 1; }
