@@ -320,6 +320,77 @@ __global__ __launch_bounds__(256) void cb_bwd_dsa64x_kernel(const float* __restr
     }
 }
 
+// b1 + the dout half of b3, for C == 256: grid (image, chunk) over b3's pixel chunks; each wave walks
+// its plane's pixels of the chunk (PX at a time, every load issued together) and writes dpre[p] as
+// cb_bwd_dsa64x_kernel (same sums in the same order), while accumulating per channel the part of b3's
+// sums that needs dout: sum (dout g) z and sum dout g (g = sa), folded over the four planes in fixed
+// order into p1[n][chunk][c].  cb_bwd_sums4_kernel<true> then adds the dsin half reading y but not
+// dout, so the pair reads dout once (b1 and b3 each read it before)
+template <int PX>
+__global__ __launch_bounds__(256) void cb_bwd_dsa_sums_kernel(const float* __restrict__ dout, const float* __restrict__ y,
+                                                              const float* __restrict__ sc, const float* __restrict__ sh,
+                                                              const float* __restrict__ ca, const float* __restrict__ sa,
+                                                              int HW, int nchunk, float* __restrict__ dpre,
+                                                              Sum2* __restrict__ p1) {
+    __shared__ float4 s_a[256], s_b[256];
+    const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, plane = tid >> 6;
+    const int p_per = (HW + nchunk - 1) / nchunk;
+    const int p0 = chunk * p_per;
+    const int pend = min(HW, p0 + p_per);
+    const float4 s = reinterpret_cast<const float4*>(sc + (long long)n * 256)[lane];
+    const float4 b = reinterpret_cast<const float4*>(sh + (long long)n * 256)[lane];
+    const float4 a = reinterpret_cast<const float4*>(ca + (long long)n * 256)[lane];
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    const long long base = (long long)n * HW;
+    for (int p = p0 + plane; p < pend; p += 4 * PX) {
+        float4 v[PX], d[PX];
+        float gg[PX];
+#pragma unroll
+        for (int k = 0; k < PX; ++k) {  // pixels past the chunk: a clamped repeat, masked below
+            const int pk = p + 4 * k < pend ? p + 4 * k : pend - 1;
+            v[k] = reinterpret_cast<const float4*>(y + (base + pk) * 256)[lane];
+            d[k] = reinterpret_cast<const float4*>(dout + (base + pk) * 256)[lane];
+            gg[k] = sa[base + pk];
+        }
+#pragma unroll
+        for (int k = 0; k < PX; ++k) {
+            const bool ok = p + 4 * k < pend;  // (wave-uniform)
+            const float zx = fmaf(v[k].x, s.x, b.x), zy = fmaf(v[k].y, s.y, b.y);
+            const float zz = fmaf(v[k].z, s.z, b.z), zw = fmaf(v[k].w, s.w, b.w);
+            float acc = 0.f;
+            acc = fmaf(d[k].x, zx * a.x, acc);
+            acc = fmaf(d[k].y, zy * a.y, acc);
+            acc = fmaf(d[k].z, zz * a.z, acc);
+            acc = fmaf(d[k].w, zw * a.w, acc);
+            acc = wave_sum(acc);
+            if (ok) {
+                if (lane == 0) dpre[base + p + 4 * k] = acc * gg[k] * (1.f - gg[k]);
+                const float g = gg[k];
+                const float dx = d[k].x * g, dy_ = d[k].y * g, dz = d[k].z * g, dw = d[k].w * g;
+                A.x = fmaf(dx, zx, A.x); A.y = fmaf(dy_, zy, A.y); A.z = fmaf(dz, zz, A.z); A.w = fmaf(dw, zw, A.w);
+                B.x += dx; B.y += dy_; B.z += dz; B.w += dw;
+            }
+        }
+    }
+    s_a[tid] = A;
+    s_b[tid] = B;
+    __syncthreads();
+    if (plane == 0) {
+#pragma unroll
+        for (int l = 1; l < 4; ++l) {
+            const float4 u = s_a[l * 64 + lane], w = s_b[l * 64 + lane];
+            A.x += u.x; A.y += u.y; A.z += u.z; A.w += u.w;
+            B.x += w.x; B.y += w.y; B.z += w.z; B.w += w.w;
+        }
+        Sum2* o = p1 + ((long long)n * nchunk + chunk) * 256 + 4 * lane;
+        o[0] = Sum2{A.x, B.x};
+        o[1] = Sum2{A.y, B.y};
+        o[2] = Sum2{A.z, B.z};
+        o[3] = Sum2{A.w, B.w};
+    }
+}
+
 // b2: dsin[q][ch] = sum_t wsa[ch][t] * dpre[q - (t - r)]  (adjoint of the zero-padded conv)
 __global__ void cb_bwd_dsin_kernel(const float* __restrict__ dpre, const float* __restrict__ wsa, int H, int W, int ksa,
                                    long long P, float* __restrict__ dsin) {
@@ -438,34 +509,49 @@ __global__ __launch_bounds__(256) void cb_bwd_sums_kernel(const float* __restric
 // b3 (float4 form, C % 4 == 0 and C/4 dividing 256): thread t owns channels 4*(t % C4).. of
 // pixel lane t / C4; a wave reads whole pixel rows (C = 256: one 1 KiB row per load), the
 // pixel lanes are folded in fixed order through LDS.  Same sums as cb_bwd_sums_kernel.
+// HALF: the dsin half only (no dout read), plus the dout half cb_bwd_dsa_sums_kernel left in p1
+template <bool HALF>
 __global__ __launch_bounds__(256) void cb_bwd_sums4_kernel(const float* __restrict__ dout, const float* __restrict__ y,
                                                            const float* __restrict__ sc, const float* __restrict__ sh,
                                                            const float* __restrict__ ca, const float* __restrict__ sa,
                                                            const float* __restrict__ dsin,
                                                            const int* __restrict__ sarg, int HW, int C, int nchunk,
-                                                           Sum3* __restrict__ parts) {
+                                                           Sum3* __restrict__ parts, const Sum2* __restrict__ p1) {
     __shared__ float4 s_a[256], s_b[256], s_c[256];
     const int n = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
     const int C4 = C >> 2, lanes = 256 / C4;
     const int c4 = tid % C4, plane = tid / C4;
     const int p_per = (HW + nchunk - 1) / nchunk;
     const int p0 = chunk * p_per;
-    const int p1 = min(HW, p0 + p_per);
+    const int pend = min(HW, p0 + p_per);
     const int nc = n * C + 4 * c4;
     const float4 s = *reinterpret_cast<const float4*>(sc + nc);
     const float4 b = *reinterpret_cast<const float4*>(sh + nc);
     const float4 a = *reinterpret_cast<const float4*>(ca + nc);
     const float invC = 1.f / (float)C;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A, Cc = A;
-    for (int p = p0 + plane; p < p1; p += lanes) {
+    for (int p = p0 + plane; p < pend; p += lanes) {
         const long long pp = (long long)n * HW + p;
         const float4 yv = reinterpret_cast<const float4*>(y + pp * C)[c4];
-        const float4 dv = reinterpret_cast<const float4*>(dout + pp * C)[c4];
-        const float g = sa[pp];
         const float2 ds = reinterpret_cast<const float2*>(dsin)[pp];
         const int am = sarg[pp] - 4 * c4;
         const float d0 = ds.x * invC;
         float z, dzc, dz0;
+        if constexpr (HALF) {  // A: sum dzc z, B: sum dzc (times the attention after the fold)
+#define DCS_SUMS_LANE(X, K)                                   \
+        z = fmaf(yv.X, s.X, b.X);                             \
+        dzc = d0;                                             \
+        if (am == K) dzc += ds.y;                             \
+        A.X = fmaf(dzc, z, A.X);                              \
+        B.X += dzc;
+            DCS_SUMS_LANE(x, 0)
+            DCS_SUMS_LANE(y, 1)
+            DCS_SUMS_LANE(z, 2)
+            DCS_SUMS_LANE(w, 3)
+#undef DCS_SUMS_LANE
+        } else {
+            const float4 dv = reinterpret_cast<const float4*>(dout + pp * C)[c4];
+            const float g = sa[pp];
 #define DCS_SUMS_LANE(X, K)                                   \
         z = fmaf(yv.X, s.X, b.X);                             \
         dzc = fmaf(dv.X, g, d0);                              \
@@ -474,11 +560,12 @@ __global__ __launch_bounds__(256) void cb_bwd_sums4_kernel(const float* __restri
         A.X = fmaf(dzc, z, A.X);                              \
         B.X += dz0;                                           \
         Cc.X = fmaf(dz0, z, Cc.X);
-        DCS_SUMS_LANE(x, 0)
-        DCS_SUMS_LANE(y, 1)
-        DCS_SUMS_LANE(z, 2)
-        DCS_SUMS_LANE(w, 3)
+            DCS_SUMS_LANE(x, 0)
+            DCS_SUMS_LANE(y, 1)
+            DCS_SUMS_LANE(z, 2)
+            DCS_SUMS_LANE(w, 3)
 #undef DCS_SUMS_LANE
+        }
     }
     s_a[tid] = A; s_b[tid] = B; s_c[tid] = Cc;
     __syncthreads();
@@ -490,10 +577,19 @@ __global__ __launch_bounds__(256) void cb_bwd_sums4_kernel(const float* __restri
             Cc.x += w.x; Cc.y += w.y; Cc.z += w.z; Cc.w += w.w;
         }
         Sum3* o = parts + ((long long)n * nchunk + chunk) * C + 4 * c4;
-        o[0] = Sum3{A.x, B.x, Cc.x};
-        o[1] = Sum3{A.y, B.y, Cc.y};
-        o[2] = Sum3{A.z, B.z, Cc.z};
-        o[3] = Sum3{A.w, B.w, Cc.w};
+        if constexpr (HALF) {  // + the dout half; B = a sum dzc, Cc = a sum dzc z
+            const Sum2* q = p1 + ((long long)n * nchunk + chunk) * C + 4 * c4;
+            const float ax = A.x + q[0].a, ay = A.y + q[1].a, az = A.z + q[2].a, aw = A.w + q[3].a;
+            o[0] = Sum3{ax, a.x * (B.x + q[0].b), a.x * ax};
+            o[1] = Sum3{ay, a.y * (B.y + q[1].b), a.y * ay};
+            o[2] = Sum3{az, a.z * (B.z + q[2].b), a.z * az};
+            o[3] = Sum3{aw, a.w * (B.w + q[3].b), a.w * aw};
+        } else {
+            o[0] = Sum3{A.x, B.x, Cc.x};
+            o[1] = Sum3{A.y, B.y, Cc.y};
+            o[2] = Sum3{A.z, B.z, Cc.z};
+            o[3] = Sum3{A.w, B.w, Cc.w};
+        }
     }
 }
 
@@ -727,6 +823,7 @@ struct CbWs {
     float* dsin;
     float* wpart;
     Sum3* parts;
+    Sum2* p1;  // dout half of the b3 sums (cb_bwd_dsa_sums_kernel)
     Sum3* coef;
     float* dwpart;
     size_t total;
@@ -741,6 +838,7 @@ static CbWs cb_layout(void* base, int N, int H, int W, int C, int Cr, int ksa) {
     w.wpart = reinterpret_cast<float*>(b + off); off = align_up(off + (size_t)sa_wchunks(P) * 2 * ksa * ksa * sizeof(float), 256);
     int nch = cb_chunks(N, H * W);
     w.parts = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * nch * C * sizeof(Sum3), 256);
+    w.p1 = reinterpret_cast<Sum2*>(b + off); off = align_up(off + (size_t)N * nch * C * sizeof(Sum2), 256);
     w.coef = reinterpret_cast<Sum3*>(b + off); off = align_up(off + (size_t)N * C * sizeof(Sum3), 256);
     w.dwpart = reinterpret_cast<float*>(b + off); off = align_up(off + (size_t)N * 2 * C * Cr * sizeof(float), 256);
     w.total = off;
@@ -809,7 +907,12 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     // one wave per pixel: the 16-lane form (4 pixels per wave, 4 quads per wave) measured 104 vs
     // 96 us per 16-image launch here (a read-only pass wants more loads in flight per wave)
     constexpr int DPX = 4;  // pixels per wave of the C == 256 form
-    if (C == 256 && HW % DPX == 0)
+    const int nch = cb_chunks(N, HW);
+    const bool fused = C == 256;  // b1 with the dout half of b3 (cb_bwd_dsa_sums_kernel)
+    if (fused)
+        hipLaunchKernelGGL(cb_bwd_dsa_sums_kernel<DPX>, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, HW,
+                           nch, w.dpre, w.p1);
+    else if (C == 256 && HW % DPX == 0)
         hipLaunchKernelGGL(cb_bwd_dsa64x_kernel<DPX>, dim3((unsigned)cdiv(P, 4 * DPX)), dim3(256), 0, s, dout, y, scale,
                            shift, ca, sa, HW, P, w.dpre);
     else
@@ -826,11 +929,13 @@ extern "C" int dcs_cbam_backward(const float* dout, const float* y, const float*
     if ((e = check_launch("cb_bwd_dwsa_partial"))) return e;
     hipLaunchKernelGGL(cb_bwd_dwsa_final_kernel, dim3((unsigned)cdiv(nt, 128)), dim3(128), 0, s, w.wpart, nt, nwc, dwsa);
     if ((e = check_launch("cb_bwd_dwsa_final"))) return e;
-    const int nch = cb_chunks(N, HW);
     const bool v4 = (C % 4 == 0) && (C / 4 <= 256) && (256 % (C / 4) == 0);
-    if (v4)
-        hipLaunchKernelGGL(cb_bwd_sums4_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
-                           sarg, HW, C, nch, w.parts);
+    if (fused)
+        hipLaunchKernelGGL(cb_bwd_sums4_kernel<true>, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
+                           sarg, HW, C, nch, w.parts, w.p1);
+    else if (v4)
+        hipLaunchKernelGGL(cb_bwd_sums4_kernel<false>, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
+                           sarg, HW, C, nch, w.parts, nullptr);
     else
         hipLaunchKernelGGL(cb_bwd_sums_kernel, dim3(N, nch), dim3(256), 0, s, dout, y, scale, shift, ca, sa, w.dsin,
                            sarg, HW, C, nch, w.parts);
