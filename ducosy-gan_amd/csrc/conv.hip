@@ -3380,7 +3380,8 @@ extern "C" int dcs_reflect_fold(const float* dxpad, const float* addend, float* 
 extern "C" size_t dcs_conv_dgrad_reflect_ring_size(const dcs_conv_desc* dp) {
     if (!dp || dp->Ho < 6 || dp->Wo < 6) return 0;
     // the window path's ring pass writes one ring copy per K split
-    return (size_t)ring_ksplit(*dp) * dp->N * (2 * dp->Wo + 2 * (dp->Ho - 2)) * dp->Co * sizeof(float);
+    const int copies = ring_ksplit(*dp) > RG_COPIES ? ring_ksplit(*dp) : RG_COPIES;  // (conv_win.hip's ring16_kernel)
+    return (size_t)copies * dp->N * (2 * dp->Wo + 2 * (dp->Ho - 2)) * dp->Co * sizeof(float);
 }
 
 extern "C" int dcs_conv_dgrad_reflect(const dcs_conv_desc* dp, const float* dy, const float* wpack,

@@ -59,6 +59,10 @@ __device__ __forceinline__ int f16x3_exp(const float* __restrict__ rng, int n) {
     return __builtin_amdgcn_readfirstlane(sh);
 }
 
+// ring copies of the residual data gradient's padded-grid ring written by conv_win.hip's ring16_kernel
+// (one per tap; the ring buffer, dcs_conv_dgrad_reflect_ring_size, holds at least this many)
+constexpr int RG_COPIES = 3;
+
 __device__ __forceinline__ int xcd_remap(int L, int T) {
     // bijective: blocks L, L+8, ... share an XCD under round-robin dispatch
     const int xcd = L & 7, q = T >> 3, r = T & 7;

@@ -40,6 +40,13 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef DCS_WIN16  // f16x3 residual convs on the 16x16x32 window kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WIN16 1
 #endif
+#ifndef DCS_WW_STAGE  // where the 16x16x32 weight gradient stages the next rows (1: beside the second k-step's
+                      // MFMAs, -1.5 % per launch; 0: between its k-steps; 2-4: rejected placements)
+#define DCS_WW_STAGE 1
+#endif
+#ifndef DCS_RING16  // the padded-grid ring of the residual data gradient on ring16_kernel (0: the rows pass)
+#define DCS_RING16 1
+#endif
 #if CLK_PROBE  // probe build only: core-clock and wall-clock counters per weight-gradient workgroup
 __device__ unsigned long long g_clk[4096 * 4];
 #endif
@@ -1545,16 +1552,22 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
         *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls) = hi;
         *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls) = lo;
     };
+    auto st_xq = [&](int slot, int q) {
+        if (q == 0 || xls[q] >= 0) {  // (unit 0 covers pixels 0..63 of the 66: always inside)
+            f16x8 hi, lo;
+            split8h(xr[q][0], xr[q][1], bsc, hi, lo);
+            *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
+            *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
+        }
+    };
     auto st_x = [&](int slot) {
 #pragma unroll
-        for (int q = 0; q < WW_XU; ++q) {
-            if (xls[q] >= 0) {
-                f16x8 hi, lo;
-                split8h(xr[q][0], xr[q][1], bsc, hi, lo);
-                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
-                *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
-            }
-        }
+        for (int q = 0; q < WW_XU; ++q) st_xq(slot, q);
+    };
+    // staging piece p of the rows loaded for the next barrier (p 0: the dy row, 1 / 2: source units 0 / 1)
+    auto st_piece = [&](int p, int y) {
+        if (p == 0) st_dy((y + 1) & 1);
+        else st_xq((y + 2) & 3, p - 1);
     };
 
     // transposed-read lane offsets (halves) of k-step 0 and the first sub-block: A (dy) at pixel row
@@ -1640,6 +1653,19 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
             for (int jp = 0; jp < 10; ++jp) {
                 if (jp < 9) rd_b(jp + 1, (jp + 1) & 1);
                 __builtin_amdgcn_sched_barrier(0);
+                // DCS_WW_STAGE 1 / 2 / 4: the three staging pieces inside the second k-step's pair iterations 1,
+                // 3, 5 (their split VALU beside MFMAs instead of a block between the k-steps; 2: interleave
+                // requested by sched_group_barrier; 4: the next row's loads issued right after the last piece,
+                // in flight across the barrier); 3: iterations 3, 5, 7
+                const int p0 = DCS_WW_STAGE == 3 ? 3 : 1;
+                const bool piece_here = DCS_WW_STAGE != 0 && (jp == p0 || jp == p0 + 2 || jp == p0 + 4);
+                if (piece_here) {
+                    if (kk == 1) st_piece((jp - p0) >> 1, y);
+                }
+                if (DCS_WW_STAGE == 4 && kk == 1 && jp == 5 && y + 1 < y_end) {  // (block-uniform)
+                    ld_dy(y + 2 < y_end ? y + 2 : y + 1);
+                    ld_x(y + 3 <= H ? y + 3 : H);
+                }
                 const int tt = jp >> 1, ns = jp & 1;
                 const int tap = R == 0 ? tt : (tt < 4 ? 5 + tt : 4);
                 const int sl = jp & 1;
@@ -1651,8 +1677,18 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
                     t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bl[sl], t[idx], 0, 0, 0);
                     t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bh[sl], t[idx], 0, 0, 0);
                 }
+                if (piece_here && DCS_WW_STAGE == 2) {
+                    if (kk == 1) {
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // then up to six VALU
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);      // the two LDS stores
+                    }
+                }
             }
-            if (kk == 0) {  // stage the rows loaded for the next barrier (buffers no row of this one reads)
+            if (DCS_WW_STAGE == 0 && kk == 0) {  // stage the rows loaded for the next barrier (buffers no row of this one reads)
                 __builtin_amdgcn_sched_barrier(0);
                 st_dy((y + 1) & 1);
                 st_x((y + 2) & 3);
@@ -1662,8 +1698,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
 
 #pragma unroll 1
     for (int y = y_beg; y < y_end; ++y) {
-        ld_dy(y + 1 < y_end ? y + 1 : y);
-        ld_x(y + 2 <= H ? y + 2 : H);
+        if (DCS_WW_STAGE != 4 || y == y_beg) {  // (DCS_WW_STAGE 4: issued by the previous row)
+            ld_dy(y + 1 < y_end ? y + 1 : y);
+            ld_x(y + 2 <= H ? y + 2 : H);
+        }
         if (half == 0) row(y, std::integral_constant<int, 0>{});
         else row(y, std::integral_constant<int, 1>{});
         if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {  // chains of two rows (128 pixels)
@@ -1693,6 +1731,223 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
             slab[(long long)rowc * 9 * C + tap * C + col] = __builtin_ldexpf(acc[i][r], eab);
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// The one-pixel ring of the residual data gradient's padded grid (dcs_conv_dgrad_reflect_win).  Over the
+// (H + 2) x (W + 2) grid dx_pad[q] = sum_t B_t^T dy[q + (ty - 2, tx - 2)] (B: the window kernel's flipped
+// pack, dcs_pack_weights_h3), and a ring position is reached by the three taps of one kernel row (top
+// ring row: ty = 2, bottom: ty = 0) or column (left: tx = 2, right: tx = 0) only.  One GEMM per ring
+// segment and tap, so B is uniform over a workgroup: M = the segment's positions over the batch (the
+// top rows of all images, ...), N = the output channels, K = C; the three taps' products go to three ring
+// copies (RG_COPIES), summed by the fold in tap order, so each position's sum has one fixed order
+// whatever the batch.  A workgroup owns 64 positions x 256 channels: four waves of 64 x 64 (4 x 4 blocks
+// of v_mfma_f32_16x16x32_f16).  A (the gathered dy pixels, fp32) arrives by LDS-DMA (the eight 16-byte
+// chunks of a row rotated by bits 1-3 of the row: conflict-free fragment reads) and is split into hi / lo
+// fp16 at the fragment read, where pixels outside the image are masked to zero (their DMA reads pixel 0).
+// B fragments come straight from the packed planes (L2) into registers.  RG_D = 2 of the 8 k-steps
+// (C = 256) are in flight, in RG_D + 1 LDS buffers and register sets (140 VGPRs: three waves per SIMD).  The B loads are inline asm like the DMA, so the compiler inserts no wait of its
+// own for them (it cannot count the DMAs, and its waits for the registers would drain later k-steps'
+// loads); the one wait per k-step (vmcnt: all but the loads of the k-steps after the next) covers both.
+// The tap split triples the workgroups (more waves per SIMD to overlap the fetch latency of these short
+// K loops).  The generic rows pass this replaces ran the ring as 128-row tiles with K split
+// over up to eight ring copies.
+constexpr int RG_NT = 256, RG_BM = 64;
+constexpr int RG_D = 2;  // k-steps in flight (RG_D + 1 register sets and LDS buffers; 4 measured slower: 202 VGPRs)
+
+template <int... I, class F>
+__device__ __forceinline__ void rg_unroll(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+struct RingArgs {
+    int N, H, W, C, Co;
+    int tiles_tb, tiles_lr;  // 64-position tiles of the top / bottom segments and of the left / right ones
+    int rng_n;
+};
+
+// 16 bytes per lane through the buffer descriptor, untracked by the compiler (see ring16_kernel)
+__device__ __forceinline__ f16x8 rg_bload(__amdgpu_buffer_rsrc_t r, int off) {
+    f16x8 v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+    return v;
+}
+
+template <int NP, int NK>  // NK: k-steps (C / 32)
+__global__ __launch_bounds__(RG_NT) void ring16_kernel(RingArgs a, const float* __restrict__ dy,
+                                                      const _Float16* __restrict__ wh,
+                                                      const _Float16* __restrict__ wl,
+                                                      const float* __restrict__ rng,
+                                                      const int* __restrict__ wexp, float* __restrict__ ring) {
+    __shared__ __attribute__((aligned(16))) float Ar[(RG_D + 1) * RG_BM * 32];  // [buffer][row][32 floats]
+    const int gco = a.Co >> 8;
+    const int L = blockIdx.x;
+    const int ct = L % gco, jt = (L / gco) % 3, mt = L / (3 * gco);
+    const int n0 = ct * 256;
+    int seg, tm;
+    if (mt < 2 * a.tiles_tb) {
+        seg = mt >= a.tiles_tb;
+        tm = mt - seg * a.tiles_tb;
+    } else {
+        const int r = mt - 2 * a.tiles_tb;
+        seg = 2 + (r >= a.tiles_lr);
+        tm = r - (seg - 2) * a.tiles_lr;
+    }
+    const int H = a.H, W = a.W, C = a.C, Wp = W + 2, K = 9 * C;
+    const int seglen = seg < 2 ? Wp : H;  // positions per image
+    const int segM = a.N * seglen, m0 = tm * RG_BM;
+    const int ringlen = 2 * Wp + 2 * H;
+    // the workgroup's tap (t0 + jt tstep); dy pixel of a position at tap jt: (py0 + jt sy, px0 + jt sx)
+    const int t0 = seg == 0 ? 6 : (seg == 2 ? 2 : 0), tstep = seg < 2 ? 1 : 3;
+    const int sy = seg < 2 ? 0 : jt, sx = seg < 2 ? jt : 0;
+    auto locate = [&](int m, int& n, int& py, int& px, int& ri) {
+        n = m / seglen;
+        const int p = m - n * seglen;
+        if (seg == 0) { py = 0; px = p - 2; ri = p; }
+        else if (seg == 1) { py = H - 1; px = p - 2; ri = Wp + p; }
+        else if (seg == 2) { py = p - 1; px = 0; ri = 2 * Wp + 2 * p; }  // padded row p + 1
+        else { py = p - 1; px = W - 1; ri = 2 * Wp + 2 * p + 1; }
+        py += sy;
+        px += sx;
+    };
+    auto inimg = [&](int py, int px) { return py >= 0 && py < H && px >= 0 && px < W; };
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int m16 = lane & 15, g = lane >> 4;
+
+    // A by LDS-DMA: wave w's instructions i = 0, 1 move chunks u = (2 w + i) * 64 + lane: row u >> 3,
+    // LDS slot u & 7 holding channel chunk (u & 7) ^ ((row >> 1) & 7) of the k-step's 32 channels
+    unsigned doff[2], dlds[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int u = (2 * wid + i) * 64 + lane, row = u >> 3, chunk = (u & 7) ^ ((row >> 1) & 7);
+        int n = 0, py = 0, px = 0, ri = 0;
+        if (m0 + row < segM) locate(m0 + row, n, py, px, ri);
+        const bool ok = m0 + row < segM && inimg(py, px);
+        doff[i] = (unsigned)((ok ? ((n * H + py) * W + px) * C * 4 : 0) + chunk * 16);
+        dlds[i] = (unsigned)__builtin_amdgcn_readfirstlane((2 * wid + i) * 64 * 16);
+    }
+    const unsigned ar_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)Ar;
+    auto a_dma = [&](int ks, int buf) {
+        const unsigned base = ar_lds + (unsigned)(buf * RG_BM * 32 * 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) win_glds(dy, doff[i] + (unsigned)(ks * 128), base + dlds[i]);
+    };
+    // fragment rows 16 i + m16 inside the image at this tap (bit i)
+    int vmask = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 16 * i + m16;
+        if (m < segM) {
+            int n, py, px, ri;
+            locate(m, n, py, px, ri);
+            if (inimg(py, px)) vmask |= 1 << i;
+        }
+    }
+    // B: lane (m16, g) of column block jb reads column n0 + 64 wid + 16 jb + m16, the k-step's channels
+    // 8 g .. 8 g + 7 (slice 2 ks + (g >> 1), half g & 1) of the workgroup's tap
+    const __amdgpu_buffer_rsrc_t bhr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(wh), (short)0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t blr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(NP == 3 ? wl : wh), (short)0, 0x7fffff00, 0x00020000);
+    const int blane = ((n0 + 64 * wid + m16) * K + (g >> 1) * 144 + 8 * (g & 1) + (t0 + jt * tstep) * 16) * 2;
+    f16x8 bq[RG_D + 1][4][2];
+    auto b_load = [&](int ks, auto setc) {
+        constexpr int S = decltype(setc)::value;
+        const int kb = blane + ks * 2 * 144 * 2;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+            bq[S][jb][0] = rg_bload(bhr, kb + jb * 16 * K * 2);
+            if constexpr (NP == 3) bq[S][jb][1] = rg_bload(blr, kb + jb * 16 * K * 2);
+        }
+    };
+
+    f32x4v acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) acc[i][jb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    // vmcnt(n) with the other counters left alone
+    auto wait_vm = [](auto nc) {
+        constexpr int n = decltype(nc)::value;
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 15) | ((n >> 4) << 14));
+    };
+    constexpr int PER = NP == 3 ? 10 : 6;  // loads per k-step and lane: 2 DMA + 4 or 8 B
+
+    // prologue: the exponents first (their loads are the compiler's to wait for), then k-steps
+    // 0 .. RG_D - 1 in flight, k-step 0 waited for
+    const int ea = f16x3_exp(rng, a.rng_n);
+    const int eb = __builtin_amdgcn_readfirstlane(wexp[0]);
+    const float asc = __builtin_ldexpf(1.f, ea);
+    __builtin_amdgcn_sched_barrier(0);
+    rg_unroll(std::make_integer_sequence<int, (RG_D < NK ? RG_D : NK)>{}, [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        a_dma(k, k);
+        b_load(k, std::integral_constant<int, k>{});
+    });
+    wait_vm(std::integral_constant<int, ((RG_D < NK ? RG_D : NK) - 1) * PER>{});
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+
+    // per lane: A rows 16 i + m16, floats 8 g .. 8 g + 7 = chunks 2 g, 2 g + 1
+    int aoff[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + m16, f = (row >> 1) & 7;
+        aoff[i][0] = row * 32 + 4 * ((2 * g) ^ f);
+        aoff[i][1] = row * 32 + 4 * ((2 * g + 1) ^ f);
+    }
+    auto step = [&](auto ksc) {
+        constexpr int ks = decltype(ksc)::value, S = ks % (RG_D + 1);
+        // no load past the end (its dead destination registers the compiler would hand to other values)
+        if constexpr (ks + RG_D < NK) {
+            a_dma(ks + RG_D, (ks + RG_D) % (RG_D + 1));
+            b_load(ks + RG_D, std::integral_constant<int, (ks + RG_D) % (RG_D + 1)>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float* const Ab = Ar + S * RG_BM * 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 r0 = *reinterpret_cast<const float4*>(Ab + aoff[i][0]);
+            const float4 r1 = *reinterpret_cast<const float4*>(Ab + aoff[i][1]);
+            const float sc = (vmask >> i) & 1 ? asc : 0.f;  // pixels outside the image: zero
+            f16x8 ah, al;
+            split8h(r0, r1, sc, ah, al);
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) {
+                if constexpr (NP == 3) {
+                    acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bq[S][jb][0], acc[i][jb], 0, 0, 0);
+                    acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bq[S][jb][1], acc[i][jb], 0, 0, 0);
+                }
+                acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bq[S][jb][0], acc[i][jb], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // k-step ks + 1 has landed once only the loads of the k-steps after it are in flight
+        constexpr int last = ks + RG_D < NK - 1 ? ks + RG_D : NK - 1;
+        wait_vm(std::integral_constant<int, (last > ks + 1 ? last - ks - 1 : 0) * PER>{});
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // fully unrolled (NK = C / 32 k-steps): the registers the asm loads fill must not meet a control-flow
+    // merge, where the compiler could copy them before the data lands
+    rg_unroll(std::make_integer_sequence<int, NK>{}, step);
+
+    // epilogue: undo the scales into ring copy jt; lane (m16, g) holds rows 16 i + 4 g + r, column
+    // 16 jb + m16
+    const int eab = -(ea + eb);
+    float* const rc = ring + (long long)jt * a.N * ringlen * a.Co;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 16 * i + 4 * g + r;
+            if (m >= segM) continue;
+            int n, py, px, ri;
+            locate(m, n, py, px, ri);
+            float* const o = rc + ((long long)n * ringlen + ri) * a.Co + n0 + 64 * wid + m16;
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) o[16 * jb] = __builtin_ldexpf(acc[i][jb][r], eab);
+        }
 }
 
 struct WWPlan {
@@ -1800,6 +2055,27 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
     return check_launch("conv3_win");
 }
 
+// the padded-grid ring on ring16_kernel (d: the data gradient's descriptor, win_check'ed): RG_COPIES ring
+// copies (one per tap)
+bool ring16_ok(const dcs_conv_desc& d) {
+    return DCS_RING16 && d.Cs == 256 && d.Co % 256 == 0 && d.Hs >= 2 && d.Ws >= 2;
+}
+int launch_ring16(const dcs_conv_desc& d, const float* dy, const void* wh, const void* wl, const int* wexp, float* ring,
+                  hipStream_t s) {
+    RingArgs a;
+    a.N = d.N; a.H = d.Hs; a.W = d.Ws; a.C = d.Cs; a.Co = d.Co; a.rng_n = d.rng_a_n;
+    a.tiles_tb = (int)cdiv((long long)d.N * (d.Ws + 2), RG_BM);
+    a.tiles_lr = (int)cdiv((long long)d.N * d.Hs, RG_BM);
+    const unsigned blocks = (unsigned)((2 * a.tiles_tb + 2 * a.tiles_lr) * 3 * (d.Co / 256));
+    const _Float16* h = reinterpret_cast<const _Float16*>(wh);
+    const _Float16* l = reinterpret_cast<const _Float16*>(wl);
+    if (d.mma == DCS_MMA_F16)
+        hipLaunchKernelGGL((ring16_kernel<1, 8>), dim3(blocks), dim3(RG_NT), 0, s, a, dy, h, l, d.rng_a, wexp, ring);
+    else
+        hipLaunchKernelGGL((ring16_kernel<3, 8>), dim3(blocks), dim3(RG_NT), 0, s, a, dy, h, l, d.rng_a, wexp, ring);
+    return check_launch("ring16");
+}
+
 }  // namespace
 
 // conv.hip: the generic rows pass (ring rows of the padded data gradient) and the ring fold
@@ -1881,7 +2157,11 @@ extern "C" int dcs_conv_dgrad_reflect_win(const dcs_conv_desc* dp, const float* 
     // interior: a 'same' zero-pad conv of dy over the flipped weights, straight into dx (+ addend)
     int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, addend, dx, nullptr, s);
     if (e) return e;
-    // the padded grid's one-pixel ring by the generic rows pass, then folded onto the border
+    // the padded grid's one-pixel ring (ring16_kernel, else the generic rows pass), folded onto the border
+    if (ring16_ok(d)) {
+        if ((e = launch_ring16(d, dy, w_hi, w_lo, wexp, ring, s))) return e;
+        return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, RG_COPIES, s);
+    }
     if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
     return reflect_ring_fold(ring, dx, d.N, d.Ho - 2, d.Wo - 2, d.Co, ring_ksplit(d), s);
 }
@@ -1913,8 +2193,11 @@ extern "C" int dcs_conv_dgrad_reflect_win_inbwd(const dcs_conv_desc* dp, const f
     const IbwArgs ib{y, scale, shift, reinterpret_cast<Sum2*>(parts), act, nch};
     int e = launch_win(d, d.Hs, d.Ws, 0, dy, w_hi, w_lo, wexp, nullptr, dx, nullptr, s, &ib);
     if (e) return e;
-    if ((e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2))) return e;
+    const bool r16 = ring16_ok(d);
+    if (r16) e = launch_ring16(d, dy, w_hi, w_lo, wexp, ring, s);
+    else e = conv_rows_impl(&d, dy, nullptr, wpack, nullptr, nullptr, nullptr, ring, nullptr, nullptr, stream, 2);
+    if (e) return e;
     *nchunk = nch;
-    return reflect_ring_fold_ibw(ring, dx, d.N, d.Hs, d.Ws, d.Co, ring_ksplit(d), y, scale, shift, act,
+    return reflect_ring_fold_ibw(ring, dx, d.N, d.Hs, d.Ws, d.Co, r16 ? RG_COPIES : ring_ksplit(d), y, scale, shift, act,
                                  reinterpret_cast<Sum2*>(parts), nch, tiles, IBW_FOLD_CHUNKS, s);
 }

@@ -205,8 +205,8 @@ def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
 def test_win_batch_vs_per_image_bit_identical(ops, mode):
     """A full-size batch (N = 3 at 128 x 128 x 256: 384 jobs, more than the GPU has CUs) against the same
     convs one image at a time: bit-identical outputs and IN statistics (forward), data gradients with
-    the residual addend bit-identical inside the two-pixel border (the border's reflection-ring pass
-    splits K by the batch size, so there the sums differ in order: 1e-6 of the largest value), and the
+    the residual addend bit-identical, the reflection ring included (ring16_kernel sums each ring position
+    in one fixed order whatever the batch; the rows pass it replaced split K by the batch size), and the
     data gradient with the InstanceNorm-backward partial sums in its epilogue (the training step's form)
     equal to the one without them."""
     ops.set_mma(mode)
@@ -226,8 +226,7 @@ def test_win_batch_vs_per_image_bit_identical(ops, mode):
         for a, b in ((st.scale, sti.scale), (st.shift, sti.shift), (st.xmax, sti.xmax), (st.xargmax, sti.xargmax)):
             assert torch.equal(a[i:i + 1], b), (mode, i)
         dxi = g.dgrad(Rd[i:i + 1].contiguous(), wd, H, W, addend=Ad[i:i + 1].contiguous())
-        assert torch.equal(dx[i:i + 1, 2:H - 2, 2:W - 2], dxi[:, 2:H - 2, 2:W - 2]), (mode, i)
-        assert float((dx[i:i + 1] - dxi).abs().max()) <= 1e-6 * float(dxi.abs().max()), (mode, i)
+        assert torch.equal(dx[i:i + 1], dxi), (mode, i)
     # the data gradient with the InstanceNorm-backward partial sums in its epilogue (the training step's
     # form; zero padding, whose window halo must survive the epilogue's LDS use): the same da as
     # without them, and the IN backward from the fused sums within 1e-5 of the separate pass
