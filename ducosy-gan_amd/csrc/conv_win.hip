@@ -2086,7 +2086,7 @@ int reflect_ring_fold_ibw(const float* ring, float* dx, int N, int H, int W, int
                           const float* sc, const float* sh, int act, Sum2* parts, int nchunk, int chunk0, int nfc,
                           hipStream_t s);
 int ring_ksplit(const dcs_conv_desc& d);
-constexpr int IBW_FOLD_CHUNKS = 16;  // partial-sum chunks of the ring fold per image
+constexpr int IBW_FOLD_CHUNKS = 64;  // partial-sum chunks of the ring fold per image (its blocks: 64 per image)
 
 }  // namespace dcs
 

@@ -66,8 +66,11 @@ def test_win_forward_and_stats_vs_fp64(ops, N, H, W):
 
 
 @pytest.mark.parametrize("addend", [False, True])
-@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128)])
+@pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128), (5, 32, 32), (3, 16, 64), (2, 8, 128)])
 def test_win_dgrad_reflect_vs_fp64(ops, N, H, W, addend):
+    """The reflect-pad data gradient: interior by the window kernel, the padded grid's ring by
+    ring16_kernel (ring segments over the batch in 64-position tiles: the sizes here leave partial
+    tiles and tiles that straddle images), folded onto the border; against float64 at 1e-5."""
     ops.set_mma("f16x3")
     g = _geom(ops)
     x = rnd((N, 256, H, W), 61, "x").double().requires_grad_(True)
@@ -186,7 +189,7 @@ def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
     R = torch.from_numpy(prng.normal(113, "R", (N, 256, H, W))).float().to(DEV).permute(0, 2, 3, 1).contiguous()
     wd = g.pack_dgrad(w)
     da_f, parts, nch = g.dgrad(R, wd, H, W, inbwd=(y, st, ACT_RELU))
-    assert parts is not None and nch == H * W // 256 + 16
+    assert parts is not None and nch == H * W // 256 + 64
     dy_f = ops.in_act_backward_parts(da_f, y, st, ACT_RELU, parts, nch)
     da_s = g.dgrad(R, wd, H, W)
     assert torch.equal(da_f, da_s)
