@@ -213,9 +213,11 @@ int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const flo
  * for none; *nchunk = H * W / 256).
  * dcs_conv_dgrad_reflect_win: the data gradient of a ReflectionPad2d(1) + 3x3 conv
  * (dcs_conv_dgrad_reflect's contract, plus the pre-split flipped weights): the interior by the
- * window pass (+ addend), the padded grid's ring by the rows pass over wpack (fp32 kind 1 |
- * DCS_PACK_KSLICE with its range record) into ring (dcs_conv_dgrad_reflect_ring_size bytes, any
- * allocation), folded onto dx's border. */
+ * window pass (+ addend), the padded grid's one-pixel ring into ring (dcs_conv_dgrad_reflect_ring_size
+ * bytes, any allocation) and folded onto dx's border.  The ring: with Cs == 256 and Co % 256 == 0 one GEMM
+ * per ring segment and tap over the pre-split weights (csrc/conv_win.hip ring16_kernel: three ring
+ * copies summed in tap order, independent of the batch), otherwise the rows pass over wpack (fp32
+ * kind 1 | DCS_PACK_KSLICE with its range record). */
 size_t dcs_pack_weights_h3_scratch_size(void);
 int dcs_pack_weights_h3(const float* w, int Cout, int Cin, int flip, int ncols, void* out_hi, void* out_lo,
                         float* scratch, int* wexp, void* stream);
