@@ -2388,9 +2388,14 @@ __global__ __launch_bounds__(256) void pack_batch2_kernel(const dcs_pack_job* __
                 if (col < jb.Cin) v = jb.w[(((long long)c * jb.Cin + col) * 3 + (2 - ty)) * 3 + (2 - tx)];
             }
             const float f = v * sc;
-            const _Float16 h = (_Float16)f;
+            const _Float16 h = (_Float16)f, l = (_Float16)(f - (float)h);
             oh[idx] = h;
-            ol[idx] = (_Float16)(f - (float)h);
+            ol[idx] = l;
+            if (jb.h3_flip) {  // the tap-major copy behind the planes (as conv_win.hip's pack_h3_kernel)
+                const long long t = total + (long long)col * K + tap * C + c;
+                oh[t] = h;
+                ol[t] = l;
+            }
         }
     } else {
         const float sc = __builtin_ldexpf(1.f, f16x3_exp(jb.rng, DCS_RANGE_PARTS));

@@ -1094,9 +1094,14 @@ __global__ __launch_bounds__(256) void pack_h3_kernel(const float* __restrict__ 
             if (col < Cin) v = w[(((long long)c * Cin + col) * 3 + (2 - ty)) * 3 + (2 - tx)];
         }
         const float f = v * sc;
-        const _Float16 h = (_Float16)f;
+        const _Float16 h = (_Float16)f, l = (_Float16)(f - (float)h);
         oh[idx] = h;
-        ol[idx] = (_Float16)(f - (float)h);
+        ol[idx] = l;
+        if (flip) {  // the tap-major copy behind the planes (k = tap * C + c: the ring kernel's B)
+            const long long t = total + (long long)col * K + tap * C + c;
+            oh[t] = h;
+            ol[t] = l;
+        }
     }
 }
 
@@ -1745,7 +1750,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
 // of v_mfma_f32_16x16x32_f16).  A (the gathered dy pixels, fp32) arrives by LDS-DMA (the eight 16-byte
 // chunks of a row rotated by bits 1-3 of the row: conflict-free fragment reads) and is split into hi / lo
 // fp16 at the fragment read, where pixels outside the image are masked to zero (their DMA reads pixel 0).
-// B fragments come straight from the packed planes (L2) into registers.  RG_D = 2 of the 8 k-steps
+// B fragments come straight from the pack's tap-major copy (L2) into registers.  RG_D = 2 of the 8 k-steps
 // (C = 256) are in flight, in RG_D + 1 LDS buffers and register sets (140 VGPRs: three waves per SIMD).  The B loads are inline asm like the DMA, so the compiler inserts no wait of its
 // own for them (it cannot count the DMAs, and its waits for the registers would drain later k-steps'
 // loads); the one wait per k-step (vmcnt: all but the loads of the k-steps after the next) covers both.
@@ -1845,14 +1850,15 @@ __global__ __launch_bounds__(RG_NT) void ring16_kernel(RingArgs a, const float* 
         }
     }
     // B: lane (m16, g) of column block jb reads column n0 + 64 wid + 16 jb + m16, the k-step's channels
-    // 8 g .. 8 g + 7 (slice 2 ks + (g >> 1), half g & 1) of the workgroup's tap
+    // 8 g .. 8 g + 7 of the workgroup's tap, from the pack's tap-major copy (behind its Co x 9C planes:
+    // the four lanes of a column read 64 contiguous bytes; the slice-major planes interleave the taps)
     const __amdgpu_buffer_rsrc_t bhr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(wh), (short)0, 0x7fffff00, 0x00020000);
     const __amdgpu_buffer_rsrc_t blr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(NP == 3 ? wl : wh), (short)0, 0x7fffff00, 0x00020000);
-    const int blane = ((n0 + 64 * wid + m16) * K + (g >> 1) * 144 + 8 * (g & 1) + (t0 + jt * tstep) * 16) * 2;
+    const int blane = (a.Co * K + (n0 + 64 * wid + m16) * K + (t0 + jt * tstep) * C + 8 * g) * 2;
     f16x8 bq[RG_D + 1][4][2];
     auto b_load = [&](int ks, auto setc) {
         constexpr int S = decltype(setc)::value;
-        const int kb = blane + ks * 2 * 144 * 2;
+        const int kb = blane + ks * 32 * 2;
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
             bq[S][jb][0] = rg_bload(bhr, kb + jb * 16 * K * 2);

@@ -476,8 +476,9 @@ class ConvGeom:
     def _attach_h3(self, wpack: torch.Tensor, w: torch.Tensor, flip: int) -> torch.Tensor:
         ncols = self.cin if flip else self.cout
         K = 9 * (self.cout if flip else self.cin)
-        hi = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
-        lo = torch.empty(ncols, K, device=w.device, dtype=torch.float16)
+        # data-gradient packs carry a tap-major copy behind the planes (the ring kernel's B)
+        hi = torch.empty((2 if flip else 1) * ncols, K, device=w.device, dtype=torch.float16)
+        lo = torch.empty((2 if flip else 1) * ncols, K, device=w.device, dtype=torch.float16)
         wexp = torch.empty(1, device=w.device, dtype=torch.int32)
         if _BATCH is not None:  # prepack: one batched launch pair for every pack of the step
             scratch = torch.empty(lib.RANGE_PARTS, device=w.device, dtype=torch.float32)

@@ -203,8 +203,9 @@ int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const flo
  * dcs_pack_weights_h3: pre-split weights of a 3x3 conv, hi / lo fp16 planes [ncols][9 * C] in the
  * slice-major K order (k = (c / 16) * 144 + tap * 16 + c % 16), C = Cin for the forward (flip = 0) or
  * Cout for the data gradient over flipped taps (flip = 1); the values are scaled by 2^wexp[0]
- * (max |w| * 2^wexp < 2^15), written to *wexp on the device.  scratch: DCS_RANGE_PARTS floats
- * (dcs_pack_weights_h3_scratch_size bytes).
+ * (max |w| * 2^wexp < 2^15), written to *wexp on the device.  With flip = 1 out_hi / out_lo hold
+ * 2 * ncols * 9 * Cout halves: the planes, then a tap-major copy (k = tap * Cout + c) that the data
+ * gradient's ring reads.  scratch: DCS_RANGE_PARTS floats (dcs_pack_weights_h3_scratch_size bytes).
  * dcs_conv3_win_ok(d, dgrad): 1 if d is a geometry these passes cover: dgrad = 0, the forward of a
  * 3x3 stride-1 pad-1 conv (d as for dcs_conv_rows_in_stats); dgrad = 1, the padded-grid data gradient
  * (d as for dcs_conv_dgrad_reflect); both with mma = DCS_MMA_F16X3 and rng_a set, contiguous NHWC,
@@ -214,8 +215,9 @@ int dcs_range_parts(const float* x, int n_img, int64_t per_img, int C, const flo
  * dcs_conv_dgrad_reflect_win: the data gradient of a ReflectionPad2d(1) + 3x3 conv
  * (dcs_conv_dgrad_reflect's contract, plus the pre-split flipped weights): the interior by the
  * window pass (+ addend), the padded grid's one-pixel ring into ring (dcs_conv_dgrad_reflect_ring_size
- * bytes, any allocation) and folded onto dx's border.  The ring: with Cs == 256 and Co % 256 == 0 one GEMM
- * per ring segment and tap over the pre-split weights (csrc/conv_win.hip ring16_kernel: three ring
+ * bytes, any allocation) and folded onto dx's border; w_hi / w_lo: a flip = 1 pack with ncols == d->Co.
+ * The ring: with Cs == 256 and Co % 256 == 0 one GEMM per ring segment and tap over the pack's tap-major
+ * copy (csrc/conv_win.hip ring16_kernel: three ring
  * copies summed in tap order, independent of the batch), otherwise the rows pass over wpack (fp32
  * kind 1 | DCS_PACK_KSLICE with its range record). */
 size_t dcs_pack_weights_h3_scratch_size(void);
