@@ -50,6 +50,11 @@ _KSLICE = True
 _FUSE_FOLD = True
 # f16x3 residual convs on the window kernel (csrc/conv_win.hip); False = the rows pass
 _WIN = True
+# window phase-kernel layers kept on f16x3 operands in the fp16 mode (ConvGeom._phase_tag).  Empty since
+# round 6: every up-conv and PatchGAN layer on fp16 operands holds the config-5 bars (the steps_64 fixture
+# pair at 0.60 of its bar, the 512 x 512 pair within 1.4e-4 / 3.7e-3 of f16x3; scripts/diag/f16_layers.py,
+# profiles/r06/ab/r06ab_*), f16 step 138.7 -> 133.5 ms same box
+_PHASE_F16X3 = frozenset()
 
 
 def _h3() -> bool:
@@ -708,12 +713,19 @@ class ConvGeom:
                  _p(xam), _stream())
         return out, INStats(scale, shift, xmax, xam)
 
+    def _phase_tag(self) -> Optional[str]:
+        """The layer's key in _PHASE_F16X3: "up1" / "up2" (the up-convs 256->128, 128->64), "pg64" /
+        "pg128" / "pg256" (the PatchGAN 4x4 layers by input channels); None for the down-convs."""
+        if self.subpixel:
+            return "up1" if self.cin >= 256 else "up2"
+        return f"pg{self.cin}" if self.k == 4 else None
+
     def _phase_mma(self, d) -> None:
-        """Operand mode of the window phase kernels' forward and data gradient: the up-convs and the
-        PatchGAN layers on f16x3 in both fp16 modes, as the stem and head (with fp16 operands the
-        config-5 fixture's f16 step misses its bar: the edge term for the up-convs, the lung
-        Discriminator loss for the PatchGAN layers, profiles/r04ah); the down-convs in the step's mode."""
-        if self.subpixel or self.k == 4:
+        """Operand mode of the window phase kernels' forward and data gradient: the step's mode, except
+        the layers in _PHASE_F16X3, which take f16x3 in both fp16 modes as the stem and head do (in
+        round 4 the up-convs and PatchGAN layers on fp16 missed the config-5 fixture's bar,
+        profiles/r04ah; since round 6 they hold it)."""
+        if self._phase_tag() in _PHASE_F16X3:
             d.mma = lib.MMA_F16X3
 
     def _phase_win_ok(self, d) -> bool:
