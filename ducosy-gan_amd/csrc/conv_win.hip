@@ -44,6 +44,11 @@ __device__ unsigned long long g_win_t[16384 * 5];
                       // MFMAs, -1.5 % per launch; 0: between its k-steps; 2-4: rejected placements)
 #define DCS_WW_STAGE 1
 #endif
+#ifndef DCS_WIN16_F16  // the f16 mode's residual convs on the 16x16x32 window kernel too (NP 1, one barrier per
+                       // 16-MFMA k-step; 0: conv3_win_h3_kernel<1>, one barrier per 36-MFMA slice).  Measured
+                       // -2..3 % per launch in kbench, neutral in the step (133.4 vs 133.6 ms): not the default
+#define DCS_WIN16_F16 0
+#endif
 #ifndef DCS_RING16  // the padded-grid ring of the residual data gradient on ring16_kernel (0: the rows pass)
 #define DCS_RING16 1
 #endif
@@ -759,7 +764,7 @@ __device__ __forceinline__ void win16_ibw(const f32x4v (&acc)[4][4], const float
     }
 }
 
-template <bool IBW, bool WIDE>  // WIDE: W >= 64
+template <int NP, bool IBW, bool WIDE>  // NP: products (3: f16x3, 1: f16, hi planes only); WIDE: W >= 64
 __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const float* __restrict__ src,
                                                                 const _Float16* __restrict__ wh,
                                                                 const _Float16* __restrict__ wl,
@@ -840,10 +845,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
         f16x8 hi, lo;
         split8h(wq_[0], wq_[1], asc, hi, lo);
         *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 0, wp, h) : Wspare) = hi;
-        *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 1, wp, h) : Wspare) = lo;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 1, wp, h) : Wspare) = lo;
         if (wd >= 0) {
             *reinterpret_cast<f16x8*>(Wn + w16_off(buf, 0, wd, h)) = hi;
-            *reinterpret_cast<f16x8*>(Wn + w16_off(buf, 1, wd, h)) = lo;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + w16_off(buf, 1, wd, h)) = lo;
         }
     };
 
@@ -856,8 +861,9 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     {
         const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int b = __builtin_amdgcn_readfirstlane(wid) * 2 + i, pl = b >> 3, rb = b & 7;
+        for (int i = 0; i < 2; ++i) {  // (NP 1: the hi plane's 8 blocks, block w of wave w)
+            const int b = NP == 3 ? __builtin_amdgcn_readfirstlane(wid) * 2 + i : __builtin_amdgcn_readfirstlane(wid);
+            const int pl = b >> 3, rb = b & 7;
             dsu[i] = 2u * (unsigned)(rb * 16 * K);
             dbase[i] = pl ? wl : wh;
             ddst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)(pl * W16_BSLOT + rb * 16 * 32));
@@ -866,7 +872,8 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     auto b_dma = [&](int j, int buf) {  // k-step j (packed k 32 j .. 32 j + 31) into B buffer buf
         const unsigned kb = 2u * (unsigned)(j * 32);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) win_glds(dbase[i], dlane + (dsu[i] + kb), ddst[i] + 2u * (unsigned)(buf * 2 * W16_BSLOT));
+        for (int i = 0; i < (NP == 3 ? 2 : 1); ++i)
+            win_glds(dbase[i], dlane + (dsu[i] + kb), ddst[i] + 2u * (unsigned)(buf * 2 * W16_BSLOT));
     };
 
     // fragment offsets (halves).  A: window pixel of row block i at tap (0, 0) = ublk[i] + m16 (wave-
@@ -933,12 +940,12 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     };
     auto rd_a = [&](const _Float16* Ak, int i, int slot) {
         const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
-        al[slot] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
+        if constexpr (NP == 3) al[slot] = *reinterpret_cast<const f16x8*>(Ak + bo + WIN_PIX * 16);
         ah[slot] = *reinterpret_cast<const f16x8*>(Ak + bo);
     };
     auto rd_b = [&](const _Float16* Bk, int jb) {
         bh[jb] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32);
-        bl[jb] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32 + W16_BSLOT);
+        if constexpr (NP == 3) bl[jb] = *reinterpret_cast<const f16x8*>(Bk + jb * 16 * 32 + W16_BSLOT);
     };
     {  // k-step 0's fragments (published by the prologue's barrier)
         rd_a(a_base(0), 0, 0);
@@ -978,8 +985,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
 #pragma unroll
                     for (int jb = 0; jb < 4; ++jb) {
                         const int sl = i & 1;
-                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[sl], bh[jb], t[i][jb], 0, 0, 0);
-                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], bl[jb], t[i][jb], 0, 0, 0);
+                        if constexpr (NP == 3) {
+                            t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[sl], bh[jb], t[i][jb], 0, 0, 0);
+                            t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], bl[jb], t[i][jb], 0, 0, 0);
+                        }
                         t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], bh[jb], t[i][jb], 0, 0, 0);
                         if (i == 3) rd_b(Bn, jb);  // the next k-step's column block jb
                     }
@@ -2034,12 +2043,16 @@ int launch_win(const dcs_conv_desc& d, int H, int W, int reflect, const float* s
     a.R = 256 / W; a.tiles = H / a.R; a.gy = d.Co / WIN_BN; a.rng_n = d.rng_a_n;
     const unsigned blocks = (unsigned)(a.N * a.tiles * a.gy);
     const IbwArgs ib = ibw ? *ibw : IbwArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-    if (DCS_WIN16 && d.mma == DCS_MMA_F16X3 && W >= 16 && d.Cs % 32 == 0) {  // the 16x16x32 kernel
+    if (DCS_WIN16 && (d.mma == DCS_MMA_F16X3 || DCS_WIN16_F16) && W >= 16 && d.Cs % 32 == 0) {  // the 16x16x32 kernel
         const _Float16* h = reinterpret_cast<const _Float16*>(wh);
         const _Float16* l = reinterpret_cast<const _Float16*>(wl);
 #define DCS_WIN16_LAUNCH(IBW_, WIDE_)                                                                              \
-    hipLaunchKernelGGL((conv3_win16_kernel<IBW_, WIDE_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src, h, l, d.rng_a, wexp, \
-                       addend, out, parts, ib);
+    if (d.mma == DCS_MMA_F16X3)                                                                                \
+        hipLaunchKernelGGL((conv3_win16_kernel<3, IBW_, WIDE_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src, h, l,   \
+                           d.rng_a, wexp, addend, out, parts, ib);                                                 \
+    else                                                                                                        \
+        hipLaunchKernelGGL((conv3_win16_kernel<1, IBW_, WIDE_>), dim3(blocks), dim3(WIN_NT), 0, s, a, src, h, l,   \
+                           d.rng_a, wexp, addend, out, parts, ib);
         if (W >= 64) {
             if (ibw) { DCS_WIN16_LAUNCH(true, true) } else { DCS_WIN16_LAUNCH(false, true) }
         } else {
