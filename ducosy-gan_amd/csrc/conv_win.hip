@@ -49,6 +49,11 @@ __device__ unsigned long long g_win_t[16384 * 5];
                        // -2..3 % per launch in kbench, neutral in the step (133.4 vs 133.6 ms): not the default
 #define DCS_WIN16_F16 0
 #endif
+#ifndef DCS_WIN_ASYNC  // the 16x16x32 window conv's unit loads as asm with explicit vmcnt waits and four B buffers
+                       // (each B DMA two k-steps to land instead of one): bit-identical, 1 % slower per launch in
+                       // kbench, neutral in the step (profiles/r06/ab/r06ad_*): off
+#define DCS_WIN_ASYNC 0
+#endif
 #ifndef DCS_RING16  // the padded-grid ring of the residual data gradient on ring16_kernel (0: the rows pass)
 #define DCS_RING16 1
 #endif
@@ -773,10 +778,14 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                                                                 const float* __restrict__ addend,
                                                                 float* __restrict__ out, Part* __restrict__ parts,
                                                                 IbwArgs ib) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + 3 * 2 * W16_BSLOT + 8];
+    // B buffers: the k-step in use's fragments are in registers; the next one's are read during it, so its
+    // DMA must have landed by the barrier before.  DCS_WIN_ASYNC: four buffers, the DMA three k-steps ahead,
+    // so each DMA has two k-steps to land; otherwise three, the DMA two ahead, and vmcnt(0) per k-step
+    constexpr int NBUF = DCS_WIN_ASYNC ? 4 : 3;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + NBUF * 2 * W16_BSLOT + 8];
     _Float16* const Wn = smem;                        // [2 buffers][2 planes][WIN_PIX][16]
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;  // [3 buffers][2 planes][128 rows][32 k]
-    _Float16* const Wspare = Bs + 3 * 2 * W16_BSLOT;  // 16 bytes nobody reads
+    _Float16* const Wspare = Bs + NBUF * 2 * W16_BSLOT;  // 16 bytes nobody reads
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -830,20 +839,36 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
         }
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
-    float4 wq_[2];
-    auto win_load_u = [&](int q, int s) {
+    f32x4v wq_[2];  // (ext vectors: tied operands of the wait below)
+    // DCS_WIN_ASYNC: the unit loads as inline asm, untracked by the compiler like the B DMA, so no wait of
+    // the compiler's drains the k-step's own DMA (its waits for these registers counted only the tracked
+    // loads: vmcnt(0) at every store); the waits are explicit (win_wait_u, the end of each k-step)
+    auto win_load_into = [&](int q, int s, f32x4v (&dst)[2]) {
         const int off = uoff[q] >= 0 ? uoff[q] + s * 64 : 0x7fffffbf;
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
-        u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
-        __builtin_memcpy(&wq_[0], &v0, 16);
-        __builtin_memcpy(&wq_[1], &v1, 16);
+        if constexpr (DCS_WIN_ASYNC) {
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(dst[0]) : "v"(off), "s"(srsrc) : "memory");
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(dst[1]) : "v"(off), "s"(srsrc) : "memory");
+        } else {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
+            u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
+            __builtin_memcpy(&dst[0], &v0, 16);
+            __builtin_memcpy(&dst[1], &v1, 16);
+        }
+    };
+    auto win_load_u = [&](int q, int s) { win_load_into(q, s, wq_); };
+    // before a unit's store: its two loads landed, the k-step's two DMA pieces issued after them may not
+    auto win_wait_u = [&]() {
+        // (asm: the compiler drops waits it sees no need for; the registers as operands so no use of them
+        // is scheduled above the wait)
+        if constexpr (DCS_WIN_ASYNC) asm volatile("s_waitcnt vmcnt(2)" : "+v"(wq_[0]), "+v"(wq_[1]) : : "memory");
     };
     auto win_store_u = [&](int q, int buf) {
         const int h = (tid + q * WIN_NT) & 1;
         const int wp = (uwd[q] & 0xffff) - 1, wd = (uwd[q] >> 16) - 1;
         f16x8 hi, lo;
-        split8h(wq_[0], wq_[1], asc, hi, lo);
+        split8h(make_float4(wq_[0][0], wq_[0][1], wq_[0][2], wq_[0][3]),
+                make_float4(wq_[1][0], wq_[1][1], wq_[1][2], wq_[1][3]), asc, hi, lo);
         *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 0, wp, h) : Wspare) = hi;
         if constexpr (NP == 3) *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + w16_off(buf, 1, wp, h) : Wspare) = lo;
         if (wd >= 0) {
@@ -901,16 +926,19 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     // flight before the first store
     b_dma(0, 0);
     b_dma(1, 1);
-    win_load_u(1, 0);
-    const float4 wp1[2] = {wq_[0], wq_[1]};
+    if constexpr (NBUF == 4) b_dma(2, 2);
+    f32x4v wp1[2];
+    win_load_into(1, 0, wp1);
     win_load_u(0, 0);
     ea = f16x3_exp(rng, a.rng_n);
     asc = __builtin_ldexpf(1.f, ea);
+    // vmcnt(0): the units (asm loads in DCS_WIN_ASYNC, so the wait is asm too, tied to their registers)
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wq_[0]), "+v"(wq_[1]), "+v"(wp1[0]), "+v"(wp1[1]) : : "memory");
     win_store_u(0, 0);
     wq_[0] = wp1[0];
     wq_[1] = wp1[1];
     win_store_u(1, 0);
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the DMAs have landed (asm: kept)
     __syncthreads();
 
     const int nstep = 9 * npair;
@@ -969,14 +997,17 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                 const int ph = js < 3 ? js : (js >= 5 && js < 8 ? js - 5 : -1);  // position in a staging window
                 const int sbuf = js < 3 ? 1 : 0, ssl = js < 3 ? s_odd : s_even;
                 if constexpr (ROLE == 1) {  // unit ph - 1 stored at the top of the next k-step
-                    if (ph == 1 || ph == 2) win_store_u(ph - 1, sbuf);
+                    if (ph == 1 || ph == 2) {
+                        win_wait_u();
+                        win_store_u(ph - 1, sbuf);
+                    }
                 }
                 if (ph == 0 || ph == 1) win_load_u(ph, ssl);
-                b_dma(j + 2 < nstep ? j + 2 : nstep - 1, (js + 2) % 3);
+                b_dma(j + NBUF - 1 < nstep ? j + NBUF - 1 : nstep - 1, (j + NBUF - 1) % NBUF);
                 __builtin_amdgcn_sched_barrier(0);  // the loads stay at the top of the k-step
                 const _Float16* const Ak = a_base(js);
                 const _Float16* const An = a_base((js + 1) % 9);
-                const _Float16* const Bn = b_base((js + 1) % 3);
+                const _Float16* const Bn = b_base((j + 1) % NBUF);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (i < 3) rd_a(Ak, i + 1, (i + 1) & 1);
@@ -995,7 +1026,10 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if constexpr (ROLE == 0) {
-                    if (ph == 0 || ph == 1) win_store_u(ph, sbuf);
+                    if (ph == 0 || ph == 1) {
+                        win_wait_u();
+                        win_store_u(ph, sbuf);
+                    }
                 }
                 if (js == 4 || js == 8) {  // close the accumulation chain (160 / 128 k)
 #pragma unroll
@@ -1008,13 +1042,23 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
                             t[i][jj] = f32x4v{0.f, 0.f, 0.f, 0.f};
                         }
                 }
-                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
+                if constexpr (DCS_WIN_ASYNC) {
+                    // the DMA issued one k-step ago (B k-step j + 2, read from the next k-step on) has landed
+                    // once only this k-step's loads (the unit's two, if any, and the DMA's two) are in flight
+                    if (ph == 0 || ph == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMAs (and window loads) landed
+                }
                 __syncthreads();
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
     };
     if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
     else kloop(std::integral_constant<int, 0>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (repeat) DMAs landed before the epilogue
 
     // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
     const int eab = -(ea + eb);
