@@ -16,7 +16,7 @@ path's on every layer, tests/test_gpu_mma.py); --mma f32 runs the exact v_mfma_f
 path; --mma f16 is BASELINE config 5's fp16 MFMA path (one product of the scaled fp16 operands).
 
 roofline: the dominant kernel is the 256-ch 3x3 residual-block convolution (forward + data-gradient
-launches; in the fp16 modes the window kernels: conv3_win16_kernel in f16x3, conv3_win_h3_kernel<1> in f16).  Its per-launch duration is
+launches; in the fp16 modes the 16x16x32 window kernel conv3_win16_kernel).  Its per-launch duration is
 measured live with HIP events on the launch stream over the timed steps; FLOPs are algorithmic
 (2*pixels*256*256*9 per launch).  Peak: 157.3 TFLOP/s for f32 (gfx950 f32 MFMA, dense); the dense
 fp16/bf16 MFMA peak (2.5 PF) divided by the products per fragment pair in the split modes (f16x3:
@@ -311,7 +311,7 @@ def main():
             },
             "roofline": {
                 "kernel": ("256-ch 3x3 residual conv on the window kernel "
-                           f"{'conv3_win16_kernel (v_mfma_f32_16x16x32_f16)' if args.mma == 'f16x3' else 'conv3_win_h3_kernel<1>'}: "
+                           f"conv3_win16_kernel<{3 if args.mma == 'f16x3' else 1}> (v_mfma_f32_16x16x32_f16): "
                            "forward, and the data gradient's interior (+ its padded-grid ring on "
                            f"ring16_kernel<{3 if args.mma == 'f16x3' else 1}, 8> and the ring fold, inside the timed launch)"
                            if args.mma in ("f16x3", "f16") else

@@ -44,10 +44,13 @@ __device__ unsigned long long g_win_t[16384 * 5];
                       // MFMAs, -1.5 % per launch; 0: between its k-steps; 2-4: rejected placements)
 #define DCS_WW_STAGE 1
 #endif
-#ifndef DCS_WIN16_F16  // the f16 mode's residual convs on the 16x16x32 window kernel too (NP 1, one barrier per
-                       // 16-MFMA k-step; 0: conv3_win_h3_kernel<1>, one barrier per 36-MFMA slice).  Measured
-                       // -2..3 % per launch in kbench, neutral in the step (133.4 vs 133.6 ms): not the default
-#define DCS_WIN16_F16 0
+#ifndef DCS_WIN16_F16  // the f16 mode's residual convs on the 16x16x32 window kernel too (NP 1, three k-steps of
+                       // 16 MFMAs per barrier, DCS_WIN16_G3; 0: conv3_win_h3_kernel<1>, one barrier per 36-MFMA
+                       // slice): -5..6 % per launch, f16 step 133.5 -> 131.0 ms (profiles/r06/ab/r06ag_*)
+#define DCS_WIN16_F16 1
+#endif
+#ifndef DCS_WIN16_G3  // NP 1 on the 16x16x32 kernel: three k-steps per barrier (0: one, as f16x3; measured neutral)
+#define DCS_WIN16_G3 1
 #endif
 #ifndef DCS_WIN_ASYNC  // the 16x16x32 window conv's unit loads as asm with explicit vmcnt waits and four B buffers
                        // (each B DMA two k-steps to land instead of one): bit-identical, 1 % slower per launch in
@@ -782,10 +785,13 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     // DMA must have landed by the barrier before.  DCS_WIN_ASYNC: four buffers, the DMA three k-steps ahead,
     // so each DMA has two k-steps to land; otherwise three, the DMA two ahead, and vmcnt(0) per k-step
     constexpr int NBUF = DCS_WIN_ASYNC ? 4 : 3;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + NBUF * 2 * W16_BSLOT + 8];
+    // G3 (NP 1, DCS_WIN16_G3): three k-steps per barrier, nine single-plane B buffers (one per k-step of a pair)
+    constexpr bool G3 = NP == 1 && DCS_WIN16_G3;
+    constexpr int BSLOTS = G3 ? 9 : NBUF * 2;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * WIN_PIX * 16 + BSLOTS * W16_BSLOT + 8];
     _Float16* const Wn = smem;                        // [2 buffers][2 planes][WIN_PIX][16]
     _Float16* const Bs = smem + 2 * 2 * WIN_PIX * 16;  // [3 buffers][2 planes][128 rows][32 k]
-    _Float16* const Wspare = Bs + NBUF * 2 * W16_BSLOT;  // 16 bytes nobody reads
+    _Float16* const Wspare = Bs + BSLOTS * W16_BSLOT;  // 16 bytes nobody reads
 
     const int T = gridDim.x;
     const int L = xcd_remap(blockIdx.x, T);
@@ -922,6 +928,137 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
 #pragma unroll
         for (int j = 0; j < 4; ++j) { acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; t[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f}; }
 
+    if constexpr (G3) {
+    // NP 1 (f16 operands, hi planes only): one product per fragment pair leaves 16 MFMAs per wave and k-step,
+    // so the k-steps of a pair run in three groups of three between barriers (48 MFMAs per wave per barrier,
+    // as one f16x3 k-step).  B: one single-plane buffer per k-step of a pair (buffer = js), the DMA for group
+    // g + 2 issued at the top of group g.  Window: the lo-plane slots are free, so slices rotate through four
+    // single-plane slots (slice s in slot s & 3): the next pair's even slice is loaded in group 0 and stored at
+    // the top of group 1 (published before group 2 reads its first fragments for the next pair), the odd one
+    // loaded in group 1 and stored at the top of group 2 (published before the next pair's group 1).
+    const unsigned bsl = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
+    const unsigned ddst1 = __builtin_amdgcn_readfirstlane(bsl + 2u * (unsigned)(wid * 16 * 32));
+    auto dma1 = [&](int j, int buf) {  // k-step j (packed k 32 j ..) into single-plane buffer buf
+        win_glds(dbase[0], dlane + (dsu[0] + 2u * (unsigned)(j * 32)), ddst1 + 2u * (unsigned)(buf * W16_BSLOT));
+    };
+    auto dma_group = [&](int p_, int g_) {  // group g_ of pair p_
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dma1(9 * p_ + 3 * g_ + k, 3 * g_ + k);
+    };
+    f32x4v wq1[2];
+    auto store_slot = [&](int q, int slot, const f32x4v (&v)[2]) {
+        const int h = (tid + q * WIN_NT) & 1;
+        const int wp = (uwd[q] & 0xffff) - 1, wd = (uwd[q] >> 16) - 1;
+        f16x8 hi, lo;
+        split8h(make_float4(v[0][0], v[0][1], v[0][2], v[0][3]), make_float4(v[1][0], v[1][1], v[1][2], v[1][3]),
+                asc, hi, lo);
+        *reinterpret_cast<f16x8*>(wp >= 0 ? Wn + (slot * WIN_PIX + wp) * 16 + 8 * h : Wspare) = hi;
+        if (wd >= 0) *reinterpret_cast<f16x8*>(Wn + (slot * WIN_PIX + wd) * 16 + 8 * h) = hi;
+    };
+    auto load_slice = [&](int sl) {  // both units of slice sl: unit 0 into wq_, unit 1 into wq1
+        win_load_into(0, sl, wq_);
+        win_load_into(1, sl, wq1);
+    };
+    auto store_slice = [&](int sl) {
+        store_slot(0, sl & 3, wq_);
+        store_slot(1, sl & 3, wq1);
+    };
+    // prologue: B groups 0 and 1 of pair 0, slices 0 and 1, the exponent
+    dma_group(0, 0);
+    dma_group(0, 1);
+    load_slice(0);
+    ea = f16x3_exp(rng, a.rng_n);
+    asc = __builtin_ldexpf(1.f, ea);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wq_[0]), "+v"(wq_[1]), "+v"(wq1[0]), "+v"(wq1[1]) : : "memory");
+    store_slice(0);
+    load_slice(1);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wq_[0]), "+v"(wq_[1]), "+v"(wq1[0]), "+v"(wq1[1]) : : "memory");
+    store_slice(1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f16x8 bh[4], ah[2];
+    auto a_base1 = [&](int js_, int podd) {  // A base of k-step js_ (units 2 js_, 2 js_ + 1) of a pair
+        const int u0 = 2 * js_, u1 = 2 * js_ + 1;
+        const int t0 = u0 % 9, t1 = u1 % 9;
+        const int o0 = (2 * podd + u0 / 9) * WIN_PIX * 16 + ((t0 / 3) * WP + t0 % 3) * 16;
+        const int o1 = (2 * podd + u1 / 9) * WIN_PIX * 16 + ((t1 / 3) * WP + t1 % 3) * 16;
+        int al_ = alane;
+        asm volatile("" : "+v"(al_));
+        return Wn + al_ + (hiu ? o1 : o0);
+    };
+    auto b_base1 = [&](int buf) {
+        int bl_ = blane;
+        asm volatile("" : "+v"(bl_));
+        return Bs + buf * W16_BSLOT + bl_;
+    };
+    auto rd_a1 = [&](const _Float16* Ak, int i, int slot) {
+        const int bo = WIDE ? 256 * i : ublk[i] - ublk[0];
+        ah[slot] = *reinterpret_cast<const f16x8*>(Ak + bo);
+    };
+    {  // k-step 0's fragments
+        rd_a1(a_base1(0, 0), 0, 0);
+        const _Float16* const B0 = b_base1(0);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) bh[jb] = *reinterpret_cast<const f16x8*>(B0 + jb * 16 * 32);
+    }
+    for (int p = 0; p < npair; ++p) {
+        const int podd = p & 1;
+        const bool more = p + 1 < npair;  // (block-uniform)
+#pragma unroll
+        for (int g_ = 0; g_ < 3; ++g_) {
+            // group top: the staging of the next pair's slices, and the B DMA two groups ahead
+            if (g_ == 0) {
+                dma_group(p, 2);
+                if (more) load_slice(2 * p + 2);
+            } else if (g_ == 1) {
+                if (more) {
+                    store_slice(2 * p + 2);
+                    dma_group(p + 1, 0);
+                    load_slice(2 * p + 3);
+                }
+            } else {
+                if (more) {
+                    store_slice(2 * p + 3);
+                    dma_group(p + 1, 1);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < 3; ++kk) {
+                const int js = 3 * g_ + kk;
+                const _Float16* const Ak = a_base1(js, podd);
+                const _Float16* const An = js < 8 ? a_base1(js + 1, podd) : a_base1(0, podd ^ 1);
+                const _Float16* const Bn = b_base1(js < 8 ? js + 1 : 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (i < 3) rd_a1(Ak, i + 1, (i + 1) & 1);
+                    else rd_a1(An, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb) {
+                        t[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i & 1], bh[jb], t[i][jb], 0, 0, 0);
+                        if (i == 3) bh[jb] = *reinterpret_cast<const f16x8*>(Bn + jb * 16 * 32);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (js == 4 || js == 8) {  // close the accumulation chain (160 / 128 k)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            acc[i][jj] += t[i][jj];
+                            asm volatile("" : "+v"(acc[i][jj]));
+                            t[i][jj] = f32x4v{0.f, 0.f, 0.f, 0.f};
+                        }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the group's DMAs and stores landed
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    } else {
     // prologue: window of slice 0 (buffer 0) and B k-steps 0 and 1, every load (and the exponent's) in
     // flight before the first store
     b_dma(0, 0);
@@ -1059,6 +1196,7 @@ __global__ __launch_bounds__(WIN_NT, 1) void conv3_win16_kernel(WinArgs a, const
     if (wid >= 4) kloop(std::integral_constant<int, 1>{});  // (wave-uniform branch)
     else kloop(std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (repeat) DMAs landed before the epilogue
+    }
 
     // epilogue: undo the operand scales, + addend, NHWC store, IN statistics
     const int eab = -(ea + eb);
