@@ -55,6 +55,14 @@ _WIN = True
 # pair at 0.60 of its bar, the 512 x 512 pair within 1.4e-4 / 3.7e-3 of f16x3; scripts/diag/f16_layers.py,
 # profiles/r06/ab/r06ab_*), f16 step 138.7 -> 133.5 ms same box
 _PHASE_F16X3 = frozenset()
+# the Generator's stem and head kernels on f16x3 operands in both fp16 modes ("stem": forward, "stem_wgrad",
+# "head": forward, data and weight gradient); a layer left out runs in the step's mode (env DUCOSY_F16X3_LAYERS:
+# a comma-separated list in place of the default)
+_FIXED_F16X3 = frozenset(x for x in os.environ.get("DUCOSY_F16X3_LAYERS", "stem,stem_wgrad,head").split(",") if x)
+
+
+def _fixed_mma(layer: str) -> int:
+    return lib.MMA_F16X3 if layer in _FIXED_F16X3 else _MMA
 
 
 def _h3() -> bool:
@@ -696,7 +704,7 @@ class ConvGeom:
         """The Generator stem (7x7 reflect-pad-3, NHWC x 4 source -> 64) on its MFMA kernel
         (csrc/conv_stem.hip), with the IN statistics of its output when ``stats``."""
         dev = s.t.device
-        d.mma = lib.MMA_F16X3  # f16x3 in both fp16 modes: the layer is small, and its error feeds every later one
+        d.mma = _fixed_mma("stem")  # (f16x3 in both fp16 modes: the layer is small, and its error feeds every later one)
         out = torch.empty(s.N, s.H, s.W, self.cout, device=dev, dtype=torch.float32)
         parts = workspace(lib.query("dcs_stem_fwd_parts_size", ctypes.byref(d)), dev) if stats else None
         nchunk = ctypes.c_int(0)
@@ -809,7 +817,7 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         if self.narrow and _HEAD_PROJ and pro is not None and pro_max is not None and _h3() and s.t2 is None:
-            d.mma = lib.MMA_F16X3  # the head in both fp16 modes (its share of the step is small)
+            d.mma = _fixed_mma("head")  # (f16x3 in both fp16 modes: its share of the step is small)
             if lib.query("dcs_head_fwd_proj_ok", ctypes.byref(d)):
                 lib.call("dcs_head_fwd_proj", ctypes.byref(d), _p(s.t), _p(wpack), _p(bias), _p(pro[0]), _p(pro[1]),
                          _p(pro_max), _p(out), _stream())
@@ -1046,7 +1054,7 @@ class ConvGeom:
         d = self._desc_fwd(s, 0, pro_act, ACT_NONE, rows=not self.narrow)
         if self.narrow and _HEAD_PROJ and pro is not None and pro_max is not None and _h3() and s.t2 is None \
                 and dy.is_contiguous():
-            m0, d.mma = d.mma, lib.MMA_F16X3
+            m0, d.mma = d.mma, _fixed_mma("head")
             if lib.query("dcs_head_fwd_proj_ok", ctypes.byref(d)):
                 if out is None:
                     out = torch.empty(self.cout, self.cin, self.k, self.k, device=dy.device, dtype=torch.float32)
@@ -1065,7 +1073,7 @@ class ConvGeom:
                               dtype=torch.float32)
         if _STEM and pro is None and dy.is_contiguous() and lib.query("dcs_stem_wgrad_ok", ctypes.byref(d)):
             ws = workspace(lib.query("dcs_stem_wgrad_workspace_size", ctypes.byref(d)), dy.device)
-            d.mma = lib.MMA_F16X3
+            d.mma = _fixed_mma("stem_wgrad")
             lib.call("dcs_stem_wgrad", ctypes.byref(d), _p(dy), _p(s.t), _p(out), _p(ws), ws.numel(), _stream())
             return out
         if self.narrow:
@@ -1153,7 +1161,7 @@ def head_dgrad_in(dy_out: torch.Tensor, wk: torch.Tensor, y: torch.Tensor, st: I
     g = dy_out.contiguous()
     g_rng = range_rec(g.view(N, H, W, 1))
     lib.call("dcs_head_dgrad_in", _p(g), _p(g_rng), g_rng.numel(), _p(wk), N, H, W, _p(y), _p(st.scale), _p(st.shift),
-             act, lib.MMA_F16X3, _p(dy), _p(ws), ws.numel(), _out_rng(dy), _stream())
+             act, _fixed_mma("head"), _p(dy), _p(ws), ws.numel(), _out_rng(dy), _stream())
     return dy
 
 

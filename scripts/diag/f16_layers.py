@@ -1,4 +1,4 @@
-"""Which window phase-kernel layers can run on fp16 operands in config 5's fp16 mode: the f16 soft +
+"""Which window phase-kernel layers (and, with --fixed, which stem / head kernels) can run on fp16 operands in config 5's fp16 mode: the f16 soft +
 lung pair (tests/test_gpu_concurrent.py::test_dual_f16_vs_reference) with ops._PHASE_F16X3 narrowed,
 printing per variant the largest deviation of every loss term as a fraction of that test's bar (<= 1
 passes).   python scripts/diag/f16_layers.py"""
@@ -20,8 +20,9 @@ from modules.trainer import ConcurrentCycleGANs  # noqa: E402
 ALL = ("up1", "up2", "pg64", "pg128", "pg256")
 
 
-def run(keep):
+def run(keep, fixed=("stem", "stem_wgrad", "head")):
     ops._PHASE_F16X3 = frozenset(keep)
+    ops._FIXED_F16X3 = frozenset(fixed)
     z = np.load(os.path.join(GOLDEN, "steps_64.npz"))
     n, hw, nb, cin, steps, seed = [int(v) for v in z["meta"]]
     lung_seed = 813
@@ -55,6 +56,14 @@ def run(keep):
 
 
 if __name__ == "__main__":
+    if "--fixed" in sys.argv:  # the stem / head kernels (ops._FIXED_F16X3), phase layers all on fp16
+        FX = ("stem", "stem_wgrad", "head")
+        for fixed in (FX, (), ("stem", "head"), ("stem",), ("head",), ("stem", "stem_wgrad")):
+            w = run((), fixed)
+            top = sorted(w.items(), key=lambda kv: -kv[1])[:3]
+            print(f"f16x3 kernels {list(fixed)}: max {max(w.values()):.2f}  " +
+                  "  ".join(f"{m}/{k.replace('loss_', '')} {r:.2f}" for (m, k), r in top), flush=True)
+        sys.exit(0)
     variants = [ALL, ()] + [tuple(x for x in ALL if x != d) for d in ALL]
     for keep in variants:
         w = run(keep)
