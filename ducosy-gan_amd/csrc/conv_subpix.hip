@@ -26,6 +26,12 @@
 #include "common.hpp"
 #include "conv_common.hpp"
 
+#ifndef DCS_SP_PAIR  // f16: two k iterations per barrier in the window phase kernel's forward-type launches (the
+                     // up-conv forward, the stride-2 forward and data gradient; 0: one, as f16x3): 3-7 % per launch,
+                     // bit-identical; the up-conv data gradient measured 2-3 % slower with it and keeps one
+#define DCS_SP_PAIR 1
+#endif
+
 namespace dcs {
 namespace {
 
@@ -80,6 +86,14 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                                                               const int* __restrict__ wexp, float* __restrict__ out,
                                                               Part* __restrict__ parts, const float* __restrict__ psc,
                                                               const float* __restrict__ psh, PhIbw ib) {
+    // f16 (NP 1, DCS_SP_PAIR; not the up-conv data gradient): a slice is only 16 MFMAs per wave, so two
+    // iterations run per barrier, the second one's window and B in the planes f16x3 gives its lo halves
+    // (same sums in the same order)
+    // Two window register sets (both loads in flight from the barrier) where the registers allow; the
+    // stride-2 and prologue kernels reuse one (the second window loaded after the first one's store)
+    constexpr bool PAIR = NP == 1 && DCS_SP_PAIR && (MODE == 0 || S2);
+    constexpr bool WR2 = !S2 && !PRO;
+    constexpr int NI = PAIR ? 2 : 1;  // iterations per barrier
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * SP_PIX * 16 + 2 * 2 * 4 * SP_SLOT];
     __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 2 * SP_PROC : 4];  // [scale | shift][channel]
     _Float16* const Wn = smem;
@@ -138,8 +152,9 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     }
     const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffff00, 0x00020000);
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    float4 wr_[SP_UNITS][2];
-    int vmask = 0, vit = 0;  // PRO: the staged units inside the image, and their iteration
+    constexpr int NWR = PAIR && WR2 ? 2 : 1;
+    float4 wr_[NWR][SP_UNITS][2];
+    int vmask[NWR] = {}, vit[NWR] = {};  // PRO: the staged units inside the image, and their iteration
     auto unit_off = [&](int q, int it) {  // byte offset of unit q's 8 channels at iteration it (OOB: zero)
         if constexpr (MODE == 0) {
             return uoff[q] >= 0 ? uoff[q] + it * 64 : 0x7fffffbf;
@@ -149,40 +164,41 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             return (uvm[q] >> ph) & 1 ? uoff[q] + pshift : 0x7fffffbf;
         }
     };
-    auto win_load = [&](int it) {
-        if constexpr (PRO) { vmask = 0; vit = it; }
+    auto win_load = [&](int it, int p) {  // into register set p
+        if constexpr (PRO) { vmask[p] = 0; vit[p] = it; }
 #pragma unroll
         for (int q = 0; q < SP_UNITS; ++q) {
             const int off = unit_off(q, it);
-            if constexpr (PRO) vmask |= (off != 0x7fffffbf) << q;
+            if constexpr (PRO) vmask[p] |= (off != 0x7fffffbf) << q;
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(srsrc, off + 16, 0, 0);
-            __builtin_memcpy(&wr_[q][0], &v0, 16);
-            __builtin_memcpy(&wr_[q][1], &v1, 16);
+            __builtin_memcpy(&wr_[p][q][0], &v0, 16);
+            __builtin_memcpy(&wr_[p][q][1], &v1, 16);
         }
     };
-    auto win_store = [&](int buf) {
+    auto win_store = [&](int buf, int p, int pl) {  // register set p: the hi plane into plane pl, f16x3 also the lo
 #pragma unroll
         for (int q = 0; q < SP_UNITS; ++q) {
             const int u = tid + q * SP_NT;
             const int wpix = u >> 1, h = u & 1;
+            float4 (&wr)[2] = wr_[p][q];
             if (wpix < npix) {
                 if constexpr (PRO) {  // a = act(y * scale + shift) inside the image, 0 in the padding
-                    const int c0 = (vit % nslice) * 16 + 8 * h;
+                    const int c0 = (vit[p] % nslice) * 16 + 8 * h;
                     const float4 s0 = *reinterpret_cast<const float4*>(pro_s + c0);
                     const float4 s1 = *reinterpret_cast<const float4*>(pro_s + c0 + 4);
                     const float4 b0 = *reinterpret_cast<const float4*>(pro_s + SP_PROC + c0);
                     const float4 b1 = *reinterpret_cast<const float4*>(pro_s + SP_PROC + c0 + 4);
-                    const bool ok = (vmask >> q) & 1;
+                    const bool ok = (vmask[p] >> q) & 1;
                     auto f = [&](float v, float sc, float sh) { return ok ? act_apply(fmaf(v, sc, sh), a.pro_act) : 0.f; };
-                    wr_[q][0] = make_float4(f(wr_[q][0].x, s0.x, b0.x), f(wr_[q][0].y, s0.y, b0.y),
-                                            f(wr_[q][0].z, s0.z, b0.z), f(wr_[q][0].w, s0.w, b0.w));
-                    wr_[q][1] = make_float4(f(wr_[q][1].x, s1.x, b1.x), f(wr_[q][1].y, s1.y, b1.y),
-                                            f(wr_[q][1].z, s1.z, b1.z), f(wr_[q][1].w, s1.w, b1.w));
+                    wr[0] = make_float4(f(wr[0].x, s0.x, b0.x), f(wr[0].y, s0.y, b0.y),
+                                        f(wr[0].z, s0.z, b0.z), f(wr[0].w, s0.w, b0.w));
+                    wr[1] = make_float4(f(wr[1].x, s1.x, b1.x), f(wr[1].y, s1.y, b1.y),
+                                        f(wr[1].z, s1.z, b1.z), f(wr[1].w, s1.w, b1.w));
                 }
                 f16x8 hi, lo;
-                split8h(wr_[q][0], wr_[q][1], asc, hi, lo);
-                *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 0, wpix, h)) = hi;
+                split8h(wr[0], wr[1], asc, hi, lo);
+                *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, pl, wpix, h)) = hi;
                 if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 1, wpix, h)) = lo;
             }
         }
@@ -191,8 +207,9 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     // plane, 2, 3 the lo plane: f16 loads only the first two); chunk -> (plane, row, tap, half) with
     // (tap, half) fastest (the 128 contiguous bytes of a row).  S2: the chunks of (row, tap) pairs the
     // MFMA loop skips load nothing (an out-of-range buffer offset reads zero without a fetch): 7 of the
-    // 16 (phase, tap) pairs of the forward, up to 5 of 8 of a data gradient launch
-    constexpr int NBC = NP == 3 ? 4 : 2;
+    // 16 (phase, tap) pairs of the forward, up to 5 of 8 of a data gradient launch.  PAIR: chunks 2, 3
+    // are the hi plane of the next iteration (clamped to the last)
+    constexpr int NBC = NP == 3 || PAIR ? 4 : 2;
     const __amdgpu_buffer_rsrc_t bhr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(wh), (short)0, 0x7fffff00, 0x00020000);
     const __amdgpu_buffer_rsrc_t blr = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(NP == 3 ? wl : wh), (short)0, 0x7fffff00, 0x00020000);
     int bg[NBC], bl[NBC], bt[NBC];
@@ -206,10 +223,11 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         bt[i] = (c8 >> 1) | ((row >> 6) << 2);  // tap (u, t) and the row's 64-row half (MODE 0: py)
     }
     u32x4 br[NBC];
-    auto b_load = [&](int it) {
-        const int kb = it * 128;  // bytes
+    auto b_load = [&](int it0) {
 #pragma unroll
         for (int i = 0; i < NBC; ++i) {
+            const int it = PAIR && i >= 2 ? (it0 + 1 < nit ? it0 + 1 : it0) : it0;
+            const int kb = it * 128;  // bytes
             bool skip = false;
             if constexpr (S2) {
                 const int u = (bt[i] >> 1) & 1, t = bt[i] & 1;
@@ -250,7 +268,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
 
     // prologue: every load of iteration 0 (and the exponent's, the PRO table's) in flight before the
     // first store
-    win_load(0);
+    win_load(0, 0);
+    if constexpr (PAIR && WR2) win_load(nit > 1 ? 1 : 0, 1);
     b_load(0);
     if constexpr (PRO) {  // the image's prologue scale / shift (published by the barrier below)
         for (int c = tid; c < C; c += SP_NT) {
@@ -261,75 +280,157 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     }
     ea = f16x3_exp(rng, a.rng_n);
     asc = __builtin_ldexpf(1.f, ea);
-    win_store(0);
+    win_store(0, 0, 0);
+    if constexpr (PAIR && !WR2) win_load(nit > 1 ? 1 : 0, 0);
+    if constexpr (PAIR) win_store(0, WR2 ? 1 : 0, 1);
     b_store(0);
     __syncthreads();
 
     f16x8 fh[3], fl[3];
-    for (int s = 0; s < nit; ++s) {
-        const int buf = s & 1, sn = s + 1 < nit ? s + 1 : s;
-        win_load(sn);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
-        b_load(sn);
-#pragma unroll
-        for (int tap = 0; tap < 4; ++tap) {
-            const int u = tap >> 1, tx = tap & 1;
-            // S2: the pairs no tap reaches (wave-uniform: py per wave, px per workgroup, the class per
-            // iteration)
-            bool skip_row = false, skip_col = false;
-            if constexpr (S2 && MODE == 0) {
-                skip_row = py == 0 && u == 0;
-                skip_col = PXC == 0 && tx == 0;  // (both runtime: the allocator spills)
-            } else if constexpr (S2) {
-                const int ph = s / nslice;
-                skip_row = (ph >> 1) == 0 && u == 1;
-                skip_col = (ph & 1) == 0 && tx == 1;
-            }
-            if (skip_row) continue;
-            f16x8 ah[2], al[2], bh[2], bl_[2];
-            if (tx == 0) {  // fragments of window pixels wbe + u * WP + 0 .. 2 (block i, offset t: f = t + i)
-#pragma unroll
-                for (int f = 0; f < 3; ++f) {
-                    const int wpix = wbe + u * WP + f;
-                    fh[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 0, wpix, kh));
-                    if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 1, wpix, kh));
+    // one k iteration s (its hi plane pl) over the staged buffer
+    auto iter = [&](int buf, int s, int pl) {
+    #pragma unroll
+            for (int tap = 0; tap < 4; ++tap) {
+                const int u = tap >> 1, tx = tap & 1;
+                // S2: the pairs no tap reaches (wave-uniform: py per wave, px per workgroup, the class per
+                // iteration)
+                bool skip_row = false, skip_col = false;
+                if constexpr (S2 && MODE == 0) {
+                    skip_row = py == 0 && u == 0;
+                    skip_col = PXC == 0 && tx == 0;  // (both runtime: the allocator spills)
+                } else if constexpr (S2) {
+                    const int ph = s / nslice;
+                    skip_row = (ph >> 1) == 0 && u == 1;
+                    skip_col = (ph & 1) == 0 && tx == 1;
                 }
-            }
-            if (skip_col) continue;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                ah[i] = fh[tx + i];
-                if constexpr (NP == 3) al[i] = fl[tx + i];
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = py * 64 + j * 32 + l32;
-                bh[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 0, tap, row, kh));
-                if constexpr (NP == 3) bl_[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 1, tap, row, kh));
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    if constexpr (NP == 3) {
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
-                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl_[j], t[i][j], 0, 0, 0);
+                if (skip_row) continue;
+                f16x8 ah[2], al[2], bh[2], bl_[2];
+                if (tx == 0) {  // fragments of window pixels wbe + u * WP + 0 .. 2 (block i, offset t: f = t + i)
+    #pragma unroll
+                    for (int f = 0; f < 3; ++f) {
+                        const int wpix = wbe + u * WP + f;
+                        fh[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, pl, wpix, kh));
+                        if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 1, wpix, kh));
                     }
-                    t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
                 }
-        }
-        // the other buffers were last read before the previous barrier
-        win_store(buf ^ 1);
-        b_store(buf ^ 1);
-        __syncthreads();
-        if ((s & 1) || s + 1 == nit) {  // close the accumulation chain every two iterations (128 k)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
+                if (skip_col) continue;
+    #pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    ah[i] = fh[tx + i];
+                    if constexpr (NP == 3) al[i] = fl[tx + i];
+                }
+    #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    acc[i][j] += t[i][j];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    const int row = py * 64 + j * 32 + l32;
+                    bh[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, pl, tap, row, kh));
+                    if constexpr (NP == 3) bl_[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 1, tap, row, kh));
                 }
+    #pragma unroll
+                for (int i = 0; i < 2; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if constexpr (NP == 3) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl_[j], t[i][j], 0, 0, 0);
+                        }
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    }
+            }
+    };
+    if constexpr (!PAIR) {
+        for (int s = 0; s < nit; ++s) {
+            const int buf = s & 1, sn = s + 1 < nit ? s + 1 : s;
+            win_load(sn, 0);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
+            b_load(sn);
+    #pragma unroll
+            for (int tap = 0; tap < 4; ++tap) {
+                const int u = tap >> 1, tx = tap & 1;
+                // S2: the pairs no tap reaches (wave-uniform: py per wave, px per workgroup, the class per
+                // iteration)
+                bool skip_row = false, skip_col = false;
+                if constexpr (S2 && MODE == 0) {
+                    skip_row = py == 0 && u == 0;
+                    skip_col = PXC == 0 && tx == 0;  // (both runtime: the allocator spills)
+                } else if constexpr (S2) {
+                    const int ph = s / nslice;
+                    skip_row = (ph >> 1) == 0 && u == 1;
+                    skip_col = (ph & 1) == 0 && tx == 1;
+                }
+                if (skip_row) continue;
+                f16x8 ah[2], al[2], bh[2], bl_[2];
+                if (tx == 0) {  // fragments of window pixels wbe + u * WP + 0 .. 2 (block i, offset t: f = t + i)
+    #pragma unroll
+                    for (int f = 0; f < 3; ++f) {
+                        const int wpix = wbe + u * WP + f;
+                        fh[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 0, wpix, kh));
+                        if constexpr (NP == 3) fl[f] = *reinterpret_cast<const f16x8*>(Wn + sp_woff(buf, 1, wpix, kh));
+                    }
+                }
+                if (skip_col) continue;
+    #pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    ah[i] = fh[tx + i];
+                    if constexpr (NP == 3) al[i] = fl[tx + i];
+                }
+    #pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int row = py * 64 + j * 32 + l32;
+                    bh[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 0, tap, row, kh));
+                    if constexpr (NP == 3) bl_[j] = *reinterpret_cast<const f16x8*>(Bs + sp_boff(buf, 1, tap, row, kh));
+                }
+    #pragma unroll
+                for (int i = 0; i < 2; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if constexpr (NP == 3) {
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], t[i][j], 0, 0, 0);
+                            t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl_[j], t[i][j], 0, 0, 0);
+                        }
+                        t[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], t[i][j], 0, 0, 0);
+                    }
+            }
+            // the other buffers were last read before the previous barrier
+            win_store(buf ^ 1, 0, 0);
+            b_store(buf ^ 1);
+            __syncthreads();
+            if ((s & 1) || s + 1 == nit) {  // close the accumulation chain every two iterations (128 k)
+    #pragma unroll
+                for (int i = 0; i < 2; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] += t[i][j];
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
+        }
+    } else {
+        for (int s0 = 0; s0 < nit; s0 += NI) {
+            const int buf = (s0 / NI) & 1, sn = s0 + NI < nit ? s0 + NI : s0, sn1 = sn + 1 < nit ? sn + 1 : sn;
+            win_load(sn, 0);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
+            if constexpr (PAIR && WR2) win_load(sn1, 1);
+            b_load(sn);
+            iter(buf, s0, 0);
+            // the other buffers were last read before the previous barrier
+            win_store(buf ^ 1, 0, 0);
+            if constexpr (PAIR && !WR2) win_load(sn1, 0);  // (one register set: the second window after the first's store)
+            if constexpr (PAIR) {
+                if (s0 + 1 < nit) iter(buf, s0 + 1, 1);  // (block-uniform)
+                win_store(buf ^ 1, WR2 ? 1 : 0, 1);
+            }
+            b_store(buf ^ 1);
+            __syncthreads();
+            const int s = s0 + NI - 1;  // the barrier's last iteration
+            if ((s & 1) || s + 1 >= nit) {  // close the accumulation chain every two iterations (128 k)
+    #pragma unroll
+                for (int i = 0; i < 2; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] += t[i][j];
+    #pragma unroll
+                        for (int r = 0; r < 16; ++r) t[i][j][r] = 0.f;
+                    }
+            }
         }
     }
 

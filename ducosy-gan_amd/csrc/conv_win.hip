@@ -37,6 +37,11 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef DCS_WGRAD16  // f16x3 residual weight gradient on the 16x16x32 kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WGRAD16 1
 #endif
+#ifndef DCS_WGRAD16_F16  // the f16 mode's residual weight gradient on it too (NP 1, two rows per barrier): bit-compatible
+                         // with the tests' bounds but 1-2 % slower per launch than wgrad3_win_h3_kernel<1> (kbench
+                         // profiles/r06/ab/r06ai_kb_*), neutral in the step; off
+#define DCS_WGRAD16_F16 0
+#endif
 #ifndef DCS_WIN16  // f16x3 residual convs on the 16x16x32 window kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WIN16 1
 #endif
@@ -1659,6 +1664,9 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 // of a 32-lane read group (rows r .. r + 3 and r + 8 .. r + 11) over all 64 banks at any tap offset;
 // the unit index's bit 1 is the 16-channel sub-block, so the second sub-block's fragment is the first
 // one's offset XOR 16 halves.
+// f16 (NP 1, hi planes only): a row is a third of the MFMAs, so two rows run per barrier (as
+// wgrad3_win_h3_kernel<1>): a ring of 8 source rows and 4 dy buffers, the next two rows' loads issued at
+// the barrier and staged in six pieces through the second row, so they have a row and a half to land.
 __device__ __forceinline__ int ww16_swz(int pix) { return (((pix >> 1) & 1) << 2) | (((pix >> 3) & 1) << 1); }
 
 __device__ __forceinline__ f16x8 ww16_frag(const _Float16* p1, const _Float16* p2) {
@@ -1667,14 +1675,20 @@ __device__ __forceinline__ f16x8 ww16_frag(const _Float16* p1, const _Float16* p
     return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+template <int NP>
 __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const float* __restrict__ dy,
                                                                 const float* __restrict__ src,
                                                                 const float* __restrict__ rnga,
                                                                 const float* __restrict__ rngb,
                                                                 float* __restrict__ ws) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * WW_XROW + 2 * WW_DROW];
-    _Float16* const Xr = smem;                 // [4 slots][2 planes][66][64]
-    _Float16* const Dy = smem + 4 * WW_XROW;   // [2 buffers][2 planes][64][64]
+    constexpr int RPB = NP == 3 ? 1 : 2;  // image rows per barrier
+    constexpr int NXS = NP == 3 ? 4 : 8;  // source-row ring slots
+    constexpr int NDB = NP == 3 ? 2 : 4;  // dy buffers
+    constexpr int XROW = NP == 3 ? WW_XROW : WW_WP * 64;
+    constexpr int DROW = NP == 3 ? WW_DROW : WW_SW * 64;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[NXS * XROW + NDB * DROW];
+    _Float16* const Xr = smem;                 // [NXS slots][planes][66][64]
+    _Float16* const Dy = smem + NXS * XROW;    // [NDB buffers][planes][64][64]
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int ntile = a.gco * a.gci;
@@ -1719,15 +1733,16 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
             xls[q] = wc * 64 + 8 * (cu ^ ww16_swz(wc));
         }
     }
-    float4 dr[2], xr[WW_XU][2];
-    auto ld_dy = [&](int y) {
+    // register sets i of the rows in flight (RPB of each)
+    float4 dr[RPB][2], xr[RPB][WW_XU][2];
+    auto ld_dy = [&](int y, int i) {
         const int rb = ((n * H + y) * W) * Co * 4;
         u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff, 0, 0);
         u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff + 16, 0, 0);
-        __builtin_memcpy(&dr[0], &v0, 16);
-        __builtin_memcpy(&dr[1], &v1, 16);
+        __builtin_memcpy(&dr[i][0], &v0, 16);
+        __builtin_memcpy(&dr[i][1], &v1, 16);
     };
-    auto ld_x = [&](int r) {  // logical source row r in [-1, H]
+    auto ld_x = [&](int r, int i) {  // logical source row r in [-1, H]
         int sy = r;
         bool ok = true;
         if (a.reflect) sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
@@ -1738,32 +1753,38 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
             const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
-            __builtin_memcpy(&xr[q][0], &v0, 16);
-            __builtin_memcpy(&xr[q][1], &v1, 16);
+            __builtin_memcpy(&xr[i][q][0], &v0, 16);
+            __builtin_memcpy(&xr[i][q][1], &v1, 16);
         }
     };
-    auto st_dy = [&](int buf) {
+    auto st_dy = [&](int buf, int i) {
         f16x8 hi, lo;
-        split8h(dr[0], dr[1], asc, hi, lo);
-        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + dls) = hi;
-        *reinterpret_cast<f16x8*>(Dy + buf * WW_DROW + WW_SW * 64 + dls) = lo;
+        split8h(dr[i][0], dr[i][1], asc, hi, lo);
+        *reinterpret_cast<f16x8*>(Dy + buf * DROW + dls) = hi;
+        if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * DROW + WW_SW * 64 + dls) = lo;
     };
-    auto st_xq = [&](int slot, int q) {
+    auto st_xq = [&](int slot, int q, int i) {
         if (q == 0 || xls[q] >= 0) {  // (unit 0 covers pixels 0..63 of the 66: always inside)
             f16x8 hi, lo;
-            split8h(xr[q][0], xr[q][1], bsc, hi, lo);
-            *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + xls[q]) = hi;
-            *reinterpret_cast<f16x8*>(Xr + slot * WW_XROW + WW_WP * 64 + xls[q]) = lo;
+            split8h(xr[i][q][0], xr[i][q][1], bsc, hi, lo);
+            *reinterpret_cast<f16x8*>(Xr + slot * XROW + xls[q]) = hi;
+            if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * XROW + WW_WP * 64 + xls[q]) = lo;
         }
     };
-    auto st_x = [&](int slot) {
+    auto st_x = [&](int slot, int i) {
 #pragma unroll
-        for (int q = 0; q < WW_XU; ++q) st_xq(slot, q);
+        for (int q = 0; q < WW_XU; ++q) st_xq(slot, q, i);
     };
-    // staging piece p of the rows loaded for the next barrier (p 0: the dy row, 1 / 2: source units 0 / 1)
+    // staging piece p of the rows loaded for the next barrier, y = this barrier's first row (f16x3, p 0..2:
+    // the dy row, source units 0 / 1; f16, p 0..5: dy rows y + 2, y + 3, then source rows y + 3, y + 4 by unit)
     auto st_piece = [&](int p, int y) {
-        if (p == 0) st_dy((y + 1) & 1);
-        else st_xq((y + 2) & 3, p - 1);
+        if constexpr (NP == 3) {
+            if (p == 0) st_dy((y + 1) & 1, 0);
+            else st_xq((y + 2) & 3, p - 1, 0);
+        } else {
+            if (p < 2) st_dy((y + 2 + p) & (NDB - 1), p);
+            else st_xq((y + 3 + ((p - 2) >> 1)) & (NXS - 1), (p - 2) & 1, (p - 2) >> 1);
+        }
     };
 
     // transposed-read lane offsets (halves) of k-step 0 and the first sub-block: A (dy) at pixel row
@@ -1787,44 +1808,53 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
 #pragma unroll
     for (int i = 0; i < 18; ++i) { acc[i] = f32x4v{0.f, 0.f, 0.f, 0.f}; t[i] = f32x4v{0.f, 0.f, 0.f, 0.f}; }
 
-    // prologue: source rows y_beg - 1 .. y_beg + 1 into their ring slots, dy row y_beg; every row's loads
-    // (and the exponents') in flight before the first store
+    // prologue: source rows y_beg - 1 .. y_beg + RPB into their ring slots, dy rows y_beg .. y_beg + RPB - 1;
+    // every row's loads (and the exponents') in flight before the first store
     {
-        float4 px_[3][WW_XU][2], pd_[2];
+        float4 px_[RPB + 2][WW_XU][2], pd_[RPB][2];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < RPB + 2; ++i) {
             const int r = y_beg - 1 + i;
-            ld_x(r <= H ? r : H);
+            ld_x(r <= H ? r : H, 0);
 #pragma unroll
-            for (int u = 0; u < WW_XU; ++u) { px_[i][u][0] = xr[u][0]; px_[i][u][1] = xr[u][1]; }
+            for (int u = 0; u < WW_XU; ++u) { px_[i][u][0] = xr[0][u][0]; px_[i][u][1] = xr[0][u][1]; }
         }
-        ld_dy(y_beg);
-        pd_[0] = dr[0];
-        pd_[1] = dr[1];
+#pragma unroll
+        for (int i = 0; i < RPB; ++i) {
+            const int r = y_beg + i;
+            ld_dy(r < y_end ? r : y_end - 1, 0);
+            pd_[i][0] = dr[0][0];
+            pd_[i][1] = dr[0][1];
+        }
         ea = f16x3_exp(rnga, a.rng_a_n);
         eb = f16x3_exp(rngb, a.rng_b_n);
         asc = __builtin_ldexpf(1.f, ea);
         bsc = __builtin_ldexpf(1.f, eb);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < RPB + 2; ++i) {
 #pragma unroll
-            for (int u = 0; u < WW_XU; ++u) { xr[u][0] = px_[i][u][0]; xr[u][1] = px_[i][u][1]; }
-            st_x((y_beg - 1 + i) & 3);
+            for (int u = 0; u < WW_XU; ++u) { xr[0][u][0] = px_[i][u][0]; xr[0][u][1] = px_[i][u][1]; }
+            st_x((y_beg - 1 + i) & (NXS - 1), 0);
         }
-        dr[0] = pd_[0];
-        dr[1] = pd_[1];
-        st_dy(y_beg & 1);
+#pragma unroll
+        for (int i = 0; i < RPB; ++i) {
+            dr[0][0] = pd_[i][0];
+            dr[0][1] = pd_[i][1];
+            st_dy((y_beg + i) & (NDB - 1), 0);
+        }
     }
     __syncthreads();
 
     // one row: two k-steps of 32 pixels; per k-step the A fragments of both co sub-blocks, then the
     // wave's five taps with the next tap's B fragments read ahead of the current one's MFMAs
-    auto row = [&](int y, auto tag) {
+    // (S: the second row of an f16 barrier, which stages the next barrier's rows)
+    auto row = [&](int y, auto tag, auto stag) {
         constexpr int R = decltype(tag)::value;
-        const _Float16* const Db = Dy + (y & 1) * WW_DROW;
+        constexpr bool S = decltype(stag)::value;
+        const _Float16* const Db = Dy + (y & (NDB - 1)) * DROW;
         const _Float16* Xs[3];
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + 3 + ty) & 3) * WW_XROW;  // row y - 1 + ty
+        for (int ty = 0; ty < 3; ++ty) Xs[ty] = Xr + ((y + NXS - 1 + ty) & (NXS - 1)) * XROW;  // row y - 1 + ty
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             f16x8 ah[2], al[2];
@@ -1832,7 +1862,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
             for (int cs = 0; cs < 2; ++cs) {
                 const int o = (aoff ^ (16 * cs)) + kk * 32 * 64;
                 ah[cs] = ww16_frag(Db + o, Db + o + 4 * 64);
-                al[cs] = ww16_frag(Db + WW_SW * 64 + o, Db + WW_SW * 64 + o + 4 * 64);
+                if constexpr (NP == 3) al[cs] = ww16_frag(Db + WW_SW * 64 + o, Db + WW_SW * 64 + o + 4 * 64);
             }
             // (tap, ci sub-block) pairs of the wave: the next pair's B fragments read ahead of this one's MFMAs
             f16x8 bh[2], bl[2];
@@ -1842,7 +1872,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
                 const int ty = tap / 3, tx = tap % 3;
                 const int o1 = (boff1[tx] ^ (16 * ns)) + kk * 32 * 64, o2 = (boff2[tx] ^ (16 * ns)) + kk * 32 * 64;
                 bh[slot] = ww16_frag(Xs[ty] + o1, Xs[ty] + o2);
-                bl[slot] = ww16_frag(Xs[ty] + WW_WP * 64 + o1, Xs[ty] + WW_WP * 64 + o2);
+                if constexpr (NP == 3) bl[slot] = ww16_frag(Xs[ty] + WW_WP * 64 + o1, Xs[ty] + WW_WP * 64 + o2);
             };
             rd_b(0, 0);
 #pragma unroll
@@ -1854,14 +1884,17 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
                 // requested by sched_group_barrier; 4: the next row's loads issued right after the last piece,
                 // in flight across the barrier); 3: iterations 3, 5, 7
                 const int p0 = DCS_WW_STAGE == 3 ? 3 : 1;
-                const bool piece_here = DCS_WW_STAGE != 0 && (jp == p0 || jp == p0 + 2 || jp == p0 + 4);
+                const bool piece_here = NP == 3 && DCS_WW_STAGE != 0 && (jp == p0 || jp == p0 + 2 || jp == p0 + 4);
                 if (piece_here) {
                     if (kk == 1) st_piece((jp - p0) >> 1, y);
                 }
-                if (DCS_WW_STAGE == 4 && kk == 1 && jp == 5 && y + 1 < y_end) {  // (block-uniform)
-                    ld_dy(y + 2 < y_end ? y + 2 : y + 1);
-                    ld_x(y + 3 <= H ? y + 3 : H);
+                if (NP == 3 && DCS_WW_STAGE == 4 && kk == 1 && jp == 5 && y + 1 < y_end) {  // (block-uniform)
+                    ld_dy(y + 2 < y_end ? y + 2 : y + 1, 0);
+                    ld_x(y + 3 <= H ? y + 3 : H, 0);
                 }
+                // f16: pieces 0..2 in the first k-step's pair iterations 3, 5, 7, pieces 3..5 in the second's 1, 3, 5
+                if (S && ((kk == 0 && (jp == 3 || jp == 5 || jp == 7)) || (kk == 1 && (jp == 1 || jp == 3 || jp == 5))))
+                    st_piece(kk == 0 ? (jp - 3) >> 1 : 3 + ((jp - 1) >> 1), y - 1);
                 const int tt = jp >> 1, ns = jp & 1;
                 const int tap = R == 0 ? tt : (tt < 4 ? 5 + tt : 4);
                 const int sl = jp & 1;
@@ -1869,9 +1902,13 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
                 for (int cs = 0; cs < 2; ++cs) {
                     if (tap == 4 && cs != R) continue;  // tap 4: co sub-block R only
                     const int idx = tap == 4 ? 16 + ns : (R == 0 ? tap : tap - 5) * 4 + cs * 2 + ns;
-                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cs], bh[sl], t[idx], 0, 0, 0);
-                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bl[sl], t[idx], 0, 0, 0);
-                    t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bh[sl], t[idx], 0, 0, 0);
+                    if constexpr (NP == 3) {
+                        t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cs], bh[sl], t[idx], 0, 0, 0);
+                        t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bl[sl], t[idx], 0, 0, 0);
+                        t[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bh[sl], t[idx], 0, 0, 0);
+                    } else {  // (one level: the fp16 operands' rounding dwarfs the fp32 sum's)
+                        acc[idx] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cs], bh[sl], acc[idx], 0, 0, 0);
+                    }
                 }
                 if (piece_here && DCS_WW_STAGE == 2) {
                     if (kk == 1) {
@@ -1884,31 +1921,54 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win16_kernel(WWArgs a, const 
                     }
                 }
             }
-            if (DCS_WW_STAGE == 0 && kk == 0) {  // stage the rows loaded for the next barrier (buffers no row of this one reads)
+            if (NP == 3 && DCS_WW_STAGE == 0 && kk == 0) {  // stage the rows loaded for the next barrier (buffers no row of this one reads)
                 __builtin_amdgcn_sched_barrier(0);
-                st_dy((y + 1) & 1);
-                st_x((y + 2) & 3);
+                st_dy((y + 1) & 1, 0);
+                st_x((y + 2) & 3, 0);
             }
         }
     };
 
+    using F_ = std::false_type;
+    using T_ = std::true_type;
+    using R0_ = std::integral_constant<int, 0>;
+    using R1_ = std::integral_constant<int, 1>;
+    if constexpr (NP == 3) {
 #pragma unroll 1
-    for (int y = y_beg; y < y_end; ++y) {
-        if (DCS_WW_STAGE != 4 || y == y_beg) {  // (DCS_WW_STAGE 4: issued by the previous row)
-            ld_dy(y + 1 < y_end ? y + 1 : y);
-            ld_x(y + 2 <= H ? y + 2 : H);
-        }
-        if (half == 0) row(y, std::integral_constant<int, 0>{});
-        else row(y, std::integral_constant<int, 1>{});
-        if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {  // chains of two rows (128 pixels)
-#pragma unroll
-            for (int i = 0; i < 18; ++i) {
-                acc[i] += t[i];
-                asm volatile("" : "+v"(acc[i]));  // (pinned: see conv3_win16_kernel)
-                t[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        for (int y = y_beg; y < y_end; ++y) {
+            if (DCS_WW_STAGE != 4 || y == y_beg) {  // (DCS_WW_STAGE 4: issued by the previous row)
+                ld_dy(y + 1 < y_end ? y + 1 : y, 0);
+                ld_x(y + 2 <= H ? y + 2 : H, 0);
             }
+            if (half == 0) row(y, R0_{}, F_{});
+            else row(y, R1_{}, F_{});
+            if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {  // chains of two rows (128 pixels)
+#pragma unroll
+                for (int i = 0; i < 18; ++i) {
+                    acc[i] += t[i];
+                    asm volatile("" : "+v"(acc[i]));  // (pinned: see conv3_win16_kernel)
+                    t[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
+    } else {
+#pragma unroll 1
+        for (int y = y_beg; y < y_end; y += 2) {
+            // the next barrier's rows in flight (clamped past the chunk, reflected / zero past the image),
+            // staged by the second row into buffers no row of this barrier reads
+            ld_dy(y + 2 < y_end ? y + 2 : y_end - 1, 0);
+            ld_dy(y + 3 < y_end ? y + 3 : y_end - 1, 1);
+            ld_x(y + 3 <= H ? y + 3 : H, 0);
+            ld_x(y + 4 <= H ? y + 4 : H, 1);
+            if (half == 0) row(y, R0_{}, F_{});
+            else row(y, R1_{}, F_{});
+            if (y + 1 < y_end) {  // (block-uniform; otherwise no later barrier reads the staged rows)
+                if (half == 0) row(y + 1, R0_{}, T_{});
+                else row(y + 1, R1_{}, T_{});
+            }
+            __syncthreads();
+        }
     }
 
     // epilogue: undo the operand scales, slab [split][co][tap * C + ci]; lane holds rows 4 g + r (co)
@@ -2192,10 +2252,12 @@ int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, fl
     a.gco = d.Co / 64; a.gci = d.Cs / 64;
     a.rng_a_n = d.rng_a_n; a.rng_b_n = d.rng_b_n;
     const unsigned blocks = (unsigned)((long long)p.nsplit * a.gco * a.gci);
-    if (d.mma == DCS_MMA_F16)
+    if (d.mma == DCS_MMA_F16 && DCS_WGRAD16_F16)
+        hipLaunchKernelGGL(wgrad3_win16_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+    else if (d.mma == DCS_MMA_F16)
         hipLaunchKernelGGL(wgrad3_win_h3_kernel<1>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
     else if (DCS_WGRAD16)
-        hipLaunchKernelGGL(wgrad3_win16_kernel, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
+        hipLaunchKernelGGL(wgrad3_win16_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
     else
         hipLaunchKernelGGL(wgrad3_win_h3_kernel<3>, dim3(blocks), dim3(WW_NT), 0, s, a, dy, x, d.rng_a, d.rng_b, ws);
     const int e = check_launch("wgrad3_win");

@@ -55,10 +55,12 @@ _WIN = True
 # pair at 0.60 of its bar, the 512 x 512 pair within 1.4e-4 / 3.7e-3 of f16x3; scripts/diag/f16_layers.py,
 # profiles/r06/ab/r06ab_*), f16 step 138.7 -> 133.5 ms same box
 _PHASE_F16X3 = frozenset()
-# the Generator's stem and head kernels on f16x3 operands in both fp16 modes ("stem": forward, "stem_wgrad",
+# the Generator's stem and head kernels kept on f16x3 operands in the fp16 mode ("stem": forward, "stem_wgrad",
 # "head": forward, data and weight gradient); a layer left out runs in the step's mode (env DUCOSY_F16X3_LAYERS:
-# a comma-separated list in place of the default)
-_FIXED_F16X3 = frozenset(x for x in os.environ.get("DUCOSY_F16X3_LAYERS", "stem,stem_wgrad,head").split(",") if x)
+# a comma-separated list in place of the default).  Empty since round 6: with every layer on fp16 the steps_64
+# fixture pair holds 0.74 of its bar (0.67 with the three kept; scripts/diag/f16_layers.py --fixed), f16 step
+# 131.3 -> 130.3 ms same box (profiles/r06/ab/r06ai_*)
+_FIXED_F16X3 = frozenset(x for x in os.environ.get("DUCOSY_F16X3_LAYERS", "").split(",") if x)
 
 
 def _fixed_mma(layer: str) -> int:
@@ -704,7 +706,7 @@ class ConvGeom:
         """The Generator stem (7x7 reflect-pad-3, NHWC x 4 source -> 64) on its MFMA kernel
         (csrc/conv_stem.hip), with the IN statistics of its output when ``stats``."""
         dev = s.t.device
-        d.mma = _fixed_mma("stem")  # (f16x3 in both fp16 modes: the layer is small, and its error feeds every later one)
+        d.mma = _fixed_mma("stem")
         out = torch.empty(s.N, s.H, s.W, self.cout, device=dev, dtype=torch.float32)
         parts = workspace(lib.query("dcs_stem_fwd_parts_size", ctypes.byref(d)), dev) if stats else None
         nchunk = ctypes.c_int(0)
@@ -817,7 +819,7 @@ class ConvGeom:
         d = self._desc_fwd(s, wpack.shape[1], pro_act, epi_act)
         out = torch.empty(s.N, Ho, Wo, self.cout, device=s.t.device, dtype=torch.float32)
         if self.narrow and _HEAD_PROJ and pro is not None and pro_max is not None and _h3() and s.t2 is None:
-            d.mma = _fixed_mma("head")  # (f16x3 in both fp16 modes: its share of the step is small)
+            d.mma = _fixed_mma("head")
             if lib.query("dcs_head_fwd_proj_ok", ctypes.byref(d)):
                 lib.call("dcs_head_fwd_proj", ctypes.byref(d), _p(s.t), _p(wpack), _p(bias), _p(pro[0]), _p(pro[1]),
                          _p(pro_max), _p(out), _stream())

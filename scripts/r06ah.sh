@@ -1,0 +1,26 @@
+# f16 mode residual weight gradient: wgrad3_win_h3_kernel<1> (w0) vs wgrad3_win16_kernel<1>, two rows per barrier (w16)
+# then the stem / head kernels on fp16 operands in the f16 mode (DUCOSY_F16X3_LAYERS): fixture diag + bench
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+L=$R/ducosy-gan_amd/lib
+DUCOSY_HIP_LIB=$L/libducosy_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_win.py -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r06ah_tests.log 2>&1 || { echo TESTFAIL; grep -E "^E  |FAILED" gpurun_out/r06ah_tests.log | head; exit 1; }
+tail -1 gpurun_out/r06ah_tests.log
+for it in 1 2; do
+  for v in w0 w16; do
+    lib=$L/libducosy_hip_$v.so; [ "$v" = w16 ] && lib=$L/libducosy_hip.so
+    DUCOSY_HIP_LIB=$lib timeout -k 10 200 python -u scripts/kbench.py --mma f16 --batch 16 --reps 20 --only res > gpurun_out/r06ah_kb_${v}_$it.log 2>&1 || { echo "KB $v FAILED"; exit 1; }
+    echo "$v/$it: $(grep -E '^res' gpurun_out/r06ah_kb_${v}_$it.log | awk '{printf "%s %s  ", $2, $3}')"
+    DUCOSY_HIP_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --mma f16 > gpurun_out/r06ah_f16_${v}_$it.log 2>&1 || exit 1
+    echo "f16 $v/$it: $(tail -1 gpurun_out/r06ah_f16_${v}_$it.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["frac"], d["roofline"]["ms_per_launch"], d["finite"])')"
+  done
+done
+timeout -k 10 300 python -u scripts/diag/f16_layers.py --fixed > gpurun_out/r06ah_fixed.log 2>&1 || { echo DIAG FAILED; tail -5 gpurun_out/r06ah_fixed.log; exit 1; }
+grep f16x3 gpurun_out/r06ah_fixed.log
+for it in 1 2; do
+  for v in fx nofx; do
+    fx="stem,stem_wgrad,head"; [ "$v" = nofx ] && fx=""
+    DUCOSY_F16X3_LAYERS=$fx timeout -k 10 200 python bench.py --no-cpu-baseline --mma f16 > gpurun_out/r06ah_f16${v}_$it.log 2>&1 || exit 1
+    echo "f16 $v/$it: $(tail -1 gpurun_out/r06ah_f16${v}_$it.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["frac"], d["finite"])')"
+  done
+done

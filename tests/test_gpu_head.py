@@ -3,7 +3,7 @@ operand modes): out = tanh(b + conv7x7(ReflectionPad2d(3)(relu(IN(y))))) (module
 against float64 on the same fp32 activation and weights, and against the exact-f32 VALU kernel it
 replaces (conv_narrow.hip).  f16x3: max |err| / max |ref| <= 2e-6 before the tanh (the f32 kernel's
 own error is ~1e-6: both sum 3136 products in fp32).  The f16 mode (config 5) runs these kernels
-on f16x3 operands too (ops.py: the head's share of the step is small), so its 3e-3 bar is loose."""
+on fp16 operands since round 6 (ops._FIXED_F16X3 empty): fp16-class bars (3e-3, 5e-3)."""
 import pytest
 import torch
 import torch.nn.functional as F

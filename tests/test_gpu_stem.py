@@ -2,7 +2,7 @@
 ReflectionPad2d(3) + Conv2d(cin, 64, 7) over the packed image and mask planes (modules/model.py:96-98)
 and the InstanceNorm statistics of its output, against float64 on the same inputs, and against the
 generic rows pass it replaces.  f16x3: output max |err| / max |ref| <= 2e-6, IN scale / shift within
-1e-5; f16: 3e-3 / 3e-3 (the f16 mode runs the stem kernels on f16x3 operands too, ops.py)."""
+1e-5; f16: 3e-3 / 3e-3 (the f16 mode runs the stem kernels on fp16 operands since round 6, ops._FIXED_F16X3)."""
 import pytest
 import torch
 import torch.nn.functional as F

@@ -5,9 +5,10 @@ the same fp32 operands:
     epilogue partials) for up1 (256 -> 128) and up2 (128 -> 64) shapes, source widths 16 .. 256
     (every tile width the kernel takes: 16, 32, 64, 128 and two column strips);
   * the fp32-class bound of the rows pass it replaces (max error / max |ref| <= 1e-5) in f16x3 mode;
-    in f16 mode the up-convs and PatchGAN layers stay on f16x3 operands (with fp16 the config-5
-    fixture's f16 step misses its bar, profiles/r04ah), the down-convs and every weight gradient
-    run on fp16 operands (2e-3);
+    in f16 mode every layer runs on fp16 operands since round 6 (ops._PHASE_F16X3 empty; a layer kept
+    there takes f16x3 and the 1e-5 bound): 2e-3 against the fp32 operands; the PatchGAN layer (whose
+    phase classes split the taps, so its fp16 operands are the taps rounded) also within 1e-4 / 2e-5
+    of float64 of the operands rounded to fp16 (the up-convs' phase weights are tap sums rounded once);
   * the data gradient (per phase a 2x2 conv of dy's phase sub-grid with the transposed phase weights)
     against float64 autograd of upsample + conv, to the same bound;
   * the weight gradient (phase weight gradients on a rolling source window, folded onto the 3x3 taps)
@@ -48,13 +49,26 @@ def _geom(ops, cin, cout):
     return ops.ConvGeom(cin, cout, 3, 1, (1, 1, 1, 1), DCS_PAD_ZERO, up=2)
 
 
-@pytest.mark.parametrize("mode,tol", [("f16x3", 1e-5), ("f16", 1e-5)])
+def _fp16_ops(ops, g, mode):
+    """True when the layer's phase kernels take fp16 operands (f16 mode, not in ops._PHASE_F16X3)."""
+    return mode == "f16" and g._phase_tag() not in ops._PHASE_F16X3
+
+
+def _h(t):
+    """float64 of t's values rounded to fp16 (the f16 path's operands)."""
+    return t.detach().half().double()
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "f16"])
 @pytest.mark.parametrize("cin,cout,N,H,W", [(256, 128, 2, 16, 16), (256, 128, 1, 8, 32), (128, 64, 2, 8, 64),
-                                            (128, 64, 1, 4, 128), (128, 64, 1, 2, 256)])
-def test_subpix_forward_and_stats_vs_fp64(ops, mode, tol, cin, cout, N, H, W):
+                                            (128, 64, 1, 4, 128), (128, 64, 1, 2, 256), (96, 64, 1, 8, 32)])
+def test_subpix_forward_and_stats_vs_fp64(ops, mode, cin, cout, N, H, W):
+    """(cin 96: an odd count of 16-channel slices, the f16 kernel's last barrier with one iteration.)"""
     ops.set_mma(mode)
     g = _geom(ops, cin, cout)
     assert g.subwin
+    f16 = _fp16_ops(ops, g, mode)
+    tol = 2e-3 if f16 else 1e-5
     x = rnd((N, cin, H, W), 81, "x").double()
     w = torch.from_numpy(prng.normal(82, "w", (cout, cin, 3, 3), 0, 0.05)).float().double()
     ref = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, padding=1)
@@ -103,7 +117,7 @@ def test_subpix_dgrad_vs_fp64(ops, mode, cin, cout, N, H, W):
     wd = g.pack_dgrad(w.float().to(DEV))
     assert getattr(wd, "_dcs_sp", None) is not None
     dx = g.dgrad(dyd, wd, H, W)
-    assert _relmax(dx.permute(0, 3, 1, 2), ref) <= 1e-5
+    assert _relmax(dx.permute(0, 3, 1, 2), ref) <= (2e-3 if _fp16_ops(ops, g, mode) else 1e-5)
     assert torch.equal(g.dgrad(dyd, wd, H, W), dx)  # deterministic
     sp = wd._dcs_sp
     del wd._dcs_sp
@@ -199,9 +213,14 @@ def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
     pro = (sc.float().to(DEV).contiguous(), sh.float().to(DEV).contiguous(), ACT_LRELU)
     wp, wd = g.pack_fwd(w.float().to(DEV)), g.pack_dgrad(w.float().to(DEV))
     assert getattr(wp, "_dcs_sp", None) is not None and getattr(wd, "_dcs_sp", None) is not None
-    tol = 1e-5  # f16x3 operands in both fp16 modes
+    f16 = _fp16_ops(ops, g, mode)
+    tol = 2e-3 if f16 else 1e-5
     out, st = g.forward_in_stats(ops.Src.nhwc(yd), wp, pro=pro)
     assert _relmax(out.permute(0, 3, 1, 2), ref) <= tol
+    if f16:  # the prologue's activation rounded to fp16 (fp32 vs float64 activation: an ulp apart at most)
+        ref16 = F.conv2d(_h(a.float()), _h(w), stride=2, padding=1)
+        assert _relmax(out.permute(0, 3, 1, 2), ref16) <= 1e-4
+        (dref16,) = torch.autograd.grad(F.conv2d(a, _h(w), stride=2, padding=1), a, _h(dy))
     rstd = 1.0 / torch.sqrt(var + 1e-5)
     assert _relmax(st.scale, rstd) <= tol
     assert float((st.shift.double().cpu() + mean * rstd).abs().max()) <= tol * float((mean * rstd).abs().max() + 1)
@@ -209,6 +228,8 @@ def test_patchgan_layer_vs_fp64(ops, mode, cin, cout, N, H, W):
     dyd = dy.float().to(DEV).permute(0, 2, 3, 1).contiguous()
     dx = g.dgrad(dyd, wd, H, W)
     assert _relmax(dx.permute(0, 3, 1, 2), dref) <= tol
+    if f16:
+        assert _relmax(dx.permute(0, 3, 1, 2), dref16) <= 2e-5
     rows_tol = 1e-5 if mode == "f16x3" else 2e-3
     for pk in (wp, wd):
         del pk._dcs_sp

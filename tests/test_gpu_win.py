@@ -174,6 +174,26 @@ def test_win_f16_mode_vs_fp64(ops, N, H, W):
         assert max(errs) <= tol, (mode, errs)
 
 
+@pytest.mark.parametrize("N,H,W", [(1, 18, 64), (2, 16, 64), (1, 20, 128), (1, 9, 64)])
+def test_win_wgrad_f16_vs_fp64(ops, N, H, W):
+    """The f16 mode's weight gradient (wgrad3_win16_kernel<1>: two image rows per barrier, the next
+    two staged through the second) over row chunks with an odd row count (H 18: two chunks of 9, H 9:
+    one) and several strips: within 3e-3 of float64 and bit-identical on a second run."""
+    g = _geom(ops)
+    x = rnd((N, 256, H, W), 121, "x").double()
+    w = torch.from_numpy(prng.normal(122, "w", (256, 256, 3, 3), 0, 0.05)).float().double().requires_grad_(True)
+    y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w)
+    R = torch.from_numpy(prng.normal(123, "R", tuple(y.shape))).float().double()
+    (y * R).sum().backward()
+    xd = x.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    Rd = R.float().to(DEV).permute(0, 2, 3, 1).contiguous()
+    ops.set_mma("f16")
+    dw = g.wgrad(Rd, ops.Src.nhwc(xd))
+    e = _relmax(dw, w.grad)
+    assert e <= 3e-3, e
+    assert torch.equal(dw, g.wgrad(Rd, ops.Src.nhwc(xd)))
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 16, 16), (1, 16, 128)])
 def test_win_dgrad_inbwd_matches_separate_pass(ops, N, H, W):
     """The InstanceNorm backward of a = relu(IN(y)) with its partial sums fused into the window data
