@@ -26,6 +26,13 @@
 #include "common.hpp"
 #include "conv_common.hpp"
 
+#ifndef DCS_SP_BDMA  // B slices by LDS-DMA (global_load_lds_dwordx4) instead of registers + ds_write, and idle window
+                     // units storing to a dummy slot so no load sinks into a branch: ~20 VGPRs fewer and every
+                     // load issued at the top of the slice, bit-identical, but no faster per launch (kbench) and
+                     // 0.5 % slower in the f16x3 step (profiles/r06/ab/r06ak_*): the phase kernels' 0.33 MFMA
+                     // busy is not the staging loads' latency; off
+#define DCS_SP_BDMA 0
+#endif
 #ifndef DCS_SP_PAIR  // f16: two k iterations per barrier in the window phase kernel's forward-type launches (the
                      // up-conv forward, the stride-2 forward and data gradient; 0: one, as f16x3): 3-7 % per launch,
                      // bit-identical; the up-conv data gradient measured 2-3 % slower with it and keeps one
@@ -60,6 +67,16 @@ struct PhIbw {
     Sum2* parts;  // [N][nchunk][Co]
     int act;
 };
+
+// one global_load_lds_dwordx4 (lane L's 16 bytes at LDS byte address lds + 16 L; inline asm as
+// conv_win.hip's win_glds: the kernel retires it with its own vmcnt wait before the publishing barrier)
+__device__ __forceinline__ void sp_glds(const void* base, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
+}
 
 // window: pixel pairs swap on odd groups of 8 pixels, 16-byte halves on odd groups of 16 (conflict-free
 // reads of every other pixel: the MFMA row blocks interleave, as conv_win.hip)
@@ -182,7 +199,10 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             const int u = tid + q * SP_NT;
             const int wpix = u >> 1, h = u & 1;
             float4 (&wr)[2] = wr_[p][q];
-            if (wpix < npix) {
+            // DCS_SP_BDMA: idle units store too, into the B tap slot's padding (never read): a store under a
+            // branch lets the compiler sink the unit's load into the branch, right before its wait
+            const bool live = wpix < npix;
+            if (DCS_SP_BDMA || live) {
                 if constexpr (PRO) {  // a = act(y * scale + shift) inside the image, 0 in the padding
                     const int c0 = (vit[p] % nslice) * 16 + 8 * h;
                     const float4 s0 = *reinterpret_cast<const float4*>(pro_s + c0);
@@ -198,8 +218,9 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                 }
                 f16x8 hi, lo;
                 split8h(wr[0], wr[1], asc, hi, lo);
-                *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, pl, wpix, h)) = hi;
-                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + sp_woff(buf, 1, wpix, h)) = lo;
+                constexpr int DUMMY = 2 * 2 * SP_PIX * 16 + 128 * 16;  // (buffer 0, plane 0, tap 0) padding row
+                *reinterpret_cast<f16x8*>(Wn + (live ? sp_woff(buf, pl, wpix, h) : DUMMY)) = hi;
+                if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Wn + (live ? sp_woff(buf, 1, wpix, h) : DUMMY)) = lo;
             }
         }
     };
@@ -241,6 +262,45 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             br[i] = __builtin_amdgcn_raw_buffer_load_b128(i < 2 ? bhr : blr, skip ? 0x7fffffbf : bg[i] + kb, 0, 0);
         }
     };
+    // DCS_SP_BDMA: the same slice as 1 KB blocks (plane, tap, 32-row block) by LDS-DMA, NBC per wave
+    // (block c = wave * NBC + i).  A block's LDS image is lane-linear (lane L -> row L / 2, half slot L % 2),
+    // so sp_boff's swizzle moves to the source: lane L fetches half (L % 2) ^ bit 3 of its row.  S2: the
+    // blocks of skipped (row half, tap) pairs are not fetched (wave-uniform; the MFMA loop never reads them)
+    constexpr bool BDMA = DCS_SP_BDMA;
+    const unsigned dlane = 2u * (unsigned)((n0 + (lane >> 1)) * K + 8 * ((lane & 1) ^ ((lane >> 4) & 1)));
+    unsigned dsu[NBC], ddst[NBC];
+    int dbt[NBC], dpl[NBC];
+    {
+        const unsigned bs_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) _Float16*)Bs;
+        const int w = __builtin_amdgcn_readfirstlane(wid);
+#pragma unroll
+        for (int i = 0; i < NBC; ++i) {
+            const int c = w * NBC + i, pl = c >> 4, tap = (c >> 2) & 3, rb = c & 3;
+            dsu[i] = 2u * (unsigned)(rb * 32 * K + tap * 16);
+            ddst[i] = __builtin_amdgcn_readfirstlane(bs_lds + 2u * (unsigned)((pl * 4 + tap) * SP_SLOT + rb * 32 * 16));
+            dbt[i] = tap | ((rb >> 1) << 2);  // as bt: tap (u, t) and the 64-row half
+            dpl[i] = pl;
+        }
+    }
+    auto b_dma = [&](int it0, int buf) {  // slice it0 (PAIR: and it0 + 1 in plane 1) into buffer buf
+#pragma unroll
+        for (int i = 0; i < NBC; ++i) {
+            const int it = PAIR && dpl[i] ? (it0 + 1 < nit ? it0 + 1 : it0) : it0;
+            bool skip = false;
+            if constexpr (S2) {
+                const int u = (dbt[i] >> 1) & 1, t = dbt[i] & 1;
+                if constexpr (MODE == 0) {
+                    skip = ((dbt[i] >> 2) == 0 && u == 0) || (PXC == 0 && t == 0);
+                } else {
+                    const int ph = it / nslice;
+                    skip = ((ph >> 1) == 0 && u == 1) || ((ph & 1) == 0 && t == 1);
+                }
+            }
+            if (!skip)
+                sp_glds(NP == 3 && dpl[i] ? wl : wh, dlane + (dsu[i] + 2u * (unsigned)(it * 64)),
+                        ddst[i] + 2u * (unsigned)(buf * 8 * SP_SLOT));
+        }
+    };
     auto b_store = [&](int buf) {
         const int boff = buf * 8 * SP_SLOT;
 #pragma unroll
@@ -270,7 +330,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     // first store
     win_load(0, 0);
     if constexpr (PAIR && WR2) win_load(nit > 1 ? 1 : 0, 1);
-    b_load(0);
+    if constexpr (BDMA) b_dma(0, 0);
+    else b_load(0);
     if constexpr (PRO) {  // the image's prologue scale / shift (published by the barrier below)
         for (int c = tid; c < C; c += SP_NT) {
             pro_s[c] = psc[(long long)n * C + c];
@@ -283,7 +344,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
     win_store(0, 0, 0);
     if constexpr (PAIR && !WR2) win_load(nit > 1 ? 1 : 0, 0);
     if constexpr (PAIR) win_store(0, WR2 ? 1 : 0, 1);
-    b_store(0);
+    if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else b_store(0);
     __syncthreads();
 
     f16x8 fh[3], fl[3];
@@ -341,7 +403,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
         for (int s = 0; s < nit; ++s) {
             const int buf = s & 1, sn = s + 1 < nit ? s + 1 : s;
             win_load(sn, 0);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
-            b_load(sn);
+            if constexpr (BDMA) b_dma(sn, buf ^ 1);
+            else b_load(sn);
     #pragma unroll
             for (int tap = 0; tap < 4; ++tap) {
                 const int u = tap >> 1, tx = tap & 1;
@@ -391,7 +454,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             }
             // the other buffers were last read before the previous barrier
             win_store(buf ^ 1, 0, 0);
-            b_store(buf ^ 1);
+            if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else b_store(buf ^ 1);
             __syncthreads();
             if ((s & 1) || s + 1 == nit) {  // close the accumulation chain every two iterations (128 k)
     #pragma unroll
@@ -409,7 +473,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
             const int buf = (s0 / NI) & 1, sn = s0 + NI < nit ? s0 + NI : s0, sn1 = sn + 1 < nit ? sn + 1 : sn;
             win_load(sn, 0);  // unconditional (clamped): a load under a branch would force vmcnt(0) below
             if constexpr (PAIR && WR2) win_load(sn1, 1);
-            b_load(sn);
+            if constexpr (BDMA) b_dma(sn, buf ^ 1);
+            else b_load(sn);
             iter(buf, s0, 0);
             // the other buffers were last read before the previous barrier
             win_store(buf ^ 1, 0, 0);
@@ -418,7 +483,8 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                 if (s0 + 1 < nit) iter(buf, s0 + 1, 1);  // (block-uniform)
                 win_store(buf ^ 1, WR2 ? 1 : 0, 1);
             }
-            b_store(buf ^ 1);
+            if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else b_store(buf ^ 1);
             __syncthreads();
             const int s = s0 + NI - 1;  // the barrier's last iteration
             if ((s & 1) || s + 1 >= nit) {  // close the accumulation chain every two iterations (128 k)
