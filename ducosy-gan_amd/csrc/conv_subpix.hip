@@ -33,9 +33,13 @@
                      // busy is not the staging loads' latency; off
 #define DCS_SP_BDMA 0
 #endif
-#ifndef DCS_SP_PAIR  // f16: two k iterations per barrier in the window phase kernel's forward-type launches (the
-                     // up-conv forward, the stride-2 forward and data gradient; 0: one, as f16x3): 3-7 % per launch,
-                     // bit-identical; the up-conv data gradient measured 2-3 % slower with it and keeps one
+#ifndef DCS_SP_PAIR_DG  // the up-conv data gradient paired too, with one window register set (two: 2-3 % slower):
+                        // up1 / up2 data gradient 0.239 / 0.264 -> 0.230 / 0.250 ms per launch, bit-identical, step
+                        // within noise (profiles/r06/ab/r06al_*)
+#define DCS_SP_PAIR_DG 1
+#endif
+#ifndef DCS_SP_PAIR  // f16: two k iterations per barrier in the window phase kernel (0: one, as f16x3): 3-7 % per
+                     // launch, bit-identical
 #define DCS_SP_PAIR 1
 #endif
 
@@ -103,13 +107,13 @@ __global__ __launch_bounds__(SP_NT, 1) void subpix_win_kernel(SubArgs a, const f
                                                               const int* __restrict__ wexp, float* __restrict__ out,
                                                               Part* __restrict__ parts, const float* __restrict__ psc,
                                                               const float* __restrict__ psh, PhIbw ib) {
-    // f16 (NP 1, DCS_SP_PAIR; not the up-conv data gradient): a slice is only 16 MFMAs per wave, so two
-    // iterations run per barrier, the second one's window and B in the planes f16x3 gives its lo halves
-    // (same sums in the same order)
-    // Two window register sets (both loads in flight from the barrier) where the registers allow; the
-    // stride-2 and prologue kernels reuse one (the second window loaded after the first one's store)
-    constexpr bool PAIR = NP == 1 && DCS_SP_PAIR && (MODE == 0 || S2);
-    constexpr bool WR2 = !S2 && !PRO;
+    // f16 (NP 1, DCS_SP_PAIR): a slice is only 16 MFMAs per wave, so two iterations run per barrier, the
+    // second one's window and B in the planes f16x3 gives its lo halves (same sums in the same order)
+    // Two window register sets (both loads in flight from the barrier) for the up-conv forward; the other
+    // launches reuse one (the second window loaded after the first one's store): two spill in the stride-2
+    // and prologue kernels and measured slower in the up-conv data gradient
+    constexpr bool PAIR = NP == 1 && DCS_SP_PAIR && (MODE == 0 || S2 || DCS_SP_PAIR_DG);
+    constexpr bool WR2 = !S2 && !PRO && MODE == 0;
     constexpr int NI = PAIR ? 2 : 1;  // iterations per barrier
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * SP_PIX * 16 + 2 * 2 * 4 * SP_SLOT];
     __shared__ __attribute__((aligned(16))) float pro_s[PRO ? 2 * SP_PROC : 4];  // [scale | shift][channel]
