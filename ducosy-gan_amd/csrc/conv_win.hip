@@ -37,6 +37,12 @@ __device__ unsigned long long g_win_t[16384 * 5];
 #ifndef DCS_WGRAD16  // f16x3 residual weight gradient on the 16x16x32 kernel (0: the 32x32x16 one; A/B builds)
 #define DCS_WGRAD16 1
 #endif
+#ifndef DCS_WW_F16_EARLY  // f16 weight gradient (wgrad3_win_h3_kernel<1>): both rows of the next barrier loaded at
+                          // its start and staged by its second row, one accumulation level (0: each row's loads
+                          // issued at its start and staged at its end).  1.5 % slower per launch, 0.2 % in the
+                          // step (profiles/r06/ab/r06an_*): not the loads' latency; off
+#define DCS_WW_F16_EARLY 0
+#endif
 #ifndef DCS_WGRAD16_F16  // the f16 mode's residual weight gradient on it too (NP 1, two rows per barrier): bit-compatible
                          // with the tests' bounds but 1-2 % slower per launch than wgrad3_win_h3_kernel<1> (kbench
                          // profiles/r06/ab/r06ai_kb_*), neutral in the step; off
@@ -1423,15 +1429,20 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             xls[q] = wc * 64 + 8 * (cu ^ ww_swz(wc));
         }
     }
-    float4 dr[2], xr[WW_XU][2];
-    auto ld_dy = [&](int y) {
+    // register sets of the rows in flight (DCS_WW_F16_EARLY, f16: both rows of the next barrier)
+    constexpr bool EARLY = NP == 1 && DCS_WW_F16_EARLY;
+    constexpr int NSET = EARLY ? 2 : 1;
+    float4 dr_[NSET][2], xr_[NSET][WW_XU][2];
+    float4 (&dr)[2] = dr_[0];
+    float4 (&xr)[WW_XU][2] = xr_[0];
+    auto ld_dy = [&](int y, int set = 0) {
         const int rb = ((n * H + y) * W) * Co * 4;
         u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff, 0, 0);
         u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(drs, rb + doff + 16, 0, 0);
-        __builtin_memcpy(&dr[0], &v0, 16);
-        __builtin_memcpy(&dr[1], &v1, 16);
+        __builtin_memcpy(&dr_[set][0], &v0, 16);
+        __builtin_memcpy(&dr_[set][1], &v1, 16);
     };
-    auto ld_x = [&](int r) {  // logical source row r in [-1, H]
+    auto ld_x = [&](int r, int set = 0) {  // logical source row r in [-1, H]
         int sy = r;
         bool ok = true;
         if (a.reflect) sy = sy < 0 ? -sy : (sy >= H ? 2 * H - 2 - sy : sy);
@@ -1442,22 +1453,22 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             const int off = (ok && xoff[q] >= 0) ? rb + xoff[q] : OOB;
             u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
             u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0);
-            __builtin_memcpy(&xr[q][0], &v0, 16);
-            __builtin_memcpy(&xr[q][1], &v1, 16);
+            __builtin_memcpy(&xr_[set][q][0], &v0, 16);
+            __builtin_memcpy(&xr_[set][q][1], &v1, 16);
         }
     };
-    auto st_dy = [&](int buf) {
+    auto st_dy = [&](int buf, int set = 0) {
         f16x8 hi, lo;
-        split8h(dr[0], dr[1], asc, hi, lo);
+        split8h(dr_[set][0], dr_[set][1], asc, hi, lo);
         *reinterpret_cast<f16x8*>(Dy + buf * DROW + dls) = hi;
         if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Dy + buf * DROW + WW_SW * 64 + dls) = lo;
     };
-    auto st_x = [&](int slot) {
+    auto st_x = [&](int slot, int set = 0) {
 #pragma unroll
         for (int q = 0; q < WW_XU; ++q) {
             if (xls[q] >= 0) {
                 f16x8 hi, lo;
-                split8h(xr[q][0], xr[q][1], bsc, hi, lo);
+                split8h(xr_[set][q][0], xr_[set][q][1], bsc, hi, lo);
                 *reinterpret_cast<f16x8*>(Xr + slot * XROW + xls[q]) = hi;
                 if constexpr (NP == 3) *reinterpret_cast<f16x8*>(Xr + slot * XROW + WW_WP * 64 + xls[q]) = lo;
             }
@@ -1527,8 +1538,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 
     // one row of this wave's taps T0 .. T0 + NT_ - 1: 4 pixel sub-tiles x NT_ taps, the fragments of
     // the next (sub-tile, tap) read before the MFMAs of the current one
-    auto row = [&](int y, auto tag) {
+    // (S: EARLY, the barrier's second row, which stages both rows loaded at the barrier, y0 = its first row)
+    auto row = [&](int y, auto tag, auto stag) {
         constexpr int R = decltype(tag)::value;
+        constexpr bool S = decltype(stag)::value;
         constexpr int NJ = 18;  // (sub-tile, tap) pairs of this wave
         const _Float16* const Db = Dy + (y & (NDB - 1)) * DROW;
         const _Float16* Xs[3];
@@ -1552,7 +1565,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                 if (ww_k(R, j + 1) != ww_k(R, j)) rdA(ww_k(R, j + 1), nah, nal);
                 rdB(j + 1, nbh, nbl);
             }
-            floatx16& tt = t[ww_acc(R, ww_tap(R, j))];
+            floatx16& tt = EARLY ? acc[ww_acc(R, ww_tap(R, j))] : t[ww_acc(R, ww_tap(R, j))];
             if constexpr (NP == 3) {
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, tt, 0, 0, 0);
                 tt = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, tt, 0, 0, 0);
@@ -1561,9 +1574,14 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             // stage the rows loaded above into the buffers no row of this barrier reads: mid-row (f16x3),
             // or at the row's end (f16: a row holds a third of the MFMAs, half a row hid too little of
             // the loads' latency)
-            if (j == (NP == 1 ? NJ - 1 : NJ / 2 - 1)) {
+            if (!EARLY && j == (NP == 1 ? NJ - 1 : NJ / 2 - 1)) {
                 st_dy((y + RPB) & (NDB - 1));
                 st_x((y + RPB + 1) & (NXS - 1));
+            }
+            if (S && (j == NJ / 2 - 1 || j == NJ - 1)) {  // set 0 mid-row, set 1 at the end (y - 1: the first row)
+                const int set = j == NJ - 1 ? 1 : 0;
+                st_dy((y + 1 + set) & (NDB - 1), set);
+                st_x((y + 2 + set) & (NXS - 1), set);
             }
             bh = nbh;
             bl = nbl;
@@ -1580,8 +1598,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
             // next rows in flight (unconditional: clamped past the chunk, reflected / zero past the image)
             ld_dy(y + 1 < y_end ? y + 1 : y);
             ld_x(y + 2 <= H ? y + 2 : H);
-            if (half == 0) row(y, std::integral_constant<int, 0>{});
-            else row(y, std::integral_constant<int, 1>{});
+            if (half == 0) row(y, std::integral_constant<int, 0>{}, std::false_type{});
+            else row(y, std::integral_constant<int, 1>{}, std::false_type{});
             if (((y - y_beg) & 1) == 1 || y + 1 == y_end) {
 #pragma unroll
                 for (int i = 0; i < WW_TPW; ++i) {
@@ -1589,6 +1607,23 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
 #pragma unroll
                     for (int r = 0; r < 16; ++r) t[i][r] = 0.f;
                 }
+            }
+            __syncthreads();
+        }
+    } else if constexpr (EARLY) {
+        // both rows of the next barrier in flight from its start, staged by the second row (one accumulation
+        // level: the fp16 operands' rounding dwarfs the fp32 sum's)
+#pragma unroll 1
+        for (int y = y_beg; y < y_end; y += 2) {
+            ld_dy(y + 2 < y_end ? y + 2 : y_end - 1, 0);
+            ld_dy(y + 3 < y_end ? y + 3 : y_end - 1, 1);
+            ld_x(y + 3 <= H ? y + 3 : H, 0);
+            ld_x(y + 4 <= H ? y + 4 : H, 1);
+            if (half == 0) row(y, std::integral_constant<int, 0>{}, std::false_type{});
+            else row(y, std::integral_constant<int, 1>{}, std::false_type{});
+            if (y + 1 < y_end) {  // (block-uniform; otherwise no later barrier reads the staged rows)
+                if (half == 0) row(y + 1, std::integral_constant<int, 0>{}, std::true_type{});
+                else row(y + 1, std::integral_constant<int, 1>{}, std::true_type{});
             }
             __syncthreads();
         }
@@ -1602,8 +1637,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad3_win_h3_kernel(WWArgs a, const
                     // next rows in flight, staged mid-row into the buffers no row of this barrier reads
                     ld_dy(yr + 2 < y_end ? yr + 2 : y_end - 1);
                     ld_x(yr + 3 <= H ? yr + 3 : H);
-                    if (half == 0) row(yr, std::integral_constant<int, 0>{});
-                    else row(yr, std::integral_constant<int, 1>{});
+                    if (half == 0) row(yr, std::integral_constant<int, 0>{}, std::false_type{});
+                    else row(yr, std::integral_constant<int, 1>{}, std::false_type{});
                 }
             }
 #pragma unroll
