@@ -44,3 +44,34 @@ def test_record_pack_plan():
     ops._record_pack(w, "pack_dgrad", g, 4)
     assert sorted(k[0] for k in w._dcs_plan) == ["pack_dgrad", "pack_fwd"]
 
+
+
+def test_fixed_f16x3_layers_switch(monkeypatch):
+    """ops._fixed_mma: a stem / head kernel listed in _FIXED_F16X3 (env DUCOSY_F16X3_LAYERS at import) takes
+    f16x3 operands in the f16 mode, any other runs in the step's mode; the default list is empty since
+    round 6 (every layer on fp16 in config 5's mode)."""
+    import os
+    import subprocess
+    import sys
+    from modules.hip import lib, ops
+    prev = ops.get_mma()
+    try:
+        ops.set_mma("f16")
+        monkeypatch.setattr(ops, "_FIXED_F16X3", frozenset({"head"}))
+        assert ops._fixed_mma("head") == lib.MMA_F16X3
+        assert ops._fixed_mma("stem") == lib.MMA_F16
+        ops.set_mma("f16x3")
+        assert ops._fixed_mma("stem") == lib.MMA_F16X3
+    finally:
+        ops.set_mma(prev)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "from modules.hip import ops; print(','.join(sorted(ops._FIXED_F16X3)))"
+    for env, want in (("", ""), ("stem,stem_wgrad", "stem,stem_wgrad")):
+        e = dict(os.environ, DUCOSY_F16X3_LAYERS=env)
+        if env == "":
+            e.pop("DUCOSY_F16X3_LAYERS")
+        out = subprocess.run([sys.executable, "-c", code], cwd=os.path.join(root, "ducosy-gan_amd"), env=e,
+                             capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        lines = out.stdout.strip().splitlines()
+        assert (lines[-1] if lines else "") == want, out.stdout
