@@ -3102,6 +3102,10 @@ WgradPlan wgrad_plan(const dcs_conv_desc& d) {
 
 // conv_win.hip: the f16x3 window weight gradient of the residual 3x3 convs
 namespace dcs {
+#ifndef DCS_X6_F16_TAG3  // the f16 PatchGAN weight gradients on the LeakyReLU-prologue instance (TAG 3) as in f16x3,
+                         // not the generic one: bit-identical, f16 step 128.26 -> 127.73 ms (profiles/r06/ab/r06aq_*)
+#define DCS_X6_F16_TAG3 1
+#endif
 bool wgrad_win_check(const dcs_conv_desc& d);
 size_t wgrad_win_workspace_size(const dcs_conv_desc& d);
 int wgrad_win_launch(const dcs_conv_desc& d, const float* dy, const float* x, float* ws, hipStream_t s);
@@ -3212,6 +3216,7 @@ extern "C" int dcs_conv_wgrad(const dcs_conv_desc* dp, const float* dy, const fl
         } else if (d.mma == MMA_F16) {  // f16: the same pipeline, one product
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else if (plain) hipLaunchKernelGGL((conv_wgrad_x6_kernel<2, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
+            else if (lrelu && DCS_X6_F16_TAG3) hipLaunchKernelGGL((conv_wgrad_x6_kernel<3, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
             else hipLaunchKernelGGL((conv_wgrad_x6_kernel<0, MMA_F16>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
         } else if (d.mma == MMA_BF16 && DCS_BF16P) {  // half precision: one product, 48 pixels per barrier
             if (res) hipLaunchKernelGGL((conv_wgrad_x6_kernel<1, MMA_BF16P>), grid, dim3(NT), 0, s, d, dy, x, psc, psh, w, 2 * p.kt_per_split, gn, gm);
